@@ -1,0 +1,193 @@
+"""Headline benchmark: Mrays/s at 4096x4096, 1000 spheres, depth 8 (BASELINE.json).
+
+One step = one full pass of the hot path over one frame of the headline
+workload (config C3): every pixel's camera ray, its Phong
+shading with shadow rays to 2 point lights, and mirror bounces to depth 8,
+f64 arithmetic, f32 RGB + sRGB BGR written to HBM.  The scene is uploaded once
+(inputs resident in HBM before timing); output stays in HBM (the PCIe copy is
+reported separately in DESIGN.md, never in `value`).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+Multi-GPU: the frame's rows are dealt in 16-row bands round-robin over ranks
+(libraytrace/shard.py); no collective touches the data path.  Total work is
+fixed as N grows ("scaling": "strong").  value = rays of the whole frame x K /
+max-over-ranks wall time of the K timed steps.
+
+Rays = every Scene::intersect query the reference would issue (camera +
+reflection + shadow), counted by the kernel; identical to the oracle's count
+(tests/test_gpu_parity.py).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+FP64_VALU_PEAK_TFLOPS = 78.6   # spec, FMA counted; the kernel issues no FMA (parity), so ~39.3 is its ceiling
+BAND = 16
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--width", type=int, default=4096)
+    p.add_argument("--height", type=int, default=4096)
+    p.add_argument("--spheres", type=int, default=1000)
+    p.add_argument("--depth", type=int, default=8)
+    p.add_argument("--algo", default="auto", choices=["auto", "lds", "global"])
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def pmc_traffic(config_key):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        e = d.get(config_key)
+        return float(e["hbm_bytes_per_launch"]) if e else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(spec, args):
+    """Oracle (algorithmically the reference: same recursion, same linear scan,
+    f64) on the host, on a deterministic row sample of the same frame."""
+    from oracle import ref64
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    rows = 8
+    stride = max(1, spec.height // rows)
+    t0 = time.time()
+    r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads, want_rgb64=False)
+    dt = time.time() - t0
+    # scale the sample to ~cpu_seconds of work
+    want = max(rows, min(spec.height, int(rows * args.cpu_seconds / max(dt, 1e-3))))
+    if want > rows * 1.5:
+        rows = want
+        stride = max(1, spec.height // rows)
+        rows = spec.height // stride
+        t0 = time.time()
+        r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads,
+                         want_rgb64=False)
+        dt = time.time() - t0
+    return {"value": r["counts"]["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{rows} rows (every {stride}th) x {spec.width} px of the same frame; "
+                      f"{r['counts']['rays']} rays in {dt:.2f} s; oracle/ref64.c, f64, {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import libraytrace as lr
+    from libraytrace import scenes, shard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=3, name="c3")
+    W, H = spec.width, spec.height
+    ctx = lr.Context(local)
+    scene = lr.Scene.deserialize(spec.to_text())
+    ctx.upload(scene)
+    rows = shard.local_rows(H, BAND, world, rank)
+    tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, world) == rank else None
+    assert tail is None or len(tail) == 0, "bench frames are whole bands"
+    algo = {"auto": lr.RT_ALGO_AUTO, "lds": lr.RT_ALGO_BRUTE_LDS, "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
+    opts = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+                          max_depth=args.depth, spp=1, algo=algo,
+                          flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8)
+    pitch = 3 * W
+    out_rgb = torch.empty((len(rows), W, 3), dtype=torch.float32, device=dev)
+    out_bgr = torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.render_device(opts, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    st = ctx.stats()                       # rays of one frame-slice (deterministic: same every step)
+    local_rays = st.rays
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+
+    t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, avg_kernel_ms = mx[0].item(), mx[2].item()
+        total_rays = int(sm[1].item())
+    else:
+        total_rays = local_rays
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = total_rays * args.steps / elapsed / 1e6
+        pixels_local = len(rows) * W
+        scene_bytes = args.spheres * (32 + 4) + args.spheres * 128 + 2 * 56
+        algo_bytes = pixels_local * (12 + 3) + scene_bytes          # f32 RGB + u8 BGR writes + scene read once
+        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        key = f"c3_{W}x{H}_n{args.spheres}_d{args.depth}"
+        traffic = pmc_traffic(key)
+        line = {
+            "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"C3: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
+                                   f"depth {args.depth}, 1 spp centre jitter (seed 3)",
+                       "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth,
+                       "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}",
+                       "algo": args.algo},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "note": "VALU(f64)-bound path; HBM fraction reported because the metric asks for it"},
+        }
+        if world == 1 and not args.no_cpu:
+            try:
+                line["cpu_baseline"] = cpu_baseline(spec, args)
+            except Exception as e:  # the oracle is optional on a box where it was not built
+                line["cpu_baseline"] = {"value": None, "error": str(e)}
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+/*
+ * raytrace_amd.h -- C ABI of the MI355X-native per-pixel ray-tracing path.
+ *
+ * This is the drop-in boundary for j-dong/rust-raytrace's hot path.  The
+ * reference has no FFI of its own: its "operator API" is Rust trait objects
+ * (Shape / Material / LightModel / Background / Camera) called once per pixel
+ * sample from the serial loop in main.rs:45-57.  A per-sample FFI call is far
+ * too fine-grained for a GPU and `dyn` objects cannot cross a C ABI, so the
+ * boundary sits one level up: the host parses and flattens the Scene, and the
+ * library renders whole frames / tiles / row bands on one device.
+ *
+ * Entry point -> reference interface it replaces:
+ *   rt_scene_parse        serialize.rs:427-441   pub fn deserialize(&String) -> Result<Scene, SyntaxError>
+ *   rt_scene_from_desc    scene.rs:201-212       building a `Scene { objects, lights, camera, background, options }` in code
+ *   rt_camera_simple_new  camera.rs:51-63        SimplePerspectiveCamera::new
+ *   rt_camera_look_at     camera.rs:67-73        SimplePerspectiveCamera::look_at
+ *   rt_render / rt_render_device
+ *                         main.rs:39-57 + raytrace.rs:270-276 (raytrace) + raytrace.rs:261-267
+ *                         (ray_color) + raytrace.rs:30-67 (PhongMaterial::color) + scene.rs:247-249
+ *                         (Scene::intersect) + shapes.rs:50-112 (Sphere/Plane::intersect)
+ *   rt_to_srgb            color.rs:593-600       fn to_srgb (used by Color::write_bgr, color.rs:628-632)
+ *   rt_bmp_header         bmp.rs:10-61           pub fn write_header
+ *   rt_write_bmp          main.rs:34-59          header + bottom-up BGR rows to a file
+ *
+ * Conventions:
+ *   - Every function returns RT_OK (0) or a negative RT_E_* code.  No C++
+ *     exception or abort crosses the ABI.  rt_last_error() describes the last
+ *     failure of a context (thread-local text for context-free calls).
+ *   - All pointers are caller-owned; the library copies what it keeps.
+ *   - One rt_ctx per device; calls on one context are not thread-safe;
+ *     different contexts may be driven concurrently (one host thread per GPU).
+ *   - All scene arithmetic is IEEE f64 exactly as the reference (no FMA
+ *     contraction); output colours are the f64 result rounded once to f32,
+ *     and the u8 BGR bytes are quantised from the f64 value on the device.
+ *   - Pixel row 0 is the image BOTTOM (the first row written, main.rs:45/58).
+ */
+#ifndef RAYTRACE_AMD_H
+#define RAYTRACE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum rt_status {
+    RT_OK = 0,
+    RT_E_INVALID = -1,      /* bad argument */
+    RT_E_NODEVICE = -2,     /* no HIP device / bad device index */
+    RT_E_HIP = -3,          /* HIP runtime error (see rt_last_error) */
+    RT_E_NOMEM = -4,
+    RT_E_UNSUPPORTED = -5,  /* scene uses a class the device path does not implement yet */
+    RT_E_PARSE = -6,        /* scene text failed to parse (SyntaxError) */
+    RT_E_NOSCENE = -7,      /* render before upload */
+    RT_E_IO = -8
+};
+
+/* ---- scene model (flattened mirror of scene.rs / shapes.rs / camera.rs) ---- */
+enum rt_shape_kind { RT_SHAPE_SPHERE = 0, RT_SHAPE_PLANE = 1 };                 /* shapes.rs:42-112 */
+enum rt_material_kind {                                                          /* scene.rs:32-89 */
+    RT_MAT_PHONG = 0, RT_MAT_INDIRECT_PHONG = 1, RT_MAT_FRESNEL = 2, RT_MAT_TRANSPARENT = 3
+};
+enum rt_light_kind { RT_LIGHT_POINT = 0, RT_LIGHT_DIRECTIONAL = 1, RT_LIGHT_AREA = 2 };  /* scene.rs:117-155 */
+enum rt_camera_kind { RT_CAMERA_SIMPLE = 0, RT_CAMERA_DOF = 1 };                 /* camera.rs:29-123 */
+enum rt_background_kind { RT_BG_SOLID = 0, RT_BG_SKYBOX = 1 };                  /* scene.rs:164-188 */
+
+typedef struct { double r, g, b; } rt_color;                                     /* color.rs:15-22 */
+
+typedef struct {
+    int32_t shape;          /* rt_shape_kind */
+    int32_t material;       /* rt_material_kind */
+    double geom[6];         /* sphere: center x,y,z, radius   plane: point x,y,z, normal x,y,z */
+    rt_color diffuse;       /* Phong / IndirectPhong / Fresnel */
+    rt_color specular;
+    rt_color ambient;       /* Phong / IndirectPhong / Fresnel */
+    double exponent;
+    double ior;             /* Fresnel / Transparent */
+    uint32_t samples;       /* IndirectPhong */
+    uint32_t _pad;
+} rt_object;
+
+typedef struct {
+    int32_t kind;           /* rt_light_kind */
+    int32_t _pad;
+    double v[9];            /* point: location; directional: direction; area: origin, side1, side2 */
+    rt_color color;
+} rt_light;
+
+typedef struct {
+    int32_t kind;           /* rt_camera_kind */
+    uint32_t samples;       /* DepthOfFieldCamera samples (1 for simple) */
+    double position[3];     /* SimplePerspectiveCamera.position */
+    double matrix[9];       /* SimplePerspectiveCamera.matrix, row-major M[i][j] */
+    double focus, aperture; /* DepthOfFieldCamera */
+} rt_camera;
+
+typedef struct {
+    const rt_object* objects; uint32_t n_objects;
+    const rt_light* lights;   uint32_t n_lights;
+    rt_camera camera;
+    int32_t background_kind;  /* only RT_BG_SOLID is representable through a desc */
+    rt_color background;
+    uint32_t width, height, antialias;   /* scene.rs:191-198 Options */
+} rt_scene_desc;
+
+typedef struct rt_scene rt_scene;   /* host-side parsed scene (opaque) */
+typedef struct rt_ctx rt_ctx;       /* one device context (opaque) */
+
+/* ---- host-side scene API ---- */
+int rt_scene_parse(const char* text, size_t len, rt_scene** out, char* err, size_t err_len);
+int rt_scene_from_desc(const rt_scene_desc* desc, rt_scene** out);
+/* Borrow the flattened view of a scene (valid until rt_scene_free). */
+int rt_scene_get_desc(const rt_scene* scene, rt_scene_desc* out);
+void rt_scene_free(rt_scene* scene);
+
+int rt_camera_simple_new(const double position[3], const double look[3], const double up[3],
+                         double im_dist, rt_camera* out);
+int rt_camera_look_at(const double focus[3], const double look[3], const double up[3],
+                      double pov, double h, rt_camera* out);
+
+uint8_t rt_to_srgb(double v);
+/* Writes the 122-byte BITMAPV4 header; *bytewidth = padded row pitch. */
+int rt_bmp_header(uint8_t out[122], uint32_t width, uint32_t height, uint32_t* bytewidth);
+/* Writes header + pixel array (bgr rows, bottom-up, `pitch` bytes each) to `path`. */
+int rt_write_bmp(const char* path, uint32_t width, uint32_t height, const uint8_t* bgr, uint32_t pitch);
+
+/* ---- device API ---- */
+int rt_device_count(int* n);
+int rt_ctx_create(int device, rt_ctx** out);
+void rt_ctx_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+/* Copies the scene to HBM in the device layout.  Classes the device path does
+ * not implement -> RT_E_UNSUPPORTED. */
+int rt_scene_upload(rt_ctx* ctx, const rt_scene* scene);
+
+enum rt_jitter { RT_JITTER_CENTER = 0 };   /* jx = jy = 0.5 (deterministic parity mode, main.rs:51-52) */
+enum rt_out_flags { RT_OUT_RGB_F32 = 1, RT_OUT_BGR_U8 = 2 };
+enum rt_algo { RT_ALGO_AUTO = 0, RT_ALGO_BRUTE_LDS = 1, RT_ALGO_BRUTE_GLOBAL = 2 };
+
+typedef struct {
+    uint32_t width, height;   /* full frame: defines the pixel -> (-1,1) mapping (main.rs:39-41) */
+    uint32_t x0, tile_w;      /* columns [x0, x0 + tile_w) */
+    uint32_t y0, tile_h;      /* local row j -> global row y0 + ((j/band)*band_stride + band_phase)*band + j%band */
+    uint32_t band, band_stride, band_phase;   /* 0 -> 1: contiguous rows */
+    uint32_t max_depth;       /* reference MAX_DEPTH = 4 (raytrace.rs:18); <= RT_MAX_DEPTH_LIMIT */
+    uint32_t spp;             /* AA samples (Options.antialias); 0 -> scene's value */
+    int32_t jitter;           /* rt_jitter */
+    uint32_t flags;           /* rt_out_flags */
+    int32_t algo;             /* rt_algo */
+    uint32_t bgr_pitch;       /* bytes per output BGR row; 0 -> 3*tile_w */
+    uint32_t _pad;
+} rt_render_opts;
+
+#define RT_MAX_DEPTH_LIMIT 30
+
+typedef struct {
+    uint64_t rays;            /* every Scene::intersect query issued (camera + reflection + shadow) */
+    uint64_t shadow_rays;
+    uint64_t pixels;
+    double kernel_ms;         /* hipEvent time of the trace kernel */
+} rt_stats;
+
+void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height);
+
+/* Synchronous: renders into caller-owned HOST buffers (either may be NULL). */
+int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* out_bgr, rt_stats* stats);
+/* Asynchronous on `stream` (a hipStream_t; NULL = the context's own stream):
+ * renders into caller-owned DEVICE buffers.  Statistics of the most recent
+ * render are read with rt_ctx_stats (which synchronises). */
+int rt_render_device(rt_ctx* ctx, const rt_render_opts* opts, void* d_rgb, void* d_bgr, void* stream);
+int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,76 @@
+// Device (HBM) layout of a flattened scene.  Shared by the host upload code
+// and the HIP kernels.  All geometry stays f64: the reference computes in f64
+// (types.rs:11-25) and the self-intersection offset 1e-5 (raytrace.rs:43,62)
+// is below f32 resolution for |coordinates| >~ 5.
+#pragma once
+
+#include <cstdint>
+
+namespace rtamd {
+
+// One sphere = 32 B, read by every ray-sphere test (shapes.rs:60-65).  rr is
+// radius*radius computed once on the host with the same f64 multiply the
+// reference does per test, so it is bit-identical.
+struct alignas(16) DevSphere {
+    double cx, cy, cz, rr;
+};
+
+// Plane as in the file: normal NOT normalised (shapes.rs:100-112).
+struct DevPlane {
+    double px, py, pz, nx, ny, nz;
+};
+
+// Per OBJECT (indexed by file-order object id), only what shading reads.
+struct DevMaterial {
+    double kd[3], ks[3], amb[3];
+    double exponent;
+    double kd_sig, ks_sig;          // Color::significance, color.rs:637-639
+    double ior;
+    int32_t kind;                   // rt_material_kind
+    int32_t _pad;
+};
+
+struct DevLight {
+    double v[3];                    // point: location; directional: direction
+    double color[3];
+    int32_t kind;                   // rt_light_kind
+    int32_t _pad;
+};
+
+// One node of the sphere BVH (2 children, AABBs padded conservatively).
+struct alignas(16) DevBvhNode {
+    double lo[3], hi[3];
+    int32_t left;                   // >= 0: inner node, children left, left+1; < 0: leaf
+    int32_t first, count;           // leaf: sphere range [first, first+count)
+    int32_t _pad;
+};
+
+struct DevScene {
+    const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
+    const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
+    const DevPlane* planes;
+    const int32_t* plane_obj;
+    const DevMaterial* mats;        // indexed by object id
+    const DevLight* lights;
+    const DevBvhNode* bvh;          // null when no BVH was built
+    int32_t n_spheres, n_planes, n_lights, n_bvh;
+    double cam_pos[3];
+    double cam_m[9];                // row-major
+    double bg[3];
+};
+
+struct FrameParams {
+    double hw, hh, scale;           // main.rs:39-41
+    uint32_t x0, tile_w, y0, tile_h;
+    uint32_t band, band_stride, band_phase;
+    uint32_t max_depth, spp;
+    uint32_t bgr_pitch;
+    float* out_rgb;                 // tile_h * tile_w * 3, may be null
+    uint8_t* out_bgr;               // tile_h * bgr_pitch, may be null
+    unsigned long long* counters;   // [kCounterShards] rays, then [kCounterShards] shadow rays
+};
+
+constexpr int kCounterShards = 256;
+constexpr int kMaxLevels = 32;      // >= RT_MAX_DEPTH_LIMIT + 2
+
+}  // namespace rtamd

@@ -1,0 +1,314 @@
+// C ABI: device contexts, scene upload to HBM, frame/tile rendering.
+// See include/raytrace_amd.h for the contract and the reference interfaces
+// these replace.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "device_layout.hpp"
+#include "host_scene.hpp"
+
+namespace rtamd {
+hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
+hipError_t upload_srgb_table(const double* avg255);
+}  // namespace rtamd
+
+using namespace rtamd;
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    void* d_blob = nullptr;
+    size_t blob_bytes = 0;
+    DevScene dsc{};
+    bool has_scene = false;
+    unsigned long long* d_counters = nullptr;
+    float* d_rgb = nullptr;
+    size_t rgb_cap = 0;
+    uint8_t* d_bgr = nullptr;
+    size_t bgr_cap = 0;
+    uint64_t last_pixels = 0;
+    bool last_timed = false;
+    hipStream_t last_stream = nullptr;
+    std::string err;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    set_thread_error(msg);
+    return code;
+}
+
+int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
+    return fail(c, RT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(c, expr)                                            \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return hip_fail((c), _e, #expr);      \
+    } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+double significance(const rt_color& c) { return c.r + c.g + c.b; }   // color.rs:637-639
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int* n) {
+    if (!n) return RT_E_INVALID;
+    *n = 0;
+    int k = 0;
+    hipError_t e = hipGetDeviceCount(&k);
+    if (e != hipSuccess) { *n = 0; return RT_OK; }
+    *n = k;
+    return RT_OK;
+}
+
+int rt_ctx_create(int device, rt_ctx** out) {
+    if (!out) return RT_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(nullptr, RT_E_NODEVICE, "no HIP device " + std::to_string(device));
+    auto* c = new (std::nothrow) rt_ctx();
+    if (!c) return RT_E_NOMEM;
+    c->device = device;
+    auto cleanup = [&](int rc) { rt_ctx_destroy(c); return rc; };
+    if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, RT_E_HIP, "hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_counters, 2 * kCounterShards * sizeof(unsigned long long)) != hipSuccess ||
+        upload_srgb_table(srgb_average_table()) != hipSuccess)
+        return cleanup(fail(nullptr, RT_E_HIP, "context initialisation failed"));
+    *out = c;
+    return RT_OK;
+}
+
+void rt_ctx_destroy(rt_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_blob) (void)hipFree(c->d_blob);
+    if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_rgb) (void)hipFree(c->d_rgb);
+    if (c->d_bgr) (void)hipFree(c->d_bgr);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : thread_error(); }
+
+int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
+    if (!c || !s) return RT_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    // The device path implements the deterministic Phong chain;
+    // the stochastic and branching classes are "next" rows (§8(f)).
+    if (s->camera.kind != RT_CAMERA_SIMPLE)
+        return fail(c, RT_E_UNSUPPORTED, "DepthOfFieldCamera is not implemented on the device path");
+    if (s->background_kind != RT_BG_SOLID)
+        return fail(c, RT_E_UNSUPPORTED, "only SolidColorBackground is implemented on the device path");
+    std::vector<DevSphere> spheres;
+    std::vector<int32_t> sphere_obj, plane_obj;
+    std::vector<DevPlane> planes;
+    std::vector<DevMaterial> mats(s->objects.size());
+    std::vector<DevLight> lights;
+    for (size_t i = 0; i < s->objects.size(); ++i) {
+        const rt_object& o = s->objects[i];
+        if (o.material != RT_MAT_PHONG)
+            return fail(c, RT_E_UNSUPPORTED, "object " + std::to_string(i) + ": only PhongMaterial is implemented on the device path");
+        if (o.shape == RT_SHAPE_SPHERE) {
+            spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
+            sphere_obj.push_back(static_cast<int32_t>(i));
+        } else if (o.shape == RT_SHAPE_PLANE) {
+            planes.push_back(DevPlane{o.geom[0], o.geom[1], o.geom[2], o.geom[3], o.geom[4], o.geom[5]});
+            plane_obj.push_back(static_cast<int32_t>(i));
+        } else {
+            return fail(c, RT_E_INVALID, "object " + std::to_string(i) + ": bad shape kind");
+        }
+        DevMaterial& m = mats[i];
+        std::memset(&m, 0, sizeof m);
+        const rt_color* src[3] = {&o.diffuse, &o.specular, &o.ambient};
+        double* dst[3] = {m.kd, m.ks, m.amb};
+        for (int k = 0; k < 3; ++k) { dst[k][0] = src[k]->r; dst[k][1] = src[k]->g; dst[k][2] = src[k]->b; }
+        m.exponent = o.exponent;
+        m.kd_sig = significance(o.diffuse);
+        m.ks_sig = significance(o.specular);
+        m.ior = o.ior;
+        m.kind = o.material;
+    }
+    for (size_t i = 0; i < s->lights.size(); ++i) {
+        const rt_light& l = s->lights[i];
+        if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_DIRECTIONAL)
+            return fail(c, RT_E_UNSUPPORTED, "light " + std::to_string(i) + ": AreaLight is not implemented on the device path");
+        DevLight d{};
+        for (int k = 0; k < 3; ++k) d.v[k] = l.v[k];
+        d.color[0] = l.color.r; d.color[1] = l.color.g; d.color[2] = l.color.b;
+        d.kind = l.kind;
+        lights.push_back(d);
+    }
+    // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights], 256-B aligned pieces.
+    size_t off = 0;
+    auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
+    const size_t o_sph = place(spheres.size() * sizeof(DevSphere));
+    const size_t o_sobj = place(sphere_obj.size() * sizeof(int32_t));
+    const size_t o_pl = place(planes.size() * sizeof(DevPlane));
+    const size_t o_pobj = place(plane_obj.size() * sizeof(int32_t));
+    const size_t o_mat = place(mats.size() * sizeof(DevMaterial));
+    const size_t o_li = place(lights.size() * sizeof(DevLight));
+    const size_t total = off ? off : 256;
+    std::vector<uint8_t> host(total, 0);
+    auto put = [&](size_t at, const void* p, size_t bytes) { if (bytes) std::memcpy(host.data() + at, p, bytes); };
+    put(o_sph, spheres.data(), spheres.size() * sizeof(DevSphere));
+    put(o_sobj, sphere_obj.data(), sphere_obj.size() * sizeof(int32_t));
+    put(o_pl, planes.data(), planes.size() * sizeof(DevPlane));
+    put(o_pobj, plane_obj.data(), plane_obj.size() * sizeof(int32_t));
+    put(o_mat, mats.data(), mats.size() * sizeof(DevMaterial));
+    put(o_li, lights.data(), lights.size() * sizeof(DevLight));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
+    if (!c->d_blob) {
+        HIP_TRY(c, hipMalloc(&c->d_blob, total));
+        c->blob_bytes = total;
+    }
+    HIP_TRY(c, hipMemcpy(c->d_blob, host.data(), total, hipMemcpyHostToDevice));
+    auto* base = static_cast<uint8_t*>(c->d_blob);
+    DevScene& d = c->dsc;
+    d = DevScene{};
+    d.spheres = reinterpret_cast<const DevSphere*>(base + o_sph);
+    d.sphere_obj = reinterpret_cast<const int32_t*>(base + o_sobj);
+    d.planes = reinterpret_cast<const DevPlane*>(base + o_pl);
+    d.plane_obj = reinterpret_cast<const int32_t*>(base + o_pobj);
+    d.mats = reinterpret_cast<const DevMaterial*>(base + o_mat);
+    d.lights = reinterpret_cast<const DevLight*>(base + o_li);
+    d.bvh = nullptr;
+    d.n_spheres = static_cast<int32_t>(spheres.size());
+    d.n_planes = static_cast<int32_t>(planes.size());
+    d.n_lights = static_cast<int32_t>(lights.size());
+    d.n_bvh = 0;
+    for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
+    for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
+    d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;
+    c->has_scene = true;
+    return RT_OK;
+}
+
+static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_t& band, uint32_t& stride, uint32_t& pitch) {
+    if (!o) return fail(c, RT_E_INVALID, "null opts");
+    if (o->width == 0 || o->height == 0) return fail(c, RT_E_INVALID, "empty frame");
+    if (o->jitter != RT_JITTER_CENTER) return fail(c, RT_E_UNSUPPORTED, "only centre jitter is implemented on the device path");
+    if (o->max_depth > RT_MAX_DEPTH_LIMIT) return fail(c, RT_E_INVALID, "max_depth above RT_MAX_DEPTH_LIMIT");
+    band = o->band ? o->band : 1;
+    stride = o->band_stride ? o->band_stride : 1;
+    if (o->band_phase >= stride) return fail(c, RT_E_INVALID, "band_phase >= band_stride");
+    if (static_cast<uint64_t>(o->x0) + o->tile_w > o->width) return fail(c, RT_E_INVALID, "tile exceeds frame width");
+    if (o->tile_h) {
+        uint64_t j = o->tile_h - 1;
+        uint64_t last = o->y0 + ((j / band) * stride + o->band_phase) * band + j % band;
+        if (last >= o->height) return fail(c, RT_E_INVALID, "tile exceeds frame height");
+    }
+    spp = o->spp;
+    if (spp == 0) return fail(c, RT_E_INVALID, "spp must be set (the scene's antialias value for reference behaviour)");
+    pitch = o->bgr_pitch ? o->bgr_pitch : 3 * o->tile_w;
+    if (pitch < 3 * o->tile_w) return fail(c, RT_E_INVALID, "bgr_pitch < 3*tile_w");
+    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_BRUTE_GLOBAL) return fail(c, RT_E_INVALID, "bad algo");
+    return RT_OK;
+}
+
+int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
+    if (!c) return RT_E_INVALID;
+    if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
+    uint32_t spp, band, stride, pitch;
+    int rc = check_opts(c, o, spp, band, stride, pitch);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    FrameParams fp{};
+    fp.hw = static_cast<double>(o->width) / 2.0;              // main.rs:39-41
+    fp.hh = static_cast<double>(o->height) / 2.0;
+    fp.scale = std::fmax(1.0 / fp.hw, 1.0 / fp.hh);
+    fp.x0 = o->x0; fp.tile_w = o->tile_w; fp.y0 = o->y0; fp.tile_h = o->tile_h;
+    fp.band = band; fp.band_stride = stride; fp.band_phase = o->band_phase;
+    fp.max_depth = o->max_depth;
+    fp.spp = spp;
+    fp.bgr_pitch = pitch;
+    fp.out_rgb = (o->flags & RT_OUT_RGB_F32) ? static_cast<float*>(d_rgb) : nullptr;
+    fp.out_bgr = (o->flags & RT_OUT_BGR_U8) ? static_cast<uint8_t*>(d_bgr) : nullptr;
+    fp.counters = c->d_counters;
+    int mode = o->algo;
+    const size_t lds_bytes = static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere);
+    if (mode == RT_ALGO_AUTO) mode = lds_bytes <= 64 * 1024 ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL;
+    if (mode == RT_ALGO_BRUTE_LDS && lds_bytes > 160 * 1024)
+        return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 2 * kCounterShards * sizeof(unsigned long long), st));
+    c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
+    c->last_stream = st;
+    if (o->tile_w == 0 || o->tile_h == 0) { c->last_timed = false; return RT_OK; }
+    HIP_TRY(c, hipEventRecord(c->ev0, st));
+    HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
+    HIP_TRY(c, hipEventRecord(c->ev1, st));
+    c->last_timed = true;
+    return RT_OK;
+}
+
+int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
+    if (!c || !s) return RT_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    unsigned long long h[2 * kCounterShards];
+    if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+    HIP_TRY(c, hipMemcpyAsync(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::memset(s, 0, sizeof *s);
+    for (int i = 0; i < kCounterShards; ++i) { s->rays += h[i]; s->shadow_rays += h[kCounterShards + i]; }
+    s->pixels = c->last_pixels;
+    if (c->last_timed) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventSynchronize(c->ev1));
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        s->kernel_ms = ms;
+    }
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
+    if (!c || !o) return RT_E_INVALID;
+    uint32_t spp, band, stride, pitch;
+    int rc = check_opts(c, o, spp, band, stride, pitch);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    rt_render_opts oo = *o;
+    oo.flags = (out_rgb ? RT_OUT_RGB_F32 : 0) | (out_bgr ? RT_OUT_BGR_U8 : 0);
+    const size_t rgb_bytes = static_cast<size_t>(o->tile_w) * o->tile_h * 3 * sizeof(float);
+    const size_t bgr_bytes = static_cast<size_t>(pitch) * o->tile_h;
+    if (out_rgb && rgb_bytes > c->rgb_cap) {
+        if (c->d_rgb) (void)hipFree(c->d_rgb);
+        c->d_rgb = nullptr; c->rgb_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_rgb, rgb_bytes));
+        c->rgb_cap = rgb_bytes;
+    }
+    if (out_bgr && bgr_bytes > c->bgr_cap) {
+        if (c->d_bgr) (void)hipFree(c->d_bgr);
+        c->d_bgr = nullptr; c->bgr_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_bgr, bgr_bytes));
+        c->bgr_cap = bgr_bytes;
+    }
+    rc = rt_render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
+    if (rc != RT_OK) return rc;
+    if (out_rgb && rgb_bytes) HIP_TRY(c, hipMemcpyAsync(out_rgb, c->d_rgb, rgb_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (out_bgr && bgr_bytes) HIP_TRY(c, hipMemcpyAsync(out_bgr, c->d_bgr, bgr_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (stats) return rt_ctx_stats(c, stats);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,283 @@
+"""ctypes binding of librtamd.so (include/raytrace_amd.h) for tests and bench.
+
+The product is the C ABI + HIP kernels; this module is plumbing that lets the
+pytest suite and bench.py drive it.  The names mirror the reference crate
+`libraytrace` (Cargo.toml [lib] name): `Scene` (scene.rs:201), `deserialize`
+(serialize.rs:427), `Context.render` (the pixel loop of main.rs:45-57),
+`to_srgb` (color.rs:593), `bmp_header` (bmp.rs:10).
+
+There is NO CPU fallback: if librtamd.so cannot be loaded the import fails,
+and device calls without a GPU raise RtError.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "librtamd.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "raytrace_amd.h")
+
+RT_OK = 0
+RT_E_INVALID, RT_E_NODEVICE, RT_E_HIP, RT_E_NOMEM = -1, -2, -3, -4
+RT_E_UNSUPPORTED, RT_E_PARSE, RT_E_NOSCENE, RT_E_IO = -5, -6, -7, -8
+RT_SHAPE_SPHERE, RT_SHAPE_PLANE = 0, 1
+RT_MAT_PHONG, RT_MAT_INDIRECT_PHONG, RT_MAT_FRESNEL, RT_MAT_TRANSPARENT = 0, 1, 2, 3
+RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AREA = 0, 1, 2
+RT_CAMERA_SIMPLE, RT_CAMERA_DOF = 0, 1
+RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
+RT_OUT_RGB_F32, RT_OUT_BGR_U8 = 1, 2
+RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL = 0, 1, 2
+RT_MAX_DEPTH_LIMIT = 30
+
+
+class RtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rt error {code}: {msg}")
+        self.code = code
+
+
+class rt_color(C.Structure):
+    _fields_ = [("r", C.c_double), ("g", C.c_double), ("b", C.c_double)]
+
+
+class rt_object(C.Structure):
+    _fields_ = [("shape", C.c_int32), ("material", C.c_int32), ("geom", C.c_double * 6),
+                ("diffuse", rt_color), ("specular", rt_color), ("ambient", rt_color),
+                ("exponent", C.c_double), ("ior", C.c_double), ("samples", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class rt_light(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("_pad", C.c_int32), ("v", C.c_double * 9), ("color", rt_color)]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("samples", C.c_uint32), ("position", C.c_double * 3),
+                ("matrix", C.c_double * 9), ("focus", C.c_double), ("aperture", C.c_double)]
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("objects", C.POINTER(rt_object)), ("n_objects", C.c_uint32),
+                ("lights", C.POINTER(rt_light)), ("n_lights", C.c_uint32),
+                ("camera", rt_camera), ("background_kind", C.c_int32), ("background", rt_color),
+                ("width", C.c_uint32), ("height", C.c_uint32), ("antialias", C.c_uint32)]
+
+
+class rt_render_opts(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("x0", C.c_uint32), ("tile_w", C.c_uint32),
+                ("y0", C.c_uint32), ("tile_h", C.c_uint32), ("band", C.c_uint32), ("band_stride", C.c_uint32),
+                ("band_phase", C.c_uint32), ("max_depth", C.c_uint32), ("spp", C.c_uint32),
+                ("jitter", C.c_int32), ("flags", C.c_uint32), ("algo", C.c_int32),
+                ("bgr_pitch", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `make -C rust-raytrace_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    sig = {
+        "rt_scene_parse": (C.c_int, [C.c_char_p, C.c_size_t, P(C.c_void_p), C.c_char_p, C.c_size_t]),
+        "rt_scene_from_desc": (C.c_int, [P(rt_scene_desc), P(C.c_void_p)]),
+        "rt_scene_get_desc": (C.c_int, [C.c_void_p, P(rt_scene_desc)]),
+        "rt_scene_free": (None, [C.c_void_p]),
+        "rt_camera_simple_new": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double), C.c_double, P(rt_camera)]),
+        "rt_camera_look_at": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double), C.c_double, C.c_double,
+                                        P(rt_camera)]),
+        "rt_to_srgb": (C.c_uint8, [C.c_double]),
+        "rt_bmp_header": (C.c_int, [P(C.c_uint8), C.c_uint32, C.c_uint32, P(C.c_uint32)]),
+        "rt_write_bmp": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_uint8), C.c_uint32]),
+        "rt_device_count": (C.c_int, [P(C.c_int)]),
+        "rt_ctx_create": (C.c_int, [C.c_int, P(C.c_void_p)]),
+        "rt_ctx_destroy": (None, [C.c_void_p]),
+        "rt_last_error": (C.c_char_p, [C.c_void_p]),
+        "rt_scene_upload": (C.c_int, [C.c_void_p, C.c_void_p]),
+        "rt_render_opts_default": (None, [P(rt_render_opts), C.c_uint32, C.c_uint32]),
+        "rt_render": (C.c_int, [C.c_void_p, P(rt_render_opts), P(C.c_float), P(C.c_uint8), P(rt_stats)]),
+        "rt_render_device": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_void_p, C.c_void_p, C.c_void_p]),
+        "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _err(ctx=None):
+    m = lib.rt_last_error(ctx)
+    return m.decode(errors="replace") if m else ""
+
+
+def _check(rc, ctx=None):
+    if rc != RT_OK:
+        raise RtError(rc, _err(ctx))
+
+
+def _d3(v):
+    return (C.c_double * 3)(*[float(x) for x in v])
+
+
+def camera_simple_new(position, look, up, im_dist):
+    """camera.rs:51-63"""
+    cam = rt_camera()
+    _check(lib.rt_camera_simple_new(_d3(position), _d3(look), _d3(up), float(im_dist), C.byref(cam)))
+    return cam
+
+
+def camera_look_at(focus, look, up, pov, h):
+    """camera.rs:67-73"""
+    cam = rt_camera()
+    _check(lib.rt_camera_look_at(_d3(focus), _d3(look), _d3(up), float(pov), float(h), C.byref(cam)))
+    return cam
+
+
+def to_srgb(v):
+    """color.rs:593-600"""
+    return lib.rt_to_srgb(float(v))
+
+
+def bmp_header(width, height):
+    """bmp.rs:10-61 -> (122 header bytes, bytewidth)"""
+    buf = (C.c_uint8 * 122)()
+    bw = C.c_uint32()
+    _check(lib.rt_bmp_header(buf, width, height, C.byref(bw)))
+    return bytes(buf), bw.value
+
+
+def write_bmp(path, width, height, bgr, pitch):
+    arr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    _check(lib.rt_write_bmp(path.encode(), width, height, arr.ctypes.data_as(C.POINTER(C.c_uint8)), pitch))
+
+
+class Scene:
+    """A parsed / built scene (scene.rs:201-212), owned by the C library."""
+
+    def __init__(self, handle):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def deserialize(cls, text):
+        """serialize.rs:427: parse scene text, raising RtError(RT_E_PARSE, "row:col: ...")."""
+        raw = text.encode() if isinstance(text, str) else bytes(text)
+        h = C.c_void_p()
+        err = C.create_string_buffer(512)
+        rc = lib.rt_scene_parse(raw, len(raw), C.byref(h), err, 512)
+        if rc != RT_OK:
+            raise RtError(rc, err.value.decode(errors="replace"))
+        return cls(h.value)
+
+    @classmethod
+    def from_desc(cls, desc):
+        h = C.c_void_p()
+        _check(lib.rt_scene_from_desc(C.byref(desc), C.byref(h)))
+        return cls(h.value)
+
+    def desc(self):
+        d = rt_scene_desc()
+        _check(lib.rt_scene_get_desc(self._h, C.byref(d)))
+        d._owner = self          # the desc borrows the scene's arrays: keep the scene alive
+        return d
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib.rt_scene_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count():
+    n = C.c_int(0)
+    lib.rt_device_count(C.byref(n))
+    return n.value
+
+
+def render_opts(width, height, **kw):
+    o = rt_render_opts()
+    lib.rt_render_opts_default(C.byref(o), width, height)
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise TypeError(f"unknown render option {k}")
+        setattr(o, k, v)
+    return o
+
+
+class Context:
+    """One device (rt_ctx).  Mirrors the reference's main.rs render step."""
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        _check(lib.rt_ctx_create(device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def upload(self, scene):
+        _check(lib.rt_scene_upload(self._h, scene.handle), self._h)
+
+    def render(self, opts, rgb=True, bgr=True):
+        """Synchronous render of opts' tile into host numpy arrays.
+        Returns (rgb float32 [tile_h, tile_w, 3] or None, bgr uint8 [tile_h, pitch] or None, stats)."""
+        pitch = opts.bgr_pitch or 3 * opts.tile_w
+        out_rgb = np.zeros((opts.tile_h, opts.tile_w, 3), np.float32) if rgb else None
+        out_bgr = np.full((opts.tile_h, pitch), 0xCD, np.uint8) if bgr else None
+        st = rt_stats()
+        rc = lib.rt_render(self._h, C.byref(opts),
+                           out_rgb.ctypes.data_as(C.POINTER(C.c_float)) if rgb else None,
+                           out_bgr.ctypes.data_as(C.POINTER(C.c_uint8)) if bgr else None,
+                           C.byref(st))
+        _check(rc, self._h)
+        return out_rgb, out_bgr, st
+
+    def render_device(self, opts, d_rgb_ptr, d_bgr_ptr, stream_ptr=None):
+        """Asynchronous render into device buffers (raw pointers, e.g. torch tensor.data_ptr())."""
+        _check(lib.rt_render_device(self._h, C.byref(opts), C.c_void_p(d_rgb_ptr or 0),
+                                    C.c_void_p(d_bgr_ptr or 0), C.c_void_p(stream_ptr or 0)), self._h)
+
+    def stats(self):
+        st = rt_stats()
+        _check(lib.rt_ctx_stats(self._h, C.byref(st)), self._h)
+        return st
+
+    def close(self):
+        if self._h:
+            lib.rt_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def header_functions():
+    """Names of every function include/raytrace_amd.h declares (for the export test)."""
+    import re
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(rt_[a-z_0-9]+)\s*\(", text, flags=re.M)))

@@ -1,0 +1,200 @@
+"""Scene specifications and the seeded synthetic-scene generators.
+
+A SceneSpec is plain Python data.  It can be emitted as text in the reference's
+own scene grammar (serialize.rs:606-814) -- that text is what the product path
+parses -- and converted to the oracle's structs by oracle/ref64.py, so the two
+paths share nothing but these numbers.  Floats are written with repr(), which
+round-trips exactly through the reference's f64::from_str (and our parser).
+
+Configs (BASELINE.json "configs"):
+  C1 test_scene.txt (IndirectPhong Cornell box; oracle-only, statistical)
+  C2 1920x1080, 8 spheres + 1 plane + 2 point lights, depth 4
+  C3 4096x4096, 1000 random spheres, 2 point lights, depth 8   <- headline
+  C4 8192x8192, 10k spheres, depth 8
+  C5 16384x16384, 100k spheres, depth 16
+Random numbers come from splitmix64 so the scenes are identical on every
+machine and numpy version.
+"""
+import colorsys
+import math
+from dataclasses import dataclass, field
+
+
+def _f(x):
+    x = float(x)
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "inf" if x > 0 else "-inf"
+    return repr(x)
+
+
+def _t(v):
+    return "(" + ", ".join(_f(x) for x in v) + ")"
+
+
+def _rgb(v):
+    return "rgb" + _t(v)
+
+
+@dataclass
+class SceneSpec:
+    objects: list = field(default_factory=list)
+    lights: list = field(default_factory=list)
+    camera: dict = field(default_factory=dict)
+    background: tuple = (0.0, 0.0, 0.0)
+    width: int = 64
+    height: int = 64
+    antialias: int = 1
+    max_depth: int = 4          # not part of the file format (raytrace.rs:18 is a constant)
+    name: str = "scene"
+
+    # ---- builders ----
+    def sphere(self, center, radius, material):
+        self.objects.append({"shape": "sphere", "center": tuple(center), "radius": float(radius), "material": material})
+        return self
+
+    def plane(self, point, normal, material):
+        self.objects.append({"shape": "plane", "point": tuple(point), "normal": tuple(normal), "material": material})
+        return self
+
+    def point_light(self, location, color):
+        self.lights.append({"kind": "point", "location": tuple(location), "color": tuple(color)})
+        return self
+
+    def directional_light(self, direction, color):
+        self.lights.append({"kind": "directional", "direction": tuple(direction), "color": tuple(color)})
+        return self
+
+    # ---- reference grammar ----
+    def to_text(self):
+        out = ["{", "    objects: ["]
+        for o in self.objects:
+            out.append("        {")
+            if o["shape"] == "sphere":
+                out.append(f"            bounds: Sphere {{ center: {_t(o['center'])} radius: {_f(o['radius'])} }}")
+            else:
+                out.append(f"            bounds: Plane {{ point: {_t(o['point'])} normal: {_t(o['normal'])} }}")
+            out.append("            material: " + _material_text(o["material"]))
+            out.append("        }")
+        out.append("    ]")
+        out.append("    lights: [")
+        for L in self.lights:
+            if L["kind"] == "point":
+                model = f"PointLight {{ location: {_t(L['location'])} }}"
+            elif L["kind"] == "directional":
+                model = f"DirectionalLight {{ direction: {_t(L['direction'])} }}"
+            else:
+                model = (f"AreaLight {{ origin: {_t(L['origin'])} side1: {_t(L['side1'])} "
+                         f"side2: {_t(L['side2'])} }}")
+            out.append(f"        {{ model: {model} color: {_rgb(L['color'])} }}")
+        out.append("    ]")
+        cam = self.camera
+        if cam.get("ctor", "new") == "new":
+            inner = (f"new({_t(cam['position'])}, {_t(cam['look'])}, {_t(cam['up'])}, {_f(cam['im_dist'])})")
+        else:
+            inner = (f"look_at({_t(cam['focus'])}, {_t(cam['look'])}, {_t(cam['up'])}, "
+                     f"{_f(cam['pov'])} rad, {_f(cam['h'])})")
+        if cam.get("dof"):
+            out.append(f"    camera: DepthOfFieldCamera new({inner}, {_f(cam['focus_dist'])}, "
+                       f"{_f(cam['aperture'])}, {int(cam['samples'])})")
+        else:
+            out.append(f"    camera: SimplePerspectiveCamera {inner}")
+        out.append(f"    background: SolidColorBackground {{ color: {_rgb(self.background)} }}")
+        out.append(f"    options: {{ width: {self.width} height: {self.height} antialias: {self.antialias} }}")
+        out.append("}")
+        return "\n".join(out) + "\n"
+
+
+def phong(diffuse, specular, exponent, ambient):
+    return {"kind": "phong", "diffuse": tuple(diffuse), "specular": tuple(specular),
+            "exponent": float(exponent), "ambient": tuple(ambient)}
+
+
+def _material_text(m):
+    k = m["kind"]
+    if k == "phong":
+        return (f"PhongMaterial {{ diffuse: {_rgb(m['diffuse'])} specular: {_rgb(m['specular'])} "
+                f"exponent: {_f(m['exponent'])} ambient: {_rgb(m['ambient'])} }}")
+    if k == "indirect_phong":
+        return (f"IndirectPhongMaterial {{ diffuse: {_rgb(m['diffuse'])} specular: {_rgb(m['specular'])} "
+                f"exponent: {_f(m['exponent'])} ambient: {_rgb(m['ambient'])} samples: {int(m['samples'])} }}")
+    if k == "fresnel":
+        return (f"FresnelMaterial {{ diffuse: {_rgb(m['diffuse'])} specular: {_rgb(m['specular'])} "
+                f"exponent: {_f(m['exponent'])} ambient: {_rgb(m['ambient'])} ior: {_f(m['ior'])} }}")
+    if k == "transparent":
+        return (f"TransparentMaterial {{ specular: {_rgb(m['specular'])} exponent: {_f(m['exponent'])} "
+                f"ior: {_f(m['ior'])} }}")
+    raise ValueError(k)
+
+
+class SplitMix64:
+    def __init__(self, seed):
+        self.s = seed & 0xFFFFFFFFFFFFFFFF
+
+    def next(self):
+        self.s = (self.s + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        return z ^ (z >> 31)
+
+    def uniform(self, lo, hi):
+        return lo + (hi - lo) * ((self.next() >> 11) * (1.0 / 9007199254740992.0))
+
+
+DEFAULT_CAMERA = {"ctor": "new", "position": (0.0, 3.0, 10.0), "look": (0.0, -0.2, -1.0),
+                  "up": (0.0, 1.0, 0.0), "im_dist": 1.5}
+
+
+def _lights(spec):
+    spec.point_light((-10.0, 10.0, 5.0), (0.8, 0.8, 0.8))
+    spec.point_light((10.0, 8.0, 0.0), (0.6, 0.6, 0.6))
+
+
+def config2(width=1920, height=1080):
+    """C2: 8 spheres in a ring + ground plane + 2 point lights, depth 4 (= MAX_DEPTH)."""
+    s = SceneSpec(width=width, height=height, antialias=1, max_depth=4, name="c2",
+                  camera=dict(DEFAULT_CAMERA), background=(0.05, 0.05, 0.05))
+    for i in range(8):
+        a = 2.0 * math.pi * i / 8.0
+        kd = colorsys.hsv_to_rgb(i / 8.0, 0.7, 0.9)
+        s.sphere((4.0 * math.cos(a), 1.0, -6.0 + 4.0 * math.sin(a)), 1.0,
+                 phong(kd, (0.3, 0.3, 0.3), 32.0, tuple(0.02 * c for c in kd)))
+    s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), phong((0.6, 0.6, 0.6), (0.1, 0.1, 0.1), 16.0, (0.01, 0.01, 0.01)))
+    _lights(s)
+    return s
+
+
+def random_spheres(n, width, height, max_depth, seed, box_scale=1.0, name="rand", plane=False):
+    """C3/C4/C5 generator: centres U(x in [-8,8], y in [0.3,6], z in [-16,-2]) scaled by
+    box_scale about (0, 0.3, -2); r in U[0.1,0.6]; Phong kd in U[0.1,0.9]^3,
+    ks = s*(1,1,1) with s in U[0.05,0.4], exponent in U[8,128], ambient = 0.02*kd."""
+    rng = SplitMix64(seed)
+    s = SceneSpec(width=width, height=height, antialias=1, max_depth=max_depth, name=name,
+                  camera=dict(DEFAULT_CAMERA), background=(0.05, 0.05, 0.05))
+    for _ in range(n):
+        cx = rng.uniform(-8.0, 8.0) * box_scale
+        cy = 0.3 + rng.uniform(0.0, 5.7) * box_scale
+        cz = -2.0 - rng.uniform(0.0, 14.0) * box_scale
+        r = rng.uniform(0.1, 0.6)
+        kd = (rng.uniform(0.1, 0.9), rng.uniform(0.1, 0.9), rng.uniform(0.1, 0.9))
+        ks = rng.uniform(0.05, 0.4)
+        ex = rng.uniform(8.0, 128.0)
+        s.sphere((cx, cy, cz), r, phong(kd, (ks, ks, ks), ex, tuple(0.02 * c for c in kd)))
+    if plane:
+        s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), phong((0.5, 0.5, 0.5), (0.2, 0.2, 0.2), 24.0, (0.01, 0.01, 0.01)))
+    _lights(s)
+    return s
+
+
+def config3(width=4096, height=4096, n=1000):
+    return random_spheres(n, width, height, 8, seed=3, name="c3")
+
+
+def config4(width=8192, height=8192, n=10000):
+    return random_spheres(n, width, height, 8, seed=4, box_scale=10.0 ** (1.0 / 3.0), name="c4")
+
+
+def config5(width=16384, height=16384, n=100000):
+    return random_spheres(n, width, height, 16, seed=5, box_scale=100.0 ** (1.0 / 3.0), name="c5")

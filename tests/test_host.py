@@ -1,0 +1,199 @@
+"""Host-side product code (no GPU): C-ABI exports, the scene parser
+(serialize.rs grammar), cameras (camera.rs), sRGB quantiser (color.rs) and BMP
+writer (bmp.rs) -- each checked against the oracle / the reference's goldens."""
+import ctypes as C
+import json
+import math
+import os
+import random
+
+import numpy as np
+import pytest
+
+import libraytrace as lr
+from libraytrace import scenes
+from oracle import ref64
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_library_exports_every_header_symbol():
+    names = lr.header_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lr.lib, n), n
+
+
+def test_abi_struct_sizes_match_header():
+    # ctypes mirrors must agree with the C layout (checked through the library's own writers)
+    assert C.sizeof(lr.rt_object) == 4 + 4 + 48 + 72 + 8 + 8 + 4 + 4
+    assert C.sizeof(lr.rt_render_opts) == 16 * 4
+
+
+def test_parse_reference_test_scene():
+    text = open(os.path.join(GOLD, "test_scene.txt")).read()
+    sc = lr.Scene.deserialize(text)
+    d = sc.desc()
+    assert (d.width, d.height, d.antialias) == (800, 800, 1024)
+    assert d.n_objects == 7 and d.n_lights == 0
+    kinds = [d.objects[i].shape for i in range(7)]
+    assert kinds == [lr.RT_SHAPE_PLANE] * 5 + [lr.RT_SHAPE_SPHERE] * 2
+    assert all(d.objects[i].material == lr.RT_MAT_INDIRECT_PHONG for i in range(7))
+    assert tuple(d.objects[6].geom[:4]) == (0.0, 10.65, 0.0, 5.0)
+    assert (d.objects[6].ambient.r, d.objects[6].samples) == (5.0, 1)
+    assert tuple(d.objects[3].geom) == (-3.0, 0.0, 0.0, 1.0, 0.0, 0.0)
+    assert (d.background.r, d.background.g, d.background.b) == (0.051, 0.051, 0.051)
+    pos, m = ref64.camera_build({"ctor": "new", "position": (0, 3, 17), "look": (0, 0, -1),
+                                 "up": (0, 1, 0), "im_dist": 3.6})
+    assert tuple(d.camera.position) == pos
+    assert tuple(d.camera.matrix) == m
+
+
+def _desc_matches_spec(d, spec):
+    assert d.n_objects == len(spec.objects)
+    for i, o in enumerate(spec.objects):
+        g = d.objects[i]
+        if o["shape"] == "sphere":
+            assert g.shape == lr.RT_SHAPE_SPHERE
+            assert tuple(g.geom[:4]) == tuple(o["center"]) + (o["radius"],)
+        else:
+            assert g.shape == lr.RT_SHAPE_PLANE
+            assert tuple(g.geom) == tuple(o["point"]) + tuple(o["normal"])
+        m = o["material"]
+        assert (g.diffuse.r, g.diffuse.g, g.diffuse.b) == tuple(m["diffuse"])
+        assert (g.specular.r, g.specular.g, g.specular.b) == tuple(m["specular"])
+        assert (g.ambient.r, g.ambient.g, g.ambient.b) == tuple(m["ambient"])
+        assert g.exponent == m["exponent"]
+    assert d.n_lights == len(spec.lights)
+
+
+def test_generated_scene_text_round_trips_bit_exactly():
+    spec = scenes.random_spheres(200, 64, 48, 8, seed=99, plane=True)
+    sc = lr.Scene.deserialize(spec.to_text())
+    _desc_matches_spec(sc.desc(), spec)
+    spec2 = scenes.config2(96, 54)
+    _desc_matches_spec(lr.Scene.deserialize(spec2.to_text()).desc(), spec2)
+
+
+def test_parser_grammar_features():
+    text = """
+    # hash comment
+    {
+        // fields in any order, repeated field: last wins
+        options: { width: 1 height: 1 antialias: 7 }
+        options: { antialias: 2.4 height: 3 width: 4 }
+        /* block
+           comment */ background: SolidColorBackground { color: rgb(0.1, +2, -3e-1) }
+        camera: SimplePerspectiveCamera look_at((0, 1, 2), (0, 0, -1), (0, 1, 0), 90 deg, 2)
+        lights: [
+            { model: DirectionalLight { direction: (0, -1, 0) } color: rgb(1, 1, 1) }
+            { color: rgb(0.5, 0.5, 0.5) model: PointLight { location: (1, 2, 3) } }
+        ]
+        objects: [
+            { bounds: Sphere { radius: 0.5 center: (1, 2, 3) }
+              material: FresnelMaterial { diffuse: rgb(1,1,1) specular: rgb(0,0,0) exponent: 1 ambient: rgb(0,0,0) ior: 1.5 } }
+            { bounds: Plane { point: (0, 0, 0) normal: (0, 1, 0) }
+              material: TransparentMaterial { specular: rgb(1,1,1) exponent: 2 ior: 1.33 } }
+        ]
+    }
+    trailing garbage after the scene is never read @@@
+    """
+    d = lr.Scene.deserialize(text).desc()
+    assert (d.width, d.height, d.antialias) == (4, 3, 2)
+    assert (d.background.r, d.background.g, d.background.b) == (0.1, 2.0, -0.3)
+    assert d.n_lights == 2 and d.lights[0].kind == lr.RT_LIGHT_DIRECTIONAL and d.lights[1].kind == lr.RT_LIGHT_POINT
+    assert d.objects[0].material == lr.RT_MAT_FRESNEL and d.objects[0].ior == 1.5
+    assert d.objects[1].material == lr.RT_MAT_TRANSPARENT and d.objects[1].ior == 1.33
+    pos, m = ref64.camera_build({"ctor": "look_at", "focus": (0, 1, 2), "look": (0, 0, -1), "up": (0, 1, 0),
+                                 "pov": 90 * math.pi / 180.0, "h": 2})
+    assert tuple(d.camera.position) == pos and tuple(d.camera.matrix) == m
+
+
+def test_depth_of_field_camera_parses():
+    spec = scenes.config2(8, 8)
+    spec.camera = dict(spec.camera, dof=True, focus_dist=7.5, aperture=0.1, samples=16)
+    d = lr.Scene.deserialize(spec.to_text()).desc()
+    assert d.camera.kind == lr.RT_CAMERA_DOF and d.camera.samples == 16
+    assert (d.camera.focus, d.camera.aperture) == (7.5, 0.1)
+
+
+@pytest.mark.parametrize("text,code,needle", [
+    ("{ bogus: 1 }", lr.RT_E_PARSE, "undefined field: bogus"),
+    ("{ objects: [] lights: [] }", lr.RT_E_PARSE, "missing"),
+    ("{ objects: [ @ ] }", lr.RT_E_PARSE, "invalid token"),
+    ("{ objects: [] lights: [] options: { width: 1.2.3", lr.RT_E_PARSE, "invalid number"),
+    ("{ objects: [ { bounds: Cube { } } ] }", lr.RT_E_PARSE, "no such class: Cube"),
+    ("{ objects: [", lr.RT_E_PARSE, "end of file"),
+    ("{ background: SkyboxBackground { } }", lr.RT_E_UNSUPPORTED, "Skybox"),
+    ("{ /* never closed ", lr.RT_E_PARSE, "unterminated"),
+    ("{ objects: [ { bounds: Sphere { center: (1 2 3) radius: 1 } } ] }", lr.RT_E_PARSE, "expected Comma"),
+])
+def test_parser_errors(text, code, needle):
+    with pytest.raises(lr.RtError) as e:
+        lr.Scene.deserialize(text)
+    assert e.value.code == code
+    assert needle in str(e.value)
+    assert ":" in str(e.value).split(": ", 1)[1]      # "row:col: message"
+
+
+def test_u32_rounding_rules():
+    spec = scenes.config2(4, 4)
+    text = spec.to_text().replace("antialias: 1", "antialias: -3")
+    assert lr.Scene.deserialize(text).desc().antialias == 0      # negative -> 0 (serialize.rs:463-465)
+    text = spec.to_text().replace("antialias: 1", "antialias: 2.5")
+    assert lr.Scene.deserialize(text).desc().antialias == 3      # f64::round, half away from zero
+
+
+def test_camera_builders_match_oracle():
+    rnd = random.Random(5)
+    for _ in range(50):
+        p = [rnd.uniform(-10, 10) for _ in range(3)]
+        lk = [rnd.uniform(-1, 1) for _ in range(3)]
+        up = [rnd.uniform(-1, 1) for _ in range(3)]
+        im = rnd.uniform(0.5, 4)
+        cam = lr.camera_simple_new(p, lk, up, im)
+        pos, m = ref64.camera_build({"ctor": "new", "position": p, "look": lk, "up": up, "im_dist": im})
+        assert tuple(cam.position) == pos and tuple(cam.matrix) == m
+        pov, h = rnd.uniform(0.2, 2.5), rnd.uniform(0.5, 5)
+        cam = lr.camera_look_at(p, lk, up, pov, h)
+        pos, m = ref64.camera_build({"ctor": "look_at", "focus": p, "look": lk, "up": up, "pov": pov, "h": h})
+        assert tuple(cam.position) == pos and tuple(cam.matrix) == m
+
+
+def test_srgb_quantiser_matches_reference_tables():
+    t = json.load(open(os.path.join(GOLD, "srgb_tables.json")))
+    avg = [float.fromhex(x) for x in t["SRGB_AVERAGE"]]
+    for i in range(255):
+        assert lr.to_srgb(avg[i]) == i + 1
+        assert lr.to_srgb(math.nextafter(avg[i], -math.inf)) == i
+    rnd = np.random.default_rng(0)
+    vals = np.concatenate([rnd.uniform(-0.1, 1.2, 20000), [float("nan"), float("inf"), -float("inf"), 0.0, -0.0]])
+    for v in vals:
+        assert lr.to_srgb(v) == ref64.to_srgb(v)
+
+
+def test_bmp_header_and_file(tmp_path):
+    gold = bytes.fromhex(open(os.path.join(GOLD, "out_bmp_header.hex")).read().strip())
+    hdr, bw = lr.bmp_header(800, 800)
+    assert hdr == gold and bw == 2400
+    for w, h in [(1, 1), (2, 3), (801, 5), (1920, 1080)]:
+        assert lr.bmp_header(w, h) == ref64.bmp_header(w, h)
+    w, h = 5, 3
+    pitch = (3 * w + 3) & ~3
+    rows = np.arange(h * 3 * w, dtype=np.uint8).reshape(h, 3 * w)
+    p = str(tmp_path / "x.bmp")
+    lr.write_bmp(p, w, h, rows, 3 * w)
+    data = open(p, "rb").read()
+    assert data[:122] == lr.bmp_header(w, h)[0]
+    assert len(data) == 122 + pitch * h
+    for y in range(h):
+        assert data[122 + y * pitch:122 + y * pitch + 3 * w] == rows[y].tobytes()
+        assert data[122 + y * pitch + 3 * w:122 + (y + 1) * pitch] == b"\0" * (pitch - 3 * w)
+
+
+def test_device_calls_fail_loudly_without_gpu():
+    if lr.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(lr.RtError) as e:
+        lr.Context(0)
+    assert e.value.code == lr.RT_E_NODEVICE

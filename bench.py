@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--height", type=int, default=4096)
     p.add_argument("--spheres", type=int, default=1000)
     p.add_argument("--depth", type=int, default=8)
-    p.add_argument("--algo", default="auto", choices=["auto", "lds", "global"])
+    p.add_argument("--algo", default="auto", choices=["auto", "wavefront", "lds", "global"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
@@ -107,14 +107,17 @@ def main():
     rows = shard.local_rows(H, BAND, world, rank)
     tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, world) == rank else None
     assert tail is None or len(tail) == 0, "bench frames are whole bands"
-    algo = {"auto": lr.RT_ALGO_AUTO, "lds": lr.RT_ALGO_BRUTE_LDS, "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
+    algo = {"auto": lr.RT_ALGO_AUTO, "wavefront": lr.RT_ALGO_WAVEFRONT, "lds": lr.RT_ALGO_BRUTE_LDS,
+            "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
     opts = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
                           max_depth=args.depth, spp=1, algo=algo,
                           flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8)
     pitch = 3 * W
     out_rgb = torch.empty((len(rows), W, 3), dtype=torch.float32, device=dev)
     out_bgr = torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a real (non-null) stream: the library launches on exactly this stream, so the
+    # torch events below bracket the kernel (handle 0 would select the context's own stream)
+    stream = torch.cuda.Stream(dev)
 
     def step():
         ctx.render_device(opts, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)

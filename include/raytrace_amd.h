@@ -138,7 +138,12 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene* scene);
 
 enum rt_jitter { RT_JITTER_CENTER = 0 };   /* jx = jy = 0.5 (deterministic parity mode, main.rs:51-52) */
 enum rt_out_flags { RT_OUT_RGB_F32 = 1, RT_OUT_BGR_U8 = 2 };
-enum rt_algo { RT_ALGO_AUTO = 0, RT_ALGO_BRUTE_LDS = 1, RT_ALGO_BRUTE_GLOBAL = 2 };
+enum rt_algo {
+    RT_ALGO_AUTO = 0,
+    RT_ALGO_BRUTE_LDS = 1,      /* megakernel, sphere list staged in LDS */
+    RT_ALGO_BRUTE_GLOBAL = 2,   /* megakernel, sphere list read through the caches */
+    RT_ALGO_WAVEFRONT = 3       /* one launch per recursion depth over compacted ray queues (default) */
+};
 
 typedef struct {
     uint32_t width, height;   /* full frame: defines the pixel -> (-1,1) mapping (main.rs:39-41) */

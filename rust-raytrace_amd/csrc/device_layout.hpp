@@ -65,11 +65,41 @@ struct FrameParams {
     uint32_t band, band_stride, band_phase;
     uint32_t max_depth, spp;
     uint32_t bgr_pitch;
+    uint32_t row0, rows;            // this launch covers local rows [row0, row0 + rows) of the tile
     float* out_rgb;                 // tile_h * tile_w * 3, may be null
     uint8_t* out_bgr;               // tile_h * bgr_pitch, may be null
     unsigned long long* counters;   // [kCounterShards] rays, then [kCounterShards] shadow rays
 };
 
+// Wavefront working set for one chunk of a tile (all in HBM; sized by the
+// host for `cap` pixels / `slots` generation-0 slots; 288 GB leaves room).
+// Generation k = recursion depth k (raytrace.rs:33,63): queue Q_k holds the
+// rays ray_color is called with at depth k.
+struct WfBufs {
+    double* qo[2][3];               // ray origin x,y,z  (queues ping-pong by generation parity)
+    double* qd[2][3];               // ray direction
+    double* qsig[2];                // significance passed down (raytrace.rs:63)
+    uint32_t* qpix[2];              // owning pixel (chunk-local index)
+    double* hit_t;                  // per queue entry of the current generation
+    int32_t* hit_obj;               // object id; INT32_MAX = miss; -2 = dead slot
+    int32_t* hit_prim;              // sphere index >= 0, ~plane index < 0
+    int32_t* shade_slot;            // index into shade_list, or -1
+    uint32_t* shade_list;           // queue entries that need light evaluation
+    uint32_t* occ;                  // per shade entry: bit l set = light l shadowed
+    double* st[3];                  // per-level local colour, [level * cap + p]
+    int32_t* st_obj;                // per-level object id (its specular colour is the fold factor)
+    double* term[3];                // terminal colour of each pixel's chain
+    uint8_t* nlev;                  // levels pushed per pixel
+    uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: |shade list_k|
+    unsigned long long* totals;     // [0] nearest queries, [1] shadow queries (accumulated over chunks)
+    uint32_t cap;                   // pixel capacity (stack stride)
+    uint32_t slots;                 // generation-0 slots (8x8-tiled, >= pixels)
+    uint32_t tiles_x;               // 8x8 tiles per row of the chunk
+};
+
+constexpr int kCntQ = 0;
+constexpr int kCntS = 64;
+constexpr int kCntWords = 128;
 constexpr int kCounterShards = 256;
 constexpr int kMaxLevels = 32;      // >= RT_MAX_DEPTH_LIMIT + 2
 

@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "device_layout.hpp"
@@ -13,6 +16,7 @@
 
 namespace rtamd {
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, bool lds, hipStream_t s);
 hipError_t upload_srgb_table(const double* avg255);
 }  // namespace rtamd
 
@@ -34,6 +38,10 @@ struct rt_ctx {
     uint64_t last_pixels = 0;
     bool last_timed = false;
     hipStream_t last_stream = nullptr;
+    // wavefront working set (grown on demand, kept across renders)
+    void* wf_mem = nullptr;
+    size_t wf_bytes = 0;
+    WfBufs wf{};
     std::string err;
 };
 
@@ -56,6 +64,56 @@ int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
     } while (0)
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// counters: [0, 256) rays per shard (megakernel), [256, 512) shadow rays per
+// shard, [512] nearest queries and [513] shadow queries (wavefront totals)
+constexpr int kCounterWords = 2 * kCounterShards + 2;
+
+uint32_t wf_chunk_pixels() {
+    const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
+    long v = e ? std::atol(e) : 0;
+    return v > 0 ? static_cast<uint32_t>(v) : (1u << 24);
+}
+
+// Carve the wavefront working set for chunks of up to `cap` pixels in
+// `slots` generation-0 slots with `levels` stack levels.
+int ensure_wf(rt_ctx* c, uint32_t cap, uint32_t slots, uint32_t levels) {
+    WfBufs& b = c->wf;
+    size_t off = 0;
+    std::vector<std::pair<void**, size_t>> parts;
+    auto add = [&](void** p, size_t bytes) { parts.emplace_back(p, off); off = align_up(off + bytes, 256); };
+    const size_t q = slots;                    // queue capacity (>= pixels)
+    for (int g = 0; g < 2; ++g) {
+        for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qo[g][a]), q * 8);
+        for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qd[g][a]), q * 8);
+        add(reinterpret_cast<void**>(&b.qsig[g]), q * 8);
+        add(reinterpret_cast<void**>(&b.qpix[g]), q * 4);
+    }
+    add(reinterpret_cast<void**>(&b.hit_t), q * 8);
+    add(reinterpret_cast<void**>(&b.hit_obj), q * 4);
+    add(reinterpret_cast<void**>(&b.hit_prim), q * 4);
+    add(reinterpret_cast<void**>(&b.shade_slot), q * 4);
+    add(reinterpret_cast<void**>(&b.shade_list), q * 4);
+    add(reinterpret_cast<void**>(&b.occ), q * 4);
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.st[a]), static_cast<size_t>(levels) * cap * 8);
+    add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.term[a]), static_cast<size_t>(cap) * 8);
+    add(reinterpret_cast<void**>(&b.nlev), cap);
+    add(reinterpret_cast<void**>(&b.cnt), kCntWords * 4);
+    if (off > c->wf_bytes) {
+        if (c->wf_mem) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->wf_mem); }
+        c->wf_mem = nullptr;
+        c->wf_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->wf_mem, off));
+        c->wf_bytes = off;
+    }
+    auto* base = static_cast<uint8_t*>(c->wf_mem);
+    for (auto& pr : parts) *pr.first = base + pr.second;
+    b.totals = c->d_counters + 2 * kCounterShards;
+    b.cap = cap;
+    b.slots = slots;
+    return RT_OK;
+}
 
 double significance(const rt_color& c) { return c.r + c.g + c.b; }   // color.rs:637-639
 
@@ -86,7 +144,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, RT_E_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, 2 * kCounterShards * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         upload_srgb_table(srgb_average_table()) != hipSuccess)
         return cleanup(fail(nullptr, RT_E_HIP, "context initialisation failed"));
     *out = c;
@@ -101,6 +159,7 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_bgr) (void)hipFree(c->d_bgr);
+    if (c->wf_mem) (void)hipFree(c->wf_mem);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -221,7 +280,7 @@ static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_
     if (spp == 0) return fail(c, RT_E_INVALID, "spp must be set (the scene's antialias value for reference behaviour)");
     pitch = o->bgr_pitch ? o->bgr_pitch : 3 * o->tile_w;
     if (pitch < 3 * o->tile_w) return fail(c, RT_E_INVALID, "bgr_pitch < 3*tile_w");
-    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_BRUTE_GLOBAL) return fail(c, RT_E_INVALID, "bad algo");
+    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_WAVEFRONT) return fail(c, RT_E_INVALID, "bad algo");
     return RT_OK;
 }
 
@@ -245,18 +304,46 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     fp.out_rgb = (o->flags & RT_OUT_RGB_F32) ? static_cast<float*>(d_rgb) : nullptr;
     fp.out_bgr = (o->flags & RT_OUT_BGR_U8) ? static_cast<uint8_t*>(d_bgr) : nullptr;
     fp.counters = c->d_counters;
-    int mode = o->algo;
+    fp.row0 = 0;
+    fp.rows = o->tile_h;
     const size_t lds_bytes = static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere);
-    if (mode == RT_ALGO_AUTO) mode = lds_bytes <= 64 * 1024 ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL;
+    const bool fits_lds = lds_bytes <= 64 * 1024;
+    int mode = o->algo;
+    if (mode == RT_ALGO_AUTO) mode = c->dsc.n_lights <= 32 ? RT_ALGO_WAVEFRONT : (fits_lds ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL);
     if (mode == RT_ALGO_BRUTE_LDS && lds_bytes > 160 * 1024)
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
-    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 2 * kCounterShards * sizeof(unsigned long long), st));
+    if (mode == RT_ALGO_WAVEFRONT && c->dsc.n_lights > 32)
+        return fail(c, RT_E_UNSUPPORTED, "the wavefront path handles at most 32 lights");
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
     c->last_stream = st;
     if (o->tile_w == 0 || o->tile_h == 0) { c->last_timed = false; return RT_OK; }
-    HIP_TRY(c, hipEventRecord(c->ev0, st));
-    HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
-    HIP_TRY(c, hipEventRecord(c->ev1, st));
+    if (mode == RT_ALGO_WAVEFRONT) {
+        // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
+        uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
+        chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
+        const uint32_t tiles_x = (o->tile_w + 7) / 8;
+        const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
+        const uint32_t cap = o->tile_w * chunk_rows;
+        int rc2 = ensure_wf(c, cap, slots, o->max_depth + 1);
+        if (rc2 != RT_OK) return rc2;
+        c->wf.tiles_x = tiles_x;
+        HIP_TRY(c, hipEventRecord(c->ev0, st));
+        for (uint32_t r0 = 0; r0 < o->tile_h; r0 += chunk_rows) {
+            FrameParams f = fp;
+            f.row0 = r0;
+            f.rows = std::min(chunk_rows, o->tile_h - r0);
+            WfBufs b = c->wf;
+            b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
+            HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), st));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, fits_lds, st));
+        }
+        HIP_TRY(c, hipEventRecord(c->ev1, st));
+    } else {
+        HIP_TRY(c, hipEventRecord(c->ev0, st));
+        HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
+        HIP_TRY(c, hipEventRecord(c->ev1, st));
+    }
     c->last_timed = true;
     return RT_OK;
 }
@@ -264,12 +351,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
 int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
-    unsigned long long h[2 * kCounterShards];
+    unsigned long long h[kCounterWords];
     if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
     HIP_TRY(c, hipMemcpyAsync(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     std::memset(s, 0, sizeof *s);
     for (int i = 0; i < kCounterShards; ++i) { s->rays += h[i]; s->shadow_rays += h[kCounterShards + i]; }
+    s->rays += h[2 * kCounterShards] + h[2 * kCounterShards + 1];
+    s->shadow_rays += h[2 * kCounterShards + 1];
     s->pixels = c->last_pixels;
     if (c->last_timed) {
         float ms = 0.f;

@@ -1,0 +1,253 @@
+// Device-side exact restatement of the reference's per-ray math, shared by the
+// megakernel and the wavefront kernels (trace_kernel.hip).
+//
+// Exactness: every operation is the reference's f64 operation in the
+// reference's order, compiled with -ffp-contract=off (no FMA fusion; Rust never
+// fuses).  f64 add/mul/div/sqrt are IEEE correctly rounded on gfx950, so the
+// only possible difference from the CPU is pow() (raytrace.rs:55): OCML vs
+// glibc, <= 1 ulp (measured: bit-identical on every parity scene so far).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_layout.hpp"
+
+namespace rtamd {
+
+extern __constant__ double c_srgb_avg[255];
+
+constexpr double kMinSignificance = 1.0 / 256.0 / 2.0;            // raytrace.rs:17
+constexpr double kEps = 0.00001;                                   // raytrace.rs:43,62
+constexpr double kFrac1Pi = 0.318309886183790671537767526745028724; // f64::consts::FRAC_1_PI
+
+struct Ray {
+    double ox, oy, oz, dx, dy, dz;
+};
+
+struct Hit {
+    double t;
+    int32_t obj;        // object id, INT32_MAX = no hit
+    int32_t prim;       // sphere index (>= 0) or ~plane index (< 0)
+    bool nan_t;
+};
+
+struct Col {
+    double r, g, b;
+};
+
+__device__ __forceinline__ double clamp_zero(double x) { return x < 0.0 ? 0.0 : x; }   // raytrace.rs:20-23
+
+// color.rs:593-600 as a binary search over the strictly increasing table.
+__device__ __forceinline__ uint8_t to_srgb(double v) {
+    if (!(v < c_srgb_avg[254])) return 255;      // also NaN
+    int lo = 0, hi = 254;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int mid = (lo + hi) >> 1;
+        bool lt = v < c_srgb_avg[mid];
+        hi = lt ? mid : hi;
+        lo = lt ? lo : mid + 1;
+    }
+    return static_cast<uint8_t>(lo);
+}
+
+// shapes.rs:60-89: the exact quadratic; true + the t the reference returns, or
+// false for None.  `a2` = 2.0*a, `a4` = 4.0*a are hoisted per ray (the same
+// f64 products the reference forms per test).
+__device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, double a2, double a4, double& t) {
+    const double ocx = r.ox - s.cx, ocy = r.oy - s.cy, ocz = r.oz - s.cz;
+    const double b = 2.0 * (r.dx * ocx + r.dy * ocy + r.dz * ocz);
+    const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - s.rr;
+    const double disc = b * b - a4 * cc;
+    if (disc > 0.0) {
+        const double sq = sqrt(disc);
+        const double t1 = (-b - sq) / a2;
+        if (t1 > 0.0) { t = t1; return true; }
+        const double t2 = (-b + sq) / a2;
+        if (t2 > 0.0) { t = t2; return true; }
+    }
+    return false;
+}
+
+// shapes.rs:100-112: t = n.(p - o) / n.d ; None iff t <= 0 (a NaN t is a hit).
+__device__ __forceinline__ bool plane_t(const DevPlane& p, const Ray& r, double& t) {
+    const double ex = p.px - r.ox, ey = p.py - r.oy, ez = p.pz - r.oz;
+    t = (p.nx * ex + p.ny * ey + p.nz * ez) / (p.nx * r.dx + p.ny * r.dy + p.nz * r.dz);
+    return !(t <= 0.0);
+}
+
+// Scene::intersect (scene.rs:247-249), brute force: every object tested.
+// min_by_key(FloatNotNan(t)): a NaN t (only a plane can produce one) is the
+// minimum key and the first in file order wins outright; otherwise smallest t,
+// ties to the FIRST object in file order.
+template <class SpherePtr>
+__device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, const Ray& r) {
+    Hit h;
+    h.t = __builtin_huge_val();
+    h.obj = INT32_MAX;
+    h.prim = 0;
+    h.nan_t = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        const int32_t obj = sc.plane_obj[i];
+        if (t != t) {
+            if (!h.nan_t) { h.nan_t = true; h.t = t; h.obj = obj; h.prim = ~i; }
+        } else if (!h.nan_t && (t < h.t || (t == h.t && obj < h.obj))) {
+            h.t = t; h.obj = obj; h.prim = ~i;
+        }
+    }
+    if (h.nan_t) return h;      // no sphere can produce a NaN t
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;     // direction.sqnorm()
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const int n = sc.n_spheres;
+#pragma unroll 2
+    for (int i = 0; i < n; ++i) {
+        const DevSphere s = S[i];
+        double t;
+        if (sphere_t(s, r, a2, a4, t)) {
+            const int32_t obj = sc.sphere_obj[i];
+            if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = i; }
+        }
+    }
+    return h;
+}
+
+// The shadow test of raytrace.rs:41-49: `intersect(shadow ray)` is Some and
+// (range is None or t*t < range).  Equivalent any-hit form:
+//  * no range (directional light): shadowed iff ANY object reports a hit;
+//  * with range (point light): if any plane reports a NaN t the nearest hit
+//    is that NaN hit and NaN*NaN < r2 is false -> lit; otherwise shadowed iff
+//    SOME hit has t*t < r2 (t_min <= t_i and rounding is monotone, so the
+//    nearest one then qualifies too).
+template <class SpherePtr>
+__device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, const Ray& r, bool has_range, double r2) {
+    bool plane_block = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        if (!has_range) return true;
+        if (t != t) return false;
+        plane_block |= t * t < r2;
+    }
+    if (plane_block) return true;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const int n = sc.n_spheres;
+    for (int i = 0; i < n; ++i) {
+        const DevSphere s = S[i];
+        double t;
+        if (sphere_t(s, r, a2, a4, t)) {
+            if (!has_range || t * t < r2) return true;
+        }
+    }
+    return false;
+}
+
+// The surface normal the reference's intersect() returned for the winner:
+// sphere normalize(ray.cast(t) - center) (shapes.rs:61,66); plane: as in the
+// file (shapes.rs:108).  pt == ray.cast(t) bit-for-bit.
+__device__ __forceinline__ void hit_normal(const DevScene& sc, const DevSphere* S, int32_t prim, double ptx, double pty,
+                                           double ptz, double& nx, double& ny, double& nz) {
+    if (prim >= 0) {
+        const DevSphere s = S[prim];
+        const double ux = ptx - s.cx, uy = pty - s.cy, uz = ptz - s.cz;
+        const double l = sqrt(ux * ux + uy * uy + uz * uz);
+        nx = ux / l; ny = uy / l; nz = uz / l;
+    } else {
+        const DevPlane& p = sc.planes[~prim];
+        nx = p.nx; ny = p.ny; nz = p.nz;
+    }
+}
+
+// Light direction and squared range (scene.rs:122-138).  Returns has_range.
+__device__ __forceinline__ bool light_dir(const DevLight& L, double ptx, double pty, double ptz, double& lx, double& ly,
+                                          double& lz, double& r2) {
+    if (L.kind == 0) {                       // PointLight
+        const double vx = L.v[0] - ptx, vy = L.v[1] - pty, vz = L.v[2] - ptz;
+        r2 = vx * vx + vy * vy + vz * vz;    // location.sqdist(pt)
+        const double l = sqrt(r2);           // == norm of the same vector
+        lx = vx / l; ly = vy / l; lz = vz / l;
+        return true;
+    }
+    lx = -L.v[0]; ly = -L.v[1]; lz = -L.v[2];  // DirectionalLight: -direction, not normalised
+    r2 = 0.0;
+    return false;
+}
+
+// The diffuse and Blinn-Phong terms of one unshadowed light (raytrace.rs:51-56).
+__device__ __forceinline__ void add_light(Col& res, const DevMaterial& m, const DevLight& L, bool diffuse, bool specular,
+                                          double lx, double ly, double lz, double nx, double ny, double nz,
+                                          double dx, double dy, double dz) {
+    if (diffuse) {
+        const double s = clamp_zero(lx * nx + ly * ny + lz * nz);
+        res.r = res.r + ((m.kd[0] * L.color[0]) * s) * kFrac1Pi;
+        res.g = res.g + ((m.kd[1] * L.color[1]) * s) * kFrac1Pi;
+        res.b = res.b + ((m.kd[2] * L.color[2]) * s) * kFrac1Pi;
+    }
+    if (specular) {
+        const double hx = lx - dx, hy = ly - dy, hz = lz - dz;
+        const double hl = sqrt(hx * hx + hy * hy + hz * hz);
+        const double c = clamp_zero(nx * (hx / hl) + ny * (hy / hl) + nz * (hz / hl));
+        const double p = pow(c, m.exponent);
+        res.r = res.r + (m.ks[0] * L.color[0]) * p;
+        res.g = res.g + (m.ks[1] * L.color[1]) * p;
+        res.b = res.b + (m.ks[2] * L.color[2]) * p;
+    }
+}
+
+// Pixel -> camera ray (main.rs:50-53 with the centre jitter; camera.rs:78).
+__device__ __forceinline__ Ray camera_ray(const DevScene& sc, const FrameParams& fp, uint32_t lx, uint32_t local_row) {
+    const uint32_t x = fp.x0 + lx;
+    const uint32_t y = fp.y0 + ((local_row / fp.band) * fp.band_stride + fp.band_phase) * fp.band + local_row % fp.band;
+    const double px = ((static_cast<double>(x) + 0.5) - fp.hw) * fp.scale;
+    const double py = ((static_cast<double>(y) + 0.5) - fp.hh) * fp.scale;
+    const double* M = sc.cam_m;
+    const double dx = M[0] * px + M[1] * py + M[2] * 1.0;
+    const double dy = M[3] * px + M[4] * py + M[5] * 1.0;
+    const double dz = M[6] * px + M[7] * py + M[8] * 1.0;
+    const double l = sqrt(dx * dx + dy * dy + dz * dz);
+    return Ray{sc.cam_pos[0], sc.cam_pos[1], sc.cam_pos[2], dx / l, dy / l, dz / l};
+}
+
+// Mirror direction and the offset origin of raytrace.rs:60-62.
+__device__ __forceinline__ Ray reflect_ray(const Ray& r, double ptx, double pty, double ptz, double nx, double ny,
+                                           double nz) {
+    const double dn = r.dx * nx + r.dy * ny + r.dz * nz;
+    const double k2 = 2.0 * dn;
+    const double rdx = r.dx - nx * k2, rdy = r.dy - ny * k2, rdz = r.dz - nz * k2;
+    return Ray{ptx + rdx * kEps, pty + rdy * kEps, ptz + rdz * kEps, rdx, rdy, rdz};
+}
+
+// Final colour of a pixel from its spp identical centre-jitter samples
+// (raytrace.rs:271-275, main.rs:47-56): res = BLACK; res += (BLACK + c)/1 per
+// sample; res / spp.
+__device__ __forceinline__ Col average_samples(Col c, uint32_t spp) {
+    c = Col{(0.0 + c.r) / 1.0, (0.0 + c.g) / 1.0, (0.0 + c.b) / 1.0};
+    Col res{0.0, 0.0, 0.0};
+    for (uint32_t k = 0; k < spp; ++k) res = Col{res.r + c.r, res.g + c.g, res.b + c.b};
+    const double aa = static_cast<double>(spp);
+    return Col{res.r / aa, res.g / aa, res.b / aa};
+}
+
+__device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, uint32_t out_row, Col res) {
+    const size_t p = static_cast<size_t>(out_row) * fp.tile_w + lx;
+    if (fp.out_rgb) {
+        fp.out_rgb[3 * p + 0] = static_cast<float>(res.r);
+        fp.out_rgb[3 * p + 1] = static_cast<float>(res.g);
+        fp.out_rgb[3 * p + 2] = static_cast<float>(res.b);
+    }
+    if (fp.out_bgr) {
+        uint8_t* q = fp.out_bgr + static_cast<size_t>(out_row) * fp.bgr_pitch + 3u * lx;
+        q[0] = to_srgb(res.b);
+        q[1] = to_srgb(res.g);
+        q[2] = to_srgb(res.r);
+        if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
+            for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k)
+                fp.out_bgr[static_cast<size_t>(out_row) * fp.bgr_pitch + k] = 0;
+    }
+}
+
+}  // namespace rtamd

@@ -1,30 +1,32 @@
-// Per-pixel ray tracing on CDNA4 (gfx950): one work-item per pixel.
+// Per-pixel ray tracing on CDNA4 (gfx950).
 //
-// One launch replaces the reference's whole pixel loop (main.rs:45-57): each
-// lane maps its pixel to a camera ray (main.rs:50-53, camera.rs:76-80), runs
-// the recursive ray_color / PhongMaterial::color chain (raytrace.rs:30-67,
-// 261-276) as a fixed-depth loop, and writes its f32 RGB and sRGB-quantised
-// BGR bytes (color.rs:593-600,628-632).
+// Two schedules of the same exact math (trace_common.hpp):
 //
-// Exactness: every operation is the reference's f64 operation in the
-// reference's order, compiled with -ffp-contract=off (no FMA fusion; Rust never
-// fuses).  f64 add/mul/div/sqrt are IEEE correctly rounded on gfx950, so the
-// only possible difference from the CPU is pow() (raytrace.rs:55): OCML vs
-// glibc, <= 1 ulp.  The recursion `res + ks * ray_color(child)`
-// (raytrace.rs:63) is evaluated inner-first, exactly: each level's local
-// colour is pushed on a per-lane stack and folded backwards at the end.
+//  * trace_frame_kernel ("megakernel"): one work-item per pixel runs the whole
+//    recursive ray_color / PhongMaterial::color chain (raytrace.rs:30-67,
+//    261-276) as a loop.  Simple, but a wave lives as long as its deepest
+//    pixel and holds all shading state across every intersection loop.
 //
-// Scene::intersect (scene.rs:247-249) semantics kept exactly: every object is
-// tested; the winner is the smallest t with ties going to the FIRST object in
-// file order, except that a NaN t (only a plane can produce one, 0/0) sorts
-// below every number and wins.  Shadow queries use an any-hit early exit that
-// is provably equivalent (see occluded()).
+//  * wavefront (wf_*): one generation per recursion depth k.  Queue Q_k in HBM
+//    holds exactly the rays ray_color is called with at depth k; per
+//    generation:
+//        wf_nearest    Scene::intersect for every ray of Q_k (scene.rs:247-249)
+//                      and compaction of the hits that need light evaluation
+//        wf_occlusion  the shadow queries of those hits (raytrace.rs:41-49)
+//        wf_shade      the Phong sum (raytrace.rs:31-56), push of the level's
+//                      local colour, compaction of the reflection rays into
+//                      Q_{k+1} (raytrace.rs:58-64)
+//    then wf_fold evaluates `res + ks * ray_color(child)` inner-first from the
+//    per-pixel level stack (bit-exact, raytrace.rs:63) and writes f32 RGB +
+//    sRGB BGR.  Every lane of every launch holds a live ray: no divergence over
+//    path length, small kernels, high occupancy.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
 
 #include "device_layout.hpp"
+#include "trace_common.hpp"
 
 namespace rtamd {
 
@@ -32,140 +34,13 @@ __constant__ double c_srgb_avg[255];
 
 namespace {
 
-constexpr double kMinSignificance = 1.0 / 256.0 / 2.0;            // raytrace.rs:17
-constexpr double kEps = 0.00001;                                   // raytrace.rs:43,62
-constexpr double kFrac1Pi = 0.318309886183790671537767526745028724; // f64::consts::FRAC_1_PI
-constexpr int kBlock = 256;                                        // 4 waves = 16x16 pixels
+constexpr int kBlock = 256;                 // 4 waves
 
-struct Ray {
-    double ox, oy, oz, dx, dy, dz;
-};
-
-struct Hit {
-    double t;
-    int32_t obj;        // object id, INT32_MAX = no hit
-    int32_t prim;       // sphere index or plane index
-    bool sphere;
-    bool nan_t;
-};
-
-__device__ __forceinline__ double clamp_zero(double x) { return x < 0.0 ? 0.0 : x; }
-
-// color.rs:593-600 as a binary search over the strictly increasing table.
-__device__ __forceinline__ uint8_t to_srgb(double v) {
-    if (!(v < c_srgb_avg[254])) return 255;      // also NaN
-    int lo = 0, hi = 254;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        int mid = (lo + hi) >> 1;
-        bool lt = v < c_srgb_avg[mid];
-        hi = lt ? mid : hi;
-        lo = lt ? lo : mid + 1;
-    }
-    return static_cast<uint8_t>(lo);
-}
-
-// shapes.rs:60-89: the exact quadratic; returns the t the reference would
-// return, or -1 when it returns None.  `a2` = 2.0*a, `a4` = 4.0*a hoisted per
-// ray (the same f64 products the reference forms per test).
-__device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, double a2, double a4, double& t) {
-    const double ocx = r.ox - s.cx, ocy = r.oy - s.cy, ocz = r.oz - s.cz;
-    const double b = 2.0 * (r.dx * ocx + r.dy * ocy + r.dz * ocz);
-    const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - s.rr;
-    const double disc = b * b - a4 * cc;
-    if (disc > 0.0) {
-        const double sq = sqrt(disc);
-        const double t1 = (-b - sq) / a2;
-        if (t1 > 0.0) { t = t1; return true; }
-        const double t2 = (-b + sq) / a2;
-        if (t2 > 0.0) { t = t2; return true; }
-    }
-    return false;
-}
-
-// shapes.rs:100-112: t = n.(p - o) / n.d ; None iff t <= 0 (a NaN t is a hit).
-__device__ __forceinline__ bool plane_t(const DevPlane& p, const Ray& r, double& t) {
-    const double ex = p.px - r.ox, ey = p.py - r.oy, ez = p.pz - r.oz;
-    t = (p.nx * ex + p.ny * ey + p.nz * ez) / (p.nx * r.dx + p.ny * r.dy + p.nz * r.dz);
-    return !(t <= 0.0);
-}
+// ---------------------------------------------------------------- megakernel
 
 template <class SpherePtr>
-__device__ __forceinline__ Hit nearest(const DevScene& sc, SpherePtr S, const Ray& r) {
-    Hit h;
-    h.t = __builtin_huge_val();
-    h.obj = INT32_MAX;
-    h.prim = -1;
-    h.sphere = false;
-    h.nan_t = false;
-    // Planes first (few).  scene.rs:248 min_by_key(FloatNotNan): a NaN t is
-    // the minimum key; the first NaN in file order wins outright.
-    for (int i = 0; i < sc.n_planes; ++i) {
-        double t;
-        if (!plane_t(sc.planes[i], r, t)) continue;
-        const int32_t obj = sc.plane_obj[i];
-        if (t != t) {
-            if (!h.nan_t || obj < h.obj) { h.nan_t = true; h.t = t; h.obj = obj; h.prim = i; h.sphere = false; }
-        } else if (!h.nan_t && (t < h.t || (t == h.t && obj < h.obj))) {
-            h.t = t; h.obj = obj; h.prim = i; h.sphere = false;
-        }
-    }
-    if (h.nan_t) return h;      // no sphere can produce a NaN t
-    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;     // direction.sqnorm()
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
-    const int n = sc.n_spheres;
-#pragma unroll 2
-    for (int i = 0; i < n; ++i) {
-        const DevSphere s = S[i];
-        double t;
-        if (sphere_t(s, r, a2, a4, t)) {
-            const int32_t obj = sc.sphere_obj[i];
-            if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = i; h.sphere = true; }
-        }
-    }
-    return h;
-}
-
-// The shadow test of raytrace.rs:41-49: `intersect(shadow ray)` is Some and
-// (range is None or t*t < range).  Equivalent any-hit form:
-//  * no range (directional light): shadowed iff ANY object reports a hit;
-//  * with range (point light): if any plane reports a NaN t the nearest-hit
-//    is that NaN hit and NaN*NaN < r2 is false -> lit; otherwise shadowed iff
-//    SOME hit has t*t < r2 (t_min <= t_i and rounding is monotone, so the
-//    nearest one then qualifies too).
-template <class SpherePtr>
-__device__ __forceinline__ bool occluded(const DevScene& sc, SpherePtr S, const Ray& r, bool has_range, double r2) {
-    bool plane_block = false;
-    for (int i = 0; i < sc.n_planes; ++i) {
-        double t;
-        if (!plane_t(sc.planes[i], r, t)) continue;
-        if (!has_range) return true;
-        if (t != t) return false;
-        plane_block |= t * t < r2;
-    }
-    if (plane_block) return true;
-    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
-    const int n = sc.n_spheres;
-    for (int i = 0; i < n; ++i) {
-        const DevSphere s = S[i];
-        double t;
-        if (sphere_t(s, r, a2, a4, t)) {
-            if (!has_range || t * t < r2) return true;
-        }
-    }
-    return false;
-}
-
-struct Col {
-    double r, g, b;
-};
-
-// ray_color (raytrace.rs:261-267) from depth 0 with significance 1.0,
-// PhongMaterial::color (raytrace.rs:30-67) flattened.  `rays`/`shadows`
-// count every Scene::intersect call, exactly as the reference issues them.
-template <class SpherePtr>
-__device__ Col trace(const DevScene& sc, SpherePtr S, Ray ray, uint32_t max_depth, uint32_t& rays, uint32_t& shadows) {
+__device__ Col trace_chain(const DevScene& sc, SpherePtr S, Ray ray, uint32_t max_depth, uint32_t& rays,
+                           uint32_t& shadows) {
     double st_r[kMaxLevels], st_g[kMaxLevels], st_b[kMaxLevels];
     int32_t st_obj[kMaxLevels];
     int lvl = 0;
@@ -173,77 +48,38 @@ __device__ Col trace(const DevScene& sc, SpherePtr S, Ray ray, uint32_t max_dept
     uint32_t depth = 0;
     Col term;
     for (;;) {
-        const Hit h = nearest(sc, S, ray);
+        const Hit h = nearest_brute(sc, S, ray);
         ++rays;
-        if (h.obj == INT32_MAX) {                                  // background, raytrace.rs:228-232
-            term = Col{sc.bg[0], sc.bg[1], sc.bg[2]};
-            break;
-        }
+        if (h.obj == INT32_MAX) { term = Col{sc.bg[0], sc.bg[1], sc.bg[2]}; break; }   // raytrace.rs:228-232
         const DevMaterial& m = sc.mats[h.obj];
         Col res{m.amb[0], m.amb[1], m.amb[2]};
         if (depth > max_depth) { term = res; break; }             // raytrace.rs:33
-        // pt = ray.cast(t) (shapes.rs:22-24)
         const double ptx = ray.ox + ray.dx * h.t, pty = ray.oy + ray.dy * h.t, ptz = ray.oz + ray.dz * h.t;
         double nx, ny, nz;
-        if (h.sphere) {             // normalize(ray.cast(t) - center) (shapes.rs:61)
-            const DevSphere s = S[h.prim];
-            const double ux = ptx - s.cx, uy = pty - s.cy, uz = ptz - s.cz;
-            const double l = sqrt(ux * ux + uy * uy + uz * uz);
-            nx = ux / l; ny = uy / l; nz = uz / l;
-        } else {
-            const DevPlane& p = sc.planes[h.prim];
-            nx = p.nx; ny = p.ny; nz = p.nz;
-        }
+        hit_normal(sc, sc.spheres, h.prim, ptx, pty, ptz, nx, ny, nz);
         const bool diffuse = m.kd_sig * sig > kMinSignificance;
         const bool specular = m.ks_sig * sig > kMinSignificance;
         if (nx * ray.dx + ny * ray.dy + nz * ray.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
         if (diffuse || specular) {
             for (int li = 0; li < sc.n_lights; ++li) {
                 const DevLight& L = sc.lights[li];
-                double lx, ly, lz, r2 = 0.0;
-                const bool has_range = L.kind == 0;
-                if (has_range) {    // PointLight, scene.rs:122-126
-                    const double vx = L.v[0] - ptx, vy = L.v[1] - pty, vz = L.v[2] - ptz;
-                    r2 = vx * vx + vy * vy + vz * vz;
-                    const double l = sqrt(r2);
-                    lx = vx / l; ly = vy / l; lz = vz / l;
-                } else {            // DirectionalLight, scene.rs:135-138
-                    lx = -L.v[0]; ly = -L.v[1]; lz = -L.v[2];
-                }
+                double lx, ly, lz, r2;
+                const bool has_range = light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
                 const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
                 ++rays;
                 ++shadows;
-                if (occluded(sc, S, sray, has_range, r2)) continue;
-                if (diffuse) {
-                    const double s = clamp_zero(lx * nx + ly * ny + lz * nz);
-                    res.r = res.r + ((m.kd[0] * L.color[0]) * s) * kFrac1Pi;
-                    res.g = res.g + ((m.kd[1] * L.color[1]) * s) * kFrac1Pi;
-                    res.b = res.b + ((m.kd[2] * L.color[2]) * s) * kFrac1Pi;
-                }
-                if (specular) {
-                    const double hx = lx - ray.dx, hy = ly - ray.dy, hz = lz - ray.dz;
-                    const double hl = sqrt(hx * hx + hy * hy + hz * hz);
-                    const double c = clamp_zero(nx * (hx / hl) + ny * (hy / hl) + nz * (hz / hl));
-                    const double p = pow(c, m.exponent);
-                    res.r = res.r + (m.ks[0] * L.color[0]) * p;
-                    res.g = res.g + (m.ks[1] * L.color[1]) * p;
-                    res.b = res.b + (m.ks[2] * L.color[2]) * p;
-                }
+                if (occluded_brute(sc, S, sray, has_range, r2)) continue;
+                add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, ray.dx, ray.dy, ray.dz);
             }
         }
         if (!specular) { term = res; break; }
-        // raytrace.rs:59-64: reflect and recurse; keep (res, object) for the fold.
         st_r[lvl] = res.r; st_g[lvl] = res.g; st_b[lvl] = res.b; st_obj[lvl] = h.obj;
         ++lvl;
-        const double dn = ray.dx * nx + ray.dy * ny + ray.dz * nz;
-        const double k2 = 2.0 * dn;
-        const double rdx = ray.dx - nx * k2, rdy = ray.dy - ny * k2, rdz = ray.dz - nz * k2;
-        ray = Ray{ptx + rdx * kEps, pty + rdy * kEps, ptz + rdz * kEps, rdx, rdy, rdz};
+        ray = reflect_ray(ray, ptx, pty, ptz, nx, ny, nz);
         sig = sig * m.ks_sig;
         ++depth;
     }
-    // Fold inner-first: res_k + ks_k * color_{k+1}  (raytrace.rs:63)
-    Col acc = term;
+    Col acc = term;                                                // fold inner-first (raytrace.rs:63)
     for (int k = lvl - 1; k >= 0; --k) {
         const DevMaterial& m = sc.mats[st_obj[k]];
         acc.r = st_r[k] + m.ks[0] * acc.r;
@@ -261,52 +97,19 @@ __global__ __launch_bounds__(kBlock) void trace_frame_kernel(DevScene sc, FrameP
         __syncthreads();
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // 16x16 pixel tile per workgroup, 8x8 per wave: neighbouring rays in a
-    // wave take the same branches more often.
+    // 16x16 pixel tile per workgroup, 8x8 per wave
     const uint32_t lx = blockIdx.x * 16u + (wave & 1) * 8u + (lane & 7);
     const uint32_t ly = blockIdx.y * 16u + (wave >> 1) * 8u + (lane >> 3);
     uint32_t rays = 0, shadows = 0;
-    if (lx < fp.tile_w && ly < fp.tile_h) {
-        const uint32_t x = fp.x0 + lx;
-        const uint32_t y = fp.y0 + ((ly / fp.band) * fp.band_stride + fp.band_phase) * fp.band + ly % fp.band;
-        // main.rs:50-53 with the deterministic centre jitter (jx = jy = 0.5)
-        const double px = ((static_cast<double>(x) + 0.5) - fp.hw) * fp.scale;
-        const double py = ((static_cast<double>(y) + 0.5) - fp.hh) * fp.scale;
-        // camera.rs:78: normalize(M * (px, py, 1))
-        const double* M = sc.cam_m;
-        const double dx = M[0] * px + M[1] * py + M[2] * 1.0;
-        const double dy = M[3] * px + M[4] * py + M[5] * 1.0;
-        const double dz = M[6] * px + M[7] * py + M[8] * 1.0;
-        const double l = sqrt(dx * dx + dy * dy + dz * dz);
-        const Ray cam{sc.cam_pos[0], sc.cam_pos[1], sc.cam_pos[2], dx / l, dy / l, dz / l};
-        Col res{0.0, 0.0, 0.0};
-        for (uint32_t k = 0; k < fp.spp; ++k) {
-            Col c;
-            if constexpr (kLds) c = trace(sc, static_cast<const DevSphere*>(lds_spheres), cam, fp.max_depth, rays, shadows);
-            else c = trace(sc, sc.spheres, cam, fp.max_depth, rays, shadows);
-            // raytrace.rs:271-275: (BLACK + c) / samples(=1); main.rs:54: res + that
-            c = Col{(0.0 + c.r) / 1.0, (0.0 + c.g) / 1.0, (0.0 + c.b) / 1.0};
-            res = Col{res.r + c.r, res.g + c.g, res.b + c.b};
-        }
-        const double aa = static_cast<double>(fp.spp);
-        res = Col{res.r / aa, res.g / aa, res.b / aa};            // main.rs:56
-        const size_t p = static_cast<size_t>(ly) * fp.tile_w + lx;
-        if (fp.out_rgb) {
-            fp.out_rgb[3 * p + 0] = static_cast<float>(res.r);
-            fp.out_rgb[3 * p + 1] = static_cast<float>(res.g);
-            fp.out_rgb[3 * p + 2] = static_cast<float>(res.b);
-        }
-        if (fp.out_bgr) {
-            uint8_t* q = fp.out_bgr + static_cast<size_t>(ly) * fp.bgr_pitch + 3u * lx;
-            q[0] = to_srgb(res.b);
-            q[1] = to_srgb(res.g);
-            q[2] = to_srgb(res.r);
-            if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
-                for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k)
-                    fp.out_bgr[static_cast<size_t>(ly) * fp.bgr_pitch + k] = 0;
-        }
+    if (lx < fp.tile_w && ly < fp.rows) {
+        const Ray cam = camera_ray(sc, fp, lx, fp.row0 + ly);
+        Col c;
+        if constexpr (kLds) c = trace_chain(sc, static_cast<const DevSphere*>(lds_spheres), cam, fp.max_depth, rays, shadows);
+        else c = trace_chain(sc, sc.spheres, cam, fp.max_depth, rays, shadows);
+        write_pixel(fp, lx, fp.row0 + ly, average_samples(c, fp.spp));
+        rays *= fp.spp;          // identical centre-jitter samples: traced once, counted as the reference issues them
+        shadows *= fp.spp;
     }
-    // Per-wave sums, one atomic per wave into a sharded counter.
     for (int off = 32; off > 0; off >>= 1) {
         rays += __shfl_xor(rays, off, 64);
         shadows += __shfl_xor(shadows, off, 64);
@@ -318,17 +121,267 @@ __global__ __launch_bounds__(kBlock) void trace_frame_kernel(DevScene sc, FrameP
     }
 }
 
+// ---------------------------------------------------------------- wavefront
+
+// Wave-aggregated append: one atomic per wave, lanes get consecutive slots in
+// lane order (keeps neighbouring rays neighbours).  All 64 lanes must call it.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool want) {
+    const unsigned long long mask = __ballot(want);
+    if (mask == 0) return 0xFFFFFFFFu;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, static_cast<uint32_t>(__popcll(mask)));
+    base = __shfl(base, leader, 64);
+    const uint32_t below = static_cast<uint32_t>(__popcll(mask & ((1ull << lane) - 1ull)));
+    return want ? base + below : 0xFFFFFFFFu;
+}
+
+// Generation-0 slot i -> pixel of the chunk, in 8x8 tiles (one tile per wave).
+__device__ __forceinline__ bool slot_pixel(const WfBufs& b, const FrameParams& fp, uint32_t i, uint32_t& lx,
+                                           uint32_t& ly) {
+    const uint32_t tile = i >> 6, w = i & 63u;
+    lx = (tile % b.tiles_x) * 8u + (w & 7u);
+    ly = (tile / b.tiles_x) * 8u + (w >> 3);
+    return lx < fp.tile_w && ly < fp.rows;
+}
+
+__device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, uint32_t i) {
+    return Ray{b.qo[q][0][i], b.qo[q][1][i], b.qo[q][2][i], b.qd[q][0][i], b.qd[q][1][i], b.qd[q][2][i]};
+}
+
+// Ray of queue entry i of generation k (generation 0 is computed, not stored).
+template <bool kCam>
+__device__ __forceinline__ bool entry_ray(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, uint32_t i,
+                                          Ray& r, double& sig, uint32_t& p) {
+    if constexpr (kCam) {
+        uint32_t lx, ly;
+        if (!slot_pixel(b, fp, i, lx, ly)) return false;
+        r = camera_ray(sc, fp, lx, fp.row0 + ly);
+        sig = 1.0;                                    // raytrace.rs:273 via main.rs:54
+        p = ly * fp.tile_w + lx;
+    } else {
+        const int q = k & 1;
+        r = load_ray(b, q, i);
+        sig = b.qsig[q][i];
+        p = b.qpix[q][i];
+    }
+    return true;
+}
+
+template <bool kLds, bool kCam>
+__global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
+    if constexpr (kLds) {
+        for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
+        __syncthreads();
+    }
+    const uint32_t n = kCam ? b.slots : b.cnt[kCntQ + k];
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        bool shade = false;
+        if (i < n) {
+            Ray r;
+            double sig;
+            uint32_t p;
+            if (!entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
+                b.hit_obj[i] = -2;                    // padding slot of a partial 8x8 tile
+            } else {
+                Hit h;
+                if constexpr (kLds) h = nearest_brute(sc, static_cast<const DevSphere*>(lds_spheres), r);
+                else h = nearest_brute(sc, sc.spheres, r);
+                b.hit_t[i] = h.t;
+                b.hit_obj[i] = h.obj;
+                b.hit_prim[i] = h.prim;
+                if (h.obj != INT32_MAX && static_cast<uint32_t>(k) <= fp.max_depth && sc.n_lights > 0) {
+                    const DevMaterial& m = sc.mats[h.obj];
+                    shade = m.kd_sig * sig > kMinSignificance || m.ks_sig * sig > kMinSignificance;
+                }
+            }
+        }
+        const uint32_t slot = wave_append(&b.cnt[kCntS + k], shade);
+        if (i < n) {
+            b.shade_slot[i] = shade ? static_cast<int32_t>(slot) : -1;
+            if (shade) b.shade_list[slot] = i;
+        }
+    }
+}
+
+template <bool kLds, bool kCam>
+__global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
+    if constexpr (kLds) {
+        for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
+        __syncthreads();
+    }
+    const uint32_t n = b.cnt[kCntS + k];
+    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
+        const uint32_t i = b.shade_list[j];
+        Ray r;
+        double sig;
+        uint32_t p;
+        entry_ray<kCam>(sc, fp, b, k, i, r, sig, p);
+        const double t = b.hit_t[i];
+        const double ptx = r.ox + r.dx * t, pty = r.oy + r.dy * t, ptz = r.oz + r.dz * t;
+        uint32_t mask = 0;
+        for (int l = 0; l < sc.n_lights; ++l) {
+            double lx, ly, lz, r2;
+            const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+            const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+            bool occ;
+            if constexpr (kLds) occ = occluded_brute(sc, static_cast<const DevSphere*>(lds_spheres), sray, has_range, r2);
+            else occ = occluded_brute(sc, sc.spheres, sray, has_range, r2);
+            mask |= static_cast<uint32_t>(occ) << l;
+        }
+        b.occ[j] = mask;
+    }
+}
+
+template <bool kCam>
+__global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    const uint32_t n = kCam ? b.slots : b.cnt[kCntQ + k];
+    const int qn = (k + 1) & 1;
+    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        bool refl = false;
+        Ray rr{};
+        double nsig = 0.0;
+        uint32_t p = 0;
+        if (i < n) {
+            const int32_t obj = b.hit_obj[i];
+            Ray r;
+            double sig;
+            if (obj != -2 && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
+                Col res;
+                bool done = true;
+                if (obj == INT32_MAX) {
+                    res = Col{sc.bg[0], sc.bg[1], sc.bg[2]};                // raytrace.rs:265, 228-232
+                } else {
+                    const DevMaterial& m = sc.mats[obj];
+                    res = Col{m.amb[0], m.amb[1], m.amb[2]};                // raytrace.rs:32
+                    if (static_cast<uint32_t>(k) <= fp.max_depth) {          // raytrace.rs:33
+                        const double t = b.hit_t[i];
+                        const double ptx = r.ox + r.dx * t, pty = r.oy + r.dy * t, ptz = r.oz + r.dz * t;
+                        double nx, ny, nz;
+                        hit_normal(sc, sc.spheres, b.hit_prim[i], ptx, pty, ptz, nx, ny, nz);
+                        const bool diffuse = m.kd_sig * sig > kMinSignificance;
+                        const bool specular = m.ks_sig * sig > kMinSignificance;
+                        if (nx * r.dx + ny * r.dy + nz * r.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+                        if ((diffuse || specular) && sc.n_lights > 0) {
+                            const uint32_t mask = b.occ[b.shade_slot[i]];
+                            for (int l = 0; l < sc.n_lights; ++l) {
+                                if ((mask >> l) & 1u) continue;              // shadowed (raytrace.rs:42-49)
+                                const DevLight& L = sc.lights[l];
+                                double lx, ly, lz, r2;
+                                light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
+                                add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, r.dx, r.dy, r.dz);
+                            }
+                        }
+                        if (specular) {                                      // raytrace.rs:58-64
+                            const size_t at = static_cast<size_t>(k) * b.cap + p;
+                            b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
+                            b.st_obj[at] = obj;
+                            rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
+                            nsig = sig * m.ks_sig;
+                            refl = true;
+                            done = false;
+                        }
+                    }
+                }
+                if (done) {
+                    b.term[0][p] = res.r; b.term[1][p] = res.g; b.term[2][p] = res.b;
+                    b.nlev[p] = static_cast<uint8_t>(k);
+                }
+            }
+        }
+        const uint32_t slot = wave_append(&b.cnt[kCntQ + k + 1], refl);
+        if (refl) {
+            b.qo[qn][0][slot] = rr.ox; b.qo[qn][1][slot] = rr.oy; b.qo[qn][2][slot] = rr.oz;
+            b.qd[qn][0][slot] = rr.dx; b.qd[qn][1][slot] = rr.dy; b.qd[qn][2][slot] = rr.dz;
+            b.qsig[qn][slot] = nsig;
+            b.qpix[qn][slot] = p;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
+    const uint32_t npix = fp.tile_w * fp.rows;
+    for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
+        Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
+        for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {   // res_k + ks_k * acc (raytrace.rs:63)
+            const size_t at = static_cast<size_t>(k) * b.cap + p;
+            const DevMaterial& m = sc.mats[b.st_obj[at]];
+            acc.r = b.st[0][at] + m.ks[0] * acc.r;
+            acc.g = b.st[1][at] + m.ks[1] * acc.g;
+            acc.b = b.st[2][at] + m.ks[2] * acc.b;
+        }
+        const uint32_t lx = p % fp.tile_w, ly = p / fp.tile_w;
+        write_pixel(fp, lx, fp.row0 + ly, average_samples(acc, fp.spp));
+    }
+}
+
+// Scene::intersect calls of this chunk: every pixel's camera ray, every later
+// queue entry, and one shadow query per light per shaded hit.
+__global__ void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
+    unsigned long long nearest = static_cast<unsigned long long>(fp.tile_w) * fp.rows, shadow = 0;
+    for (int k = 1; k < generations; ++k) nearest += b.cnt[kCntQ + k];
+    for (int k = 0; k < generations; ++k) shadow += static_cast<unsigned long long>(b.cnt[kCntS + k]) * n_lights;
+    b.totals[0] += nearest * fp.spp;
+    b.totals[1] += shadow * fp.spp;
+}
+
+inline int blocks_for(uint64_t items, int cap_blocks) {
+    uint64_t b = (items + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    return static_cast<int>(b < static_cast<uint64_t>(cap_blocks) ? b : cap_blocks);
+}
+
 }  // namespace
 
-// Host-side launcher.  mode: 1 = spheres staged in LDS, 2 = read from global.
+// Host-side launchers -------------------------------------------------------
+
+// mode: 1 = spheres staged in LDS, 2 = read from global.
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream) {
-    dim3 grid((fp.tile_w + 15) / 16, (fp.tile_h + 15) / 16);
+    dim3 grid((fp.tile_w + 15) / 16, (fp.rows + 15) / 16);
     if (mode == 1) {
         size_t lds = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
         hipLaunchKernelGGL(trace_frame_kernel<true>, grid, dim3(kBlock), lds, stream, sc, fp);
     } else {
         hipLaunchKernelGGL(trace_frame_kernel<false>, grid, dim3(kBlock), 0, stream, sc, fp);
     }
+    return hipGetLastError();
+}
+
+// One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
+// must be zero on entry (the caller memsets them).
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, bool lds, hipStream_t s) {
+    const size_t lds_bytes = lds ? static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere) : 0;
+    const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
+    const int gq = blocks_for(b.slots, 1024), gs = blocks_for(b.slots, 2048);
+    for (int k = 0; k < gens; ++k) {
+        if (k == 0) {
+            if (lds) {
+                hipLaunchKernelGGL((wf_nearest<true, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+                hipLaunchKernelGGL((wf_occlusion<true, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+            } else {
+                hipLaunchKernelGGL((wf_nearest<false, true>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
+                hipLaunchKernelGGL((wf_occlusion<false, true>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
+            }
+            hipLaunchKernelGGL((wf_shade<true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        } else {
+            if (lds) {
+                hipLaunchKernelGGL((wf_nearest<true, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+                hipLaunchKernelGGL((wf_occlusion<true, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+            } else {
+                hipLaunchKernelGGL((wf_nearest<false, false>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
+                hipLaunchKernelGGL((wf_occlusion<false, false>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
+            }
+            hipLaunchKernelGGL((wf_shade<false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        }
+    }
+    hipLaunchKernelGGL(wf_fold, dim3(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048)), dim3(kBlock), 0, s,
+                       sc, fp, b);
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(1), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-ALGOS = [lr.RT_ALGO_BRUTE_LDS, lr.RT_ALGO_BRUTE_GLOBAL]
+ALGOS = [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_BRUTE_LDS, lr.RT_ALGO_BRUTE_GLOBAL]
 
 
 def gpu_render(ctx, spec, algo=lr.RT_ALGO_AUTO, **kw):

@@ -142,7 +142,8 @@ enum rt_algo {
     RT_ALGO_AUTO = 0,
     RT_ALGO_BRUTE_LDS = 1,      /* megakernel, sphere list staged in LDS */
     RT_ALGO_BRUTE_GLOBAL = 2,   /* megakernel, sphere list read through the caches */
-    RT_ALGO_WAVEFRONT = 3       /* one launch per recursion depth over compacted ray queues (default) */
+    RT_ALGO_WAVEFRONT = 3,      /* per-depth launches over compacted ray queues, sphere BVH (default) */
+    RT_ALGO_WAVEFRONT_BRUTE = 4 /* the same schedule, every sphere tested (linear scan like scene.rs:248) */
 };
 
 typedef struct {

@@ -37,13 +37,16 @@ struct DevLight {
     int32_t _pad;
 };
 
-// One node of the sphere BVH (2 children, AABBs padded conservatively).
+// One BVH2 node: the boxes of BOTH children (one 64-B fetch decides both),
+// f32, rounded outward and padded on the host (host_bvh.cpp).  Child pointer
+// c >= 0: inner node c; c < 0: leaf with spheres [(~c) >> 3, +((~c) & 7) + 1).
 struct alignas(16) DevBvhNode {
-    double lo[3], hi[3];
-    int32_t left;                   // >= 0: inner node, children left, left+1; < 0: leaf
-    int32_t first, count;           // leaf: sphere range [first, first+count)
-    int32_t _pad;
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    int32_t c0, c1;
+    int32_t _pad[2];
 };
+static_assert(sizeof(DevBvhNode) == 64, "BVH node is one 64-B line");
 
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
@@ -52,7 +55,8 @@ struct DevScene {
     const int32_t* plane_obj;
     const DevMaterial* mats;        // indexed by object id
     const DevLight* lights;
-    const DevBvhNode* bvh;          // null when no BVH was built
+    const DevBvhNode* bvh;          // sphere BVH (spheres[] are in its leaf order)
+    int32_t bvh_root;               // encoded child pointer of the root (see DevBvhNode)
     int32_t n_spheres, n_planes, n_lights, n_bvh;
     double cam_pos[3];
     double cam_m[9];                // row-major

@@ -1,0 +1,174 @@
+// Sphere BVH builder (host).  The reference has no acceleration structure: its
+// Scene::intersect (scene.rs:247-249) tests every object.  The BVH only decides
+// which spheres a ray is TESTED against; the leaf test is the reference's
+// exact f64 quadratic and the winner is chosen by (NaN, t, object id) exactly
+// as min_by_key does, so the result is identical whenever the culling is
+// conservative ("BVH exactness").  Conservative here:
+//   * each sphere's box is [c - r, c + r] widened by `pad` and rounded OUTWARD
+//     to f32 (so it contains every point the f64 test can report as a hit);
+//   * the traversal (trace_common.hpp, box_hit) widens every slab interval by
+//     a relative 1e-5, covering f32 rounding of the ray and of the slab math.
+// Binned SAH (16 bins) with leaves of <= 4 spheres; median split below depth
+// 40 keeps the depth (and the per-lane traversal stack) bounded.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "bvh_build.hpp"
+
+namespace rtamd {
+namespace {
+
+float down(double x) {
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) > x) f = std::nextafter(f, -FLT_MAX);
+    return f;
+}
+float up(double x) {
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) < x) f = std::nextafter(f, FLT_MAX);
+    return f;
+}
+
+struct Box {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL};
+    double hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    void grow(const Box& b) {
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); }
+    }
+    double area() const {
+        double d[3];
+        for (int a = 0; a < 3; ++a) d[a] = std::max(0.0, hi[a] - lo[a]);
+        return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+};
+
+struct Prim {
+    Box box;
+    double c[3];
+    int32_t idx;
+};
+
+constexpr int kLeafMax = 4;
+constexpr int kBins = 16;
+constexpr int kSahDepth = 40;
+
+struct Builder {
+    std::vector<Prim>& prims;
+    std::vector<BvhNodeHost>& nodes;
+    double pad;
+
+    Box bounds(int b, int e) const {
+        Box r;
+        for (int i = b; i < e; ++i) r.grow(prims[i].box);
+        return r;
+    }
+
+    // Returns the encoded child pointer for prims[b, e).
+    int32_t build(int b, int e, int depth) {
+        const int n = e - b;
+        if (n <= kLeafMax) return ~((b << 3) | (n - 1));
+        Box cb;                         // centroid bounds
+        for (int i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) { cb.lo[a] = std::min(cb.lo[a], prims[i].c[a]); cb.hi[a] = std::max(cb.hi[a], prims[i].c[a]); }
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (cb.hi[a] - cb.lo[a] > cb.hi[axis] - cb.lo[axis]) axis = a;
+        int mid = -1;
+        const double ext = cb.hi[axis] - cb.lo[axis];
+        if (depth < kSahDepth && ext > 0) {
+            // binned SAH over all three axes
+            double best = HUGE_VAL;
+            int best_axis = -1, best_bin = -1;
+            for (int a = 0; a < 3; ++a) {
+                const double ea = cb.hi[a] - cb.lo[a];
+                if (!(ea > 0)) continue;
+                Box bb[kBins];
+                int bc[kBins] = {0};
+                for (int i = b; i < e; ++i) {
+                    int k = static_cast<int>((prims[i].c[a] - cb.lo[a]) / ea * kBins);
+                    k = std::min(kBins - 1, std::max(0, k));
+                    bb[k].grow(prims[i].box);
+                    ++bc[k];
+                }
+                Box lb[kBins], rb[kBins];
+                int lc[kBins], rc[kBins];
+                Box acc;
+                int cnt = 0;
+                for (int k = 0; k < kBins; ++k) { acc.grow(bb[k]); cnt += bc[k]; lb[k] = acc; lc[k] = cnt; }
+                acc = Box();
+                cnt = 0;
+                for (int k = kBins - 1; k >= 0; --k) { acc.grow(bb[k]); cnt += bc[k]; rb[k] = acc; rc[k] = cnt; }
+                for (int k = 0; k < kBins - 1; ++k) {
+                    if (lc[k] == 0 || rc[k + 1] == 0) continue;
+                    const double cost = lb[k].area() * lc[k] + rb[k + 1].area() * rc[k + 1];
+                    if (cost < best) { best = cost; best_axis = a; best_bin = k; }
+                }
+            }
+            if (best_axis >= 0) {
+                const int a = best_axis;
+                const double ea = cb.hi[a] - cb.lo[a];
+                auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim& p) {
+                    int k = static_cast<int>((p.c[a] - cb.lo[a]) / ea * kBins);
+                    k = std::min(kBins - 1, std::max(0, k));
+                    return k <= best_bin;
+                });
+                mid = static_cast<int>(it - prims.begin());
+                if (mid == b || mid == e) mid = -1;
+            }
+        }
+        if (mid < 0) {                  // median split (also for coincident centroids)
+            mid = b + n / 2;
+            std::nth_element(prims.begin() + b, prims.begin() + mid, prims.begin() + e,
+                             [&](const Prim& p, const Prim& q) {
+                                 return p.c[axis] < q.c[axis] || (p.c[axis] == q.c[axis] && p.idx < q.idx);
+                             });
+        }
+        const int32_t self = static_cast<int32_t>(nodes.size());
+        nodes.emplace_back();
+        const Box l = bounds(b, mid), r = bounds(mid, e);
+        const int32_t c0 = build(b, mid, depth + 1);
+        const int32_t c1 = build(mid, e, depth + 1);
+        BvhNodeHost& nd = nodes[self];
+        for (int a = 0; a < 3; ++a) {
+            nd.lo0[a] = down(l.lo[a]); nd.hi0[a] = up(l.hi[a]);
+            nd.lo1[a] = down(r.lo[a]); nd.hi1[a] = up(r.hi[a]);
+        }
+        nd.c0 = c0;
+        nd.c1 = c1;
+        return self;
+    }
+};
+
+}  // namespace
+
+BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& cz,
+                           const std::vector<double>& radius, double pad) {
+    BvhResult res;
+    const size_t n = cx.size();
+    if (n == 0) { res.root = 0; return res; }
+    std::vector<Prim> prims(n);
+    for (size_t i = 0; i < n; ++i) {
+        Prim& p = prims[i];
+        const double c[3] = {cx[i], cy[i], cz[i]};
+        const double r = std::fabs(radius[i]);
+        for (int a = 0; a < 3; ++a) {
+            p.c[a] = c[a];
+            // a NaN radius/centre never produces a hit (disc > 0 is false): any box works
+            p.box.lo[a] = std::isfinite(c[a] - r) ? c[a] - r - pad : -HUGE_VAL;
+            p.box.hi[a] = std::isfinite(c[a] + r) ? c[a] + r + pad : HUGE_VAL;
+            if (!std::isfinite(p.c[a])) p.c[a] = 0.0;
+        }
+        p.idx = static_cast<int32_t>(i);
+    }
+    res.nodes.reserve(2 * n / kLeafMax + 2);
+    Builder bld{prims, res.nodes, pad};
+    res.root = bld.build(0, static_cast<int>(n), 0);
+    res.order.resize(n);
+    for (size_t i = 0; i < n; ++i) res.order[i] = prims[i].idx;
+    return res;
+}
+
+}  // namespace rtamd

@@ -11,12 +11,13 @@
 #include <utility>
 #include <vector>
 
+#include "bvh_build.hpp"
 #include "device_layout.hpp"
 #include "host_scene.hpp"
 
 namespace rtamd {
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, bool lds, hipStream_t s);
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, hipStream_t s);
 hipError_t upload_srgb_table(const double* avg255);
 }  // namespace rtamd
 
@@ -178,6 +179,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (s->background_kind != RT_BG_SOLID)
         return fail(c, RT_E_UNSUPPORTED, "only SolidColorBackground is implemented on the device path");
     std::vector<DevSphere> spheres;
+    std::vector<double> sx, sy, sz, srad;
     std::vector<int32_t> sphere_obj, plane_obj;
     std::vector<DevPlane> planes;
     std::vector<DevMaterial> mats(s->objects.size());
@@ -189,6 +191,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
         if (o.shape == RT_SHAPE_SPHERE) {
             spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
             sphere_obj.push_back(static_cast<int32_t>(i));
+            sx.push_back(o.geom[0]); sy.push_back(o.geom[1]); sz.push_back(o.geom[2]); srad.push_back(o.geom[3]);
         } else if (o.shape == RT_SHAPE_PLANE) {
             planes.push_back(DevPlane{o.geom[0], o.geom[1], o.geom[2], o.geom[3], o.geom[4], o.geom[5]});
             plane_obj.push_back(static_cast<int32_t>(i));
@@ -216,7 +219,23 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
         d.kind = l.kind;
         lights.push_back(d);
     }
-    // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights], 256-B aligned pieces.
+    // Sphere BVH; spheres (and their object ids) are stored in its leaf order.
+    // Box padding scales with the largest sphere-box coordinate (BVH exactness).
+    double extent = 0.0;
+    for (size_t k = 0; k < spheres.size(); ++k) {
+        const double r = std::fabs(srad[k]);
+        for (double v : {sx[k] - r, sx[k] + r, sy[k] - r, sy[k] + r, sz[k] - r, sz[k] + r})
+            if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
+    }
+    BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, 1e-5 * (1.0 + extent));
+    {
+        std::vector<DevSphere> s2(spheres.size());
+        std::vector<int32_t> o2(spheres.size());
+        for (size_t k = 0; k < spheres.size(); ++k) { s2[k] = spheres[bvh.order[k]]; o2[k] = sphere_obj[bvh.order[k]]; }
+        spheres.swap(s2);
+        sphere_obj.swap(o2);
+    }
+    // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights][bvh], 256-B aligned pieces.
     size_t off = 0;
     auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
     const size_t o_sph = place(spheres.size() * sizeof(DevSphere));
@@ -225,6 +244,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_pobj = place(plane_obj.size() * sizeof(int32_t));
     const size_t o_mat = place(mats.size() * sizeof(DevMaterial));
     const size_t o_li = place(lights.size() * sizeof(DevLight));
+    const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
     const size_t total = off ? off : 256;
     std::vector<uint8_t> host(total, 0);
     auto put = [&](size_t at, const void* p, size_t bytes) { if (bytes) std::memcpy(host.data() + at, p, bytes); };
@@ -234,6 +254,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_pobj, plane_obj.data(), plane_obj.size() * sizeof(int32_t));
     put(o_mat, mats.data(), mats.size() * sizeof(DevMaterial));
     put(o_li, lights.data(), lights.size() * sizeof(DevLight));
+    put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
     if (!c->d_blob) {
@@ -250,11 +271,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.plane_obj = reinterpret_cast<const int32_t*>(base + o_pobj);
     d.mats = reinterpret_cast<const DevMaterial*>(base + o_mat);
     d.lights = reinterpret_cast<const DevLight*>(base + o_li);
-    d.bvh = nullptr;
+    d.bvh = reinterpret_cast<const DevBvhNode*>(base + o_bvh);
+    d.bvh_root = bvh.root;
     d.n_spheres = static_cast<int32_t>(spheres.size());
     d.n_planes = static_cast<int32_t>(planes.size());
     d.n_lights = static_cast<int32_t>(lights.size());
-    d.n_bvh = 0;
+    d.n_bvh = static_cast<int32_t>(bvh.nodes.size());
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
     for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
     d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;
@@ -280,7 +302,7 @@ static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_
     if (spp == 0) return fail(c, RT_E_INVALID, "spp must be set (the scene's antialias value for reference behaviour)");
     pitch = o->bgr_pitch ? o->bgr_pitch : 3 * o->tile_w;
     if (pitch < 3 * o->tile_w) return fail(c, RT_E_INVALID, "bgr_pitch < 3*tile_w");
-    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_WAVEFRONT) return fail(c, RT_E_INVALID, "bad algo");
+    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_WAVEFRONT_BRUTE) return fail(c, RT_E_INVALID, "bad algo");
     return RT_OK;
 }
 
@@ -312,13 +334,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     if (mode == RT_ALGO_AUTO) mode = c->dsc.n_lights <= 32 ? RT_ALGO_WAVEFRONT : (fits_lds ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL);
     if (mode == RT_ALGO_BRUTE_LDS && lds_bytes > 160 * 1024)
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
-    if (mode == RT_ALGO_WAVEFRONT && c->dsc.n_lights > 32)
+    if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)
         return fail(c, RT_E_UNSUPPORTED, "the wavefront path handles at most 32 lights");
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
     c->last_stream = st;
     if (o->tile_w == 0 || o->tile_h == 0) { c->last_timed = false; return RT_OK; }
-    if (mode == RT_ALGO_WAVEFRONT) {
+    if (mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) {
+        const int src = mode == RT_ALGO_WAVEFRONT ? 2 : (fits_lds ? 1 : 0);
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
@@ -336,7 +359,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             WfBufs b = c->wf;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
             HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), st));
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, fits_lds, st));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, st));
         }
         HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {

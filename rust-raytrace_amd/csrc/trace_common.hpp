@@ -146,6 +146,173 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
     return false;
 }
 
+// ------------------------------------------------------------------ BVH
+//
+// Culling must never skip a sphere the exact f64 test would report, or the
+// result would differ from the reference's linear scan.  Boxes are padded and
+// rounded outward on the host; here every slab interval is computed in f32
+// from the f32-rounded ray and then widened by a relative kBoxTol, which
+// covers the f32 rounding of origin, direction and slab arithmetic (each a few
+// ulps, relative to the t values they perturb).  Direction components below
+// 1e-20 are clamped (no 0 * inf NaNs); such a ray moves < 1e-14 along that
+// axis over any relevant t, far below the box padding.  DESIGN.md "BVH
+// exactness" has the argument in full.
+constexpr float kBoxTol = 1e-5f;
+constexpr int kBvhStack = 64;      // host builder bounds the depth (median splits past depth 40)
+
+struct RayBox {
+    float ox, oy, oz, ix, iy, iz;
+};
+
+__device__ __forceinline__ float inv_dir(double d) {
+    float f = static_cast<float>(d);
+    if (!(fabsf(f) >= 1e-20f)) f = copysignf(1e-20f, f);
+    return 1.0f / f;
+}
+
+__device__ __forceinline__ RayBox make_raybox(const Ray& r) {
+    return RayBox{static_cast<float>(r.ox), static_cast<float>(r.oy), static_cast<float>(r.oz),
+                  inv_dir(r.dx), inv_dir(r.dy), inv_dir(r.dz)};
+}
+
+// Conservative slab test; tlim = largest t still of interest.
+__device__ __forceinline__ bool box_hit(const float* lo, const float* hi, const RayBox& rb, float tlim, float& tnear) {
+    const float ax = (lo[0] - rb.ox) * rb.ix, bx = (hi[0] - rb.ox) * rb.ix;
+    const float ay = (lo[1] - rb.oy) * rb.iy, by = (hi[1] - rb.oy) * rb.iy;
+    const float az = (lo[2] - rb.oz) * rb.iz, bz = (hi[2] - rb.oz) * rb.iz;
+    float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    tn = tn - kBoxTol * fabsf(tn);
+    tf = tf + kBoxTol * fabsf(tf);
+    tnear = tn;
+    return tn <= tf && tf >= 0.0f && tn <= tlim;
+}
+
+// An f32 bound >= t (t >= 0 or +inf), for culling boxes that start beyond t.
+__device__ __forceinline__ float t_limit(double t) {
+    float f = static_cast<float>(t);
+    if (static_cast<double>(f) < t) f = __uint_as_float(__float_as_uint(f) + 1u);   // next f32 up (t >= 0)
+    return f + kBoxTol * f;
+}
+
+// Planes of the scene (always brute force: few, and they carry the NaN quirk).
+__device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) {
+    Hit h;
+    h.t = __builtin_huge_val();
+    h.obj = INT32_MAX;
+    h.prim = 0;
+    h.nan_t = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        const int32_t obj = sc.plane_obj[i];
+        if (t != t) {
+            if (!h.nan_t) { h.nan_t = true; h.t = t; h.obj = obj; h.prim = ~i; }
+        } else if (!h.nan_t && (t < h.t || (t == h.t && obj < h.obj))) {
+            h.t = t; h.obj = obj; h.prim = ~i;
+        }
+    }
+    return h;
+}
+
+// Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
+// compete on (t, object id), independent of visiting order.
+__device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    int32_t st_ptr[kBvhStack];
+    float st_t[kBvhStack];
+    int sp = 0;
+    int32_t cur = sc.bvh_root;
+    for (;;) {
+        if (cur >= 0) {
+            const DevBvhNode nd = sc.bvh[cur];
+            float t0, t1;
+            const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
+            const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                st_ptr[sp] = first0 ? nd.c1 : nd.c0;
+                st_t[sp] = first0 ? t1 : t0;
+                ++sp;
+                cur = first0 ? nd.c0 : nd.c1;
+                continue;
+            }
+            if (h0) { cur = nd.c0; continue; }
+            if (h1) { cur = nd.c1; continue; }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            for (int k = first; k < first + cnt; ++k) {
+                double t;
+                if (sphere_t(sc.spheres[k], r, a2, a4, t)) {
+                    const int32_t obj = sc.sphere_obj[k];
+                    if (t < h.t || (t == h.t && obj < h.obj)) {
+                        h.t = t; h.obj = obj; h.prim = k;
+                        tlim = t_limit(t);
+                    }
+                }
+            }
+        }
+        // pop, skipping entries that the current best already rules out
+        for (;;) {
+            if (sp == 0) return h;
+            --sp;
+            if (st_t[sp] <= tlim) break;
+        }
+        cur = st_ptr[sp];
+    }
+}
+
+// The shadow query (see occluded_brute for the any-hit equivalence).
+__device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, bool has_range, double r2) {
+    bool plane_block = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        if (!has_range) return true;
+        if (t != t) return false;
+        plane_block |= t * t < r2;
+    }
+    if (plane_block) return true;
+    if (sc.n_spheres == 0) return false;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
+    const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
+    int32_t st_ptr[kBvhStack];
+    int sp = 0;
+    int32_t cur = sc.bvh_root;
+    for (;;) {
+        if (cur >= 0) {
+            const DevBvhNode nd = sc.bvh[cur];
+            float t0, t1;
+            const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
+            const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
+            if (h0 && h1) {
+                const bool first0 = t0 <= t1;
+                st_ptr[sp++] = first0 ? nd.c1 : nd.c0;
+                cur = first0 ? nd.c0 : nd.c1;
+                continue;
+            }
+            if (h0) { cur = nd.c0; continue; }
+            if (h1) { cur = nd.c1; continue; }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            for (int k = first; k < first + cnt; ++k) {
+                double t;
+                if (sphere_t(sc.spheres[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+            }
+        }
+        if (sp == 0) return false;
+        cur = st_ptr[--sp];
+    }
+}
+
 // The surface normal the reference's intersect() returned for the winner:
 // sphere normalize(ray.cast(t) - center) (shapes.rs:61,66); plane: as in the
 // file (shapes.rs:108).  pt == ray.cast(t) bit-for-bit.

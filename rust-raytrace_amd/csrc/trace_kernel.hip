@@ -169,10 +169,30 @@ __device__ __forceinline__ bool entry_ray(const DevScene& sc, const FrameParams&
     return true;
 }
 
-template <bool kLds, bool kCam>
+// Sphere sources of the wavefront intersection kernels.
+constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
+constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
+constexpr int kSrcBvh = 2;          // BVH (conservative f32 boxes, exact f64 leaves)
+
+template <int kSrc>
+__device__ __forceinline__ Hit nearest_any(const DevScene& sc, const DevSphere* lds, const Ray& r) {
+    if constexpr (kSrc == kSrcBvh) return nearest_bvh(sc, r);
+    else if constexpr (kSrc == kSrcLds) return nearest_brute(sc, lds, r);
+    else return nearest_brute(sc, sc.spheres, r);
+}
+
+template <int kSrc>
+__device__ __forceinline__ bool occluded_any(const DevScene& sc, const DevSphere* lds, const Ray& r, bool has_range,
+                                             double r2) {
+    if constexpr (kSrc == kSrcBvh) return occluded_bvh(sc, r, has_range, r2);
+    else if constexpr (kSrc == kSrcLds) return occluded_brute(sc, lds, r, has_range, r2);
+    else return occluded_brute(sc, sc.spheres, r, has_range, r2);
+}
+
+template <int kSrc, bool kCam>
 __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
-    if constexpr (kLds) {
+    if constexpr (kSrc == kSrcLds) {
         for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
         __syncthreads();
     }
@@ -187,9 +207,7 @@ __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp
             if (!entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
                 b.hit_obj[i] = -2;                    // padding slot of a partial 8x8 tile
             } else {
-                Hit h;
-                if constexpr (kLds) h = nearest_brute(sc, static_cast<const DevSphere*>(lds_spheres), r);
-                else h = nearest_brute(sc, sc.spheres, r);
+                const Hit h = nearest_any<kSrc>(sc, lds_spheres, r);
                 b.hit_t[i] = h.t;
                 b.hit_obj[i] = h.obj;
                 b.hit_prim[i] = h.prim;
@@ -207,10 +225,10 @@ __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp
     }
 }
 
-template <bool kLds, bool kCam>
+template <int kSrc, bool kCam>
 __global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
-    if constexpr (kLds) {
+    if constexpr (kSrc == kSrcLds) {
         for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
         __syncthreads();
     }
@@ -228,9 +246,7 @@ __global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams 
             double lx, ly, lz, r2;
             const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
             const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-            bool occ;
-            if constexpr (kLds) occ = occluded_brute(sc, static_cast<const DevSphere*>(lds_spheres), sray, has_range, r2);
-            else occ = occluded_brute(sc, sc.spheres, sray, has_range, r2);
+            const bool occ = occluded_any<kSrc>(sc, lds_spheres, sray, has_range, r2);
             mask |= static_cast<uint32_t>(occ) << l;
         }
         b.occ[j] = mask;
@@ -354,30 +370,30 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 
 // One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
 // must be zero on entry (the caller memsets them).
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, bool lds, hipStream_t s) {
-    const size_t lds_bytes = lds ? static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere) : 0;
-    const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
+template <int kSrc>
+void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s) {
+    const size_t lds_bytes = kSrc == kSrcLds ? static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere) : 0;
     const int gq = blocks_for(b.slots, 1024), gs = blocks_for(b.slots, 2048);
+    if (k == 0) {
+        hipLaunchKernelGGL((wf_nearest<kSrc, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_occlusion<kSrc, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+    } else {
+        hipLaunchKernelGGL((wf_nearest<kSrc, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_occlusion<kSrc, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+    }
+}
+
+// One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
+// must be zero on entry (the caller memsets them).  src: 0 brute/global,
+// 1 brute/LDS, 2 BVH.
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, hipStream_t s) {
+    const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
-        if (k == 0) {
-            if (lds) {
-                hipLaunchKernelGGL((wf_nearest<true, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-                hipLaunchKernelGGL((wf_occlusion<true, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-            } else {
-                hipLaunchKernelGGL((wf_nearest<false, true>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
-                hipLaunchKernelGGL((wf_occlusion<false, true>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
-            }
-            hipLaunchKernelGGL((wf_shade<true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-        } else {
-            if (lds) {
-                hipLaunchKernelGGL((wf_nearest<true, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-                hipLaunchKernelGGL((wf_occlusion<true, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-            } else {
-                hipLaunchKernelGGL((wf_nearest<false, false>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
-                hipLaunchKernelGGL((wf_occlusion<false, false>), dim3(gq), dim3(kBlock), 0, s, sc, fp, b, k);
-            }
-            hipLaunchKernelGGL((wf_shade<false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-        }
+        if (src == kSrcBvh) launch_generation<kSrcBvh>(sc, fp, b, k, s);
+        else if (src == kSrcLds) launch_generation<kSrcLds>(sc, fp, b, k, s);
+        else launch_generation<kSrcGlobal>(sc, fp, b, k, s);
     }
     hipLaunchKernelGGL(wf_fold, dim3(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048)), dim3(kBlock), 0, s,
                        sc, fp, b);

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-ALGOS = [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_BRUTE_LDS, lr.RT_ALGO_BRUTE_GLOBAL]
+ALGOS = [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE, lr.RT_ALGO_BRUTE_LDS, lr.RT_ALGO_BRUTE_GLOBAL]
 
 
 def gpu_render(ctx, spec, algo=lr.RT_ALGO_AUTO, **kw):
@@ -224,3 +224,57 @@ def test_render_without_scene_and_bad_opts():
             with pytest.raises(lr.RtError) as e:
                 ctx.render(lr.render_opts(8, 8, **bad))
             assert e.value.code == lr.RT_E_INVALID
+
+
+# ---- BVH culling must be conservative: adversarial scenes ------------------
+
+@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
+def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
+    """Odd image sizes put pixel centres exactly on the camera axes (direction
+    components exactly 0); 24 coincident spheres with different colours land in
+    different BVH leaves and must still resolve to the FIRST in file order."""
+    s = scenes.SceneSpec(width=33, height=31, max_depth=6, background=(0.1, 0.1, 0.2),
+                         camera={"ctor": "new", "position": (0, 0, 0), "look": (0, 0, -1), "up": (0, 1, 0),
+                                 "im_dist": 1.0})
+    rng = scenes.SplitMix64(77)
+    for k in range(24):
+        kd = (rng.uniform(0, 1), rng.uniform(0, 1), rng.uniform(0, 1))
+        s.sphere((0.0, 0.0, -6.0), 1.5, scenes.phong(kd, (0.3, 0.3, 0.3), 20.0, (0.01, 0.01, 0.01)))
+    for k in range(300):     # clutter so the duplicates spread over the tree
+        c = (rng.uniform(-6, 6), rng.uniform(-6, 6), rng.uniform(-20, -3))
+        s.sphere(c, rng.uniform(0.05, 0.5), scenes.phong((0.5, 0.5, 0.5), (0.4, 0.4, 0.4), 30.0, (0, 0, 0)))
+    # spheres exactly tangent to the axis rays and to each other
+    s.sphere((1.0, 0.0, -10.0), 1.0, scenes.phong((0.9, 0.2, 0.2), (0.5, 0.5, 0.5), 8.0, (0, 0, 0)))
+    s.sphere((-1.0, 0.0, -10.0), 1.0, scenes.phong((0.2, 0.9, 0.2), (0.5, 0.5, 0.5), 8.0, (0, 0, 0)))
+    s.point_light((0.0, 5.0, 0.0), (1, 1, 1))
+    s.directional_light((0.0, -1.0, 0.0), (0.3, 0.3, 0.3))
+    check_parity(gpu_ctx, s, algo)
+
+
+@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
+def test_extreme_sphere_sizes_and_far_plane_origins(gpu_ctx, algo):
+    s = scenes.config2(97, 61)
+    s.max_depth = 8
+    rng = scenes.SplitMix64(5)
+    for k in range(200):
+        c = (rng.uniform(-30, 30), rng.uniform(0.001, 4), rng.uniform(-60, 0))
+        s.sphere(c, 10 ** rng.uniform(-4, 0.3), scenes.phong((0.3, 0.6, 0.9), (0.6, 0.6, 0.6), 50.0, (0, 0, 0)))
+    s.sphere((0.0, -1e4 + 0.0, -5.0), 1e4, scenes.phong((0.2, 0.2, 0.2), (0.5, 0.5, 0.5), 5.0, (0, 0, 0)))
+    s.sphere((1e5, 3.0, -1e5), 2e3, scenes.phong((0.9, 0.9, 0.2), (0.2, 0.2, 0.2), 5.0, (0, 0, 0)))
+    check_parity(gpu_ctx, s, algo)
+
+
+def test_bvh_ten_thousand_spheres(gpu_ctx):
+    s = scenes.config4(96, 96)
+    check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+
+
+def test_bvh_matches_brute_force_bit_for_bit_full_frame(gpu_ctx):
+    """Headline scene, full 4096x4096: BVH and linear scan agree on every byte
+    and every ray (a size-independent property of conservative culling)."""
+    spec = scenes.config3()
+    a = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    b = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT_BRUTE)
+    assert np.array_equal(a[1], b[1])
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    assert a[2].rays == b[2].rays and a[2].shadow_rays == b[2].shadow_rays

@@ -144,7 +144,20 @@ def main():
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
 
-    t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms], dtype=torch.float64, device=dev)
+    # one more, untimed frame with the instrumented kernels: exact box / sphere test counts
+    work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+                          max_depth=args.depth, spp=1, algo=algo,
+                          flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK)
+    ctx.render_device(work, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    wst = ctx.stats()
+    try:
+        gen_q, gen_s = ctx.generation_counts()
+    except lr.RtError:
+        gen_q, gen_s = [], []
+
+    t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms, float(wst.sphere_tests), float(wst.box_tests)],
+                     dtype=torch.float64, device=dev)
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -152,8 +165,10 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, avg_kernel_ms = mx[0].item(), mx[2].item()
         total_rays = int(sm[1].item())
+        sphere_tests, box_tests = int(sm[3].item()), int(sm[4].item())
     else:
         total_rays = local_rays
+        sphere_tests, box_tests = wst.sphere_tests, wst.box_tests
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -177,9 +192,19 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
+                         "kernel": "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
+                                   "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
-                         "note": "VALU(f64)-bound path; HBM fraction reported because the metric asks for it"},
+                         "note": "VALU-bound path (f64 exact tests, f32 BVH boxes); HBM fraction reported "
+                                 "because the metric asks for it; see 'compute'"},
+            "compute": {"bound": "valu", "sphere_tests_per_frame": sphere_tests, "box_tests_per_frame": box_tests,
+                        "f64_flops_per_sphere_test": 19, "f32_flops_per_box_test": 20,
+                        "achieved_f64_tflops": round(sphere_tests * 19 / (avg_kernel_ms * 1e-3) / 1e12 * world, 3),
+                        "achieved_f32_box_tflops": round(box_tests * 20 / (avg_kernel_ms * 1e-3) / 1e12 * world, 3),
+                        "peak_f64_tflops": FP64_VALU_PEAK_TFLOPS,
+                        "tests_per_ray": round((sphere_tests + box_tests) / max(1, total_rays), 2),
+                        "generation_queue_sizes": gen_q[:args.depth + 3] if world == 1 else None,
+                        "generation_shaded": gen_s[:args.depth + 3] if world == 1 else None},
         }
         if world == 1 and not args.no_cpu:
             try:

@@ -137,7 +137,11 @@ const char* rt_last_error(const rt_ctx* ctx);
 int rt_scene_upload(rt_ctx* ctx, const rt_scene* scene);
 
 enum rt_jitter { RT_JITTER_CENTER = 0 };   /* jx = jy = 0.5 (deterministic parity mode, main.rs:51-52) */
-enum rt_out_flags { RT_OUT_RGB_F32 = 1, RT_OUT_BGR_U8 = 2 };
+enum rt_out_flags {
+    RT_OUT_RGB_F32 = 1,
+    RT_OUT_BGR_U8 = 2,
+    RT_COUNT_WORK = 4          /* also count box / sphere tests (instrumented kernels; wavefront only) */
+};
 enum rt_algo {
     RT_ALGO_AUTO = 0,
     RT_ALGO_BRUTE_LDS = 1,      /* megakernel, sphere list staged in LDS */
@@ -166,7 +170,10 @@ typedef struct {
     uint64_t rays;            /* every Scene::intersect query issued (camera + reflection + shadow) */
     uint64_t shadow_rays;
     uint64_t pixels;
-    double kernel_ms;         /* hipEvent time of the trace kernel */
+    double kernel_ms;         /* hipEvent time from the first to the last launch of the render */
+    uint64_t box_tests;       /* RT_COUNT_WORK only: BVH slab tests (2 per inner node visited) */
+    uint64_t sphere_tests;    /* RT_COUNT_WORK only: exact ray-sphere quadratics evaluated */
+    uint64_t shadow_box_tests, shadow_sphere_tests;   /* the shadow-query share of the two above */
 } rt_stats;
 
 void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height);
@@ -178,6 +185,10 @@ int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* 
  * render are read with rt_ctx_stats (which synchronises). */
 int rt_render_device(rt_ctx* ctx, const rt_render_opts* opts, void* d_rgb, void* d_bgr, void* stream);
 int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
+/* Queue sizes of the last wavefront chunk: queue[k] = rays traced at depth k
+ * (generation 0: 0, the camera rays are not queued), shaded[k] = hits that
+ * issued shadow queries.  Diagnostic. */
+int rt_ctx_generation_counts(rt_ctx* ctx, uint32_t* queue, uint32_t* shaded, int n);
 
 #ifdef __cplusplus
 }

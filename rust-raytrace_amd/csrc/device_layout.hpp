@@ -95,7 +95,8 @@ struct WfBufs {
     double* term[3];                // terminal colour of each pixel's chain
     uint8_t* nlev;                  // levels pushed per pixel
     uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: |shade list_k|
-    unsigned long long* totals;     // [0] nearest queries, [1] shadow queries (accumulated over chunks)
+    unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
+                                    // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     uint32_t cap;                   // pixel capacity (stack stride)
     uint32_t slots;                 // generation-0 slots (8x8-tiled, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk

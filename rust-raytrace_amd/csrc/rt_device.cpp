@@ -17,7 +17,8 @@
 
 namespace rtamd {
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, hipStream_t s);
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
+                            hipStream_t s);
 hipError_t upload_srgb_table(const double* avg255);
 }  // namespace rtamd
 
@@ -67,8 +68,8 @@ int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // counters: [0, 256) rays per shard (megakernel), [256, 512) shadow rays per
-// shard, [512] nearest queries and [513] shadow queries (wavefront totals)
-constexpr int kCounterWords = 2 * kCounterShards + 2;
+// shard, [512..] wavefront totals (see WfBufs::totals)
+constexpr int kCounterWords = 2 * kCounterShards + 8;
 
 uint32_t wf_chunk_pixels() {
     const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
@@ -359,7 +360,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             WfBufs b = c->wf;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
             HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), st));
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, st));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, (o->flags & RT_COUNT_WORK) != 0, st));
         }
         HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {
@@ -382,6 +383,10 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     for (int i = 0; i < kCounterShards; ++i) { s->rays += h[i]; s->shadow_rays += h[kCounterShards + i]; }
     s->rays += h[2 * kCounterShards] + h[2 * kCounterShards + 1];
     s->shadow_rays += h[2 * kCounterShards + 1];
+    s->box_tests = h[2 * kCounterShards + 2] + h[2 * kCounterShards + 4];
+    s->sphere_tests = h[2 * kCounterShards + 3] + h[2 * kCounterShards + 5];
+    s->shadow_box_tests = h[2 * kCounterShards + 4];
+    s->shadow_sphere_tests = h[2 * kCounterShards + 5];
     s->pixels = c->last_pixels;
     if (c->last_timed) {
         float ms = 0.f;
@@ -389,6 +394,18 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
         HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         s->kernel_ms = ms;
     }
+    return RT_OK;
+}
+
+int rt_ctx_generation_counts(rt_ctx* c, uint32_t* queue, uint32_t* shaded, int n) {
+    if (!c || n < 0 || (n && (!queue || !shaded))) return RT_E_INVALID;
+    if (!c->wf_mem) return fail(c, RT_E_NOSCENE, "no wavefront render yet");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
+    uint32_t h[kCntWords];
+    HIP_TRY(c, hipMemcpyAsync(h, c->wf.cnt, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < n && k < kCntS; ++k) { queue[k] = h[kCntQ + k]; shaded[k] = h[kCntS + k]; }
     return RT_OK;
 }
 

@@ -82,8 +82,14 @@ __device__ __forceinline__ bool plane_t(const DevPlane& p, const Ray& r, double&
 // min_by_key(FloatNotNan(t)): a NaN t (only a plane can produce one) is the
 // minimum key and the first in file order wins outright; otherwise smallest t,
 // ties to the FIRST object in file order.
-template <class SpherePtr>
-__device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, const Ray& r) {
+// Work counters (only in the kCount instantiations): boxes = slab tests,
+// spheres = exact quadratic tests.
+struct Work {
+    uint32_t boxes = 0, spheres = 0;
+};
+
+template <bool kCount = false, class SpherePtr>
+__device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, const Ray& r, Work* w = nullptr) {
     Hit h;
     h.t = __builtin_huge_val();
     h.obj = INT32_MAX;
@@ -103,6 +109,7 @@ __device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, co
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;     // direction.sqnorm()
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const int n = sc.n_spheres;
+    if constexpr (kCount) w->spheres += n;
 #pragma unroll 2
     for (int i = 0; i < n; ++i) {
         const DevSphere s = S[i];
@@ -122,8 +129,9 @@ __device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, co
 //    is that NaN hit and NaN*NaN < r2 is false -> lit; otherwise shadowed iff
 //    SOME hit has t*t < r2 (t_min <= t_i and rounding is monotone, so the
 //    nearest one then qualifies too).
-template <class SpherePtr>
-__device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, const Ray& r, bool has_range, double r2) {
+template <bool kCount = false, class SpherePtr>
+__device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, const Ray& r, bool has_range, double r2,
+                                               Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -139,6 +147,7 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
     for (int i = 0; i < n; ++i) {
         const DevSphere s = S[i];
         double t;
+        if constexpr (kCount) ++w->spheres;
         if (sphere_t(s, r, a2, a4, t)) {
             if (!has_range || t * t < r2) return true;
         }
@@ -217,7 +226,8 @@ __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) 
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
-__device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r) {
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
@@ -231,6 +241,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r) {
     for (;;) {
         if (cur >= 0) {
             const DevBvhNode nd = sc.bvh[cur];
+            if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
@@ -246,6 +257,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r) {
             if (h1) { cur = nd.c1; continue; }
         } else {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
                 if (sphere_t(sc.spheres[k], r, a2, a4, t)) {
@@ -268,7 +280,9 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r) {
 }
 
 // The shadow query (see occluded_brute for the any-hit equivalence).
-__device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, bool has_range, double r2) {
+template <bool kCount = false>
+__device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, bool has_range, double r2,
+                                             Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -290,6 +304,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, b
     for (;;) {
         if (cur >= 0) {
             const DevBvhNode nd = sc.bvh[cur];
+            if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
@@ -303,6 +318,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, b
             if (h1) { cur = nd.c1; continue; }
         } else {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
                 if (sphere_t(sc.spheres[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;

@@ -174,23 +174,40 @@ constexpr int kSrcGlobal = 0;       // brute force, sphere list through the cach
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
 constexpr int kSrcBvh = 2;          // BVH (conservative f32 boxes, exact f64 leaves)
 
-template <int kSrc>
-__device__ __forceinline__ Hit nearest_any(const DevScene& sc, const DevSphere* lds, const Ray& r) {
-    if constexpr (kSrc == kSrcBvh) return nearest_bvh(sc, r);
-    else if constexpr (kSrc == kSrcLds) return nearest_brute(sc, lds, r);
-    else return nearest_brute(sc, sc.spheres, r);
+template <int kSrc, bool kCount>
+__device__ __forceinline__ Hit nearest_any(const DevScene& sc, const DevSphere* lds, const Ray& r, Work* w) {
+    if constexpr (kSrc == kSrcBvh) return nearest_bvh<kCount>(sc, r, w);
+    else if constexpr (kSrc == kSrcLds) return nearest_brute<kCount>(sc, lds, r, w);
+    else return nearest_brute<kCount>(sc, sc.spheres, r, w);
 }
 
-template <int kSrc>
+template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const DevSphere* lds, const Ray& r, bool has_range,
-                                             double r2) {
-    if constexpr (kSrc == kSrcBvh) return occluded_bvh(sc, r, has_range, r2);
-    else if constexpr (kSrc == kSrcLds) return occluded_brute(sc, lds, r, has_range, r2);
-    else return occluded_brute(sc, sc.spheres, r, has_range, r2);
+                                             double r2, Work* w) {
+    if constexpr (kSrc == kSrcBvh) return occluded_bvh<kCount>(sc, r, has_range, r2, w);
+    else if constexpr (kSrc == kSrcLds) return occluded_brute<kCount>(sc, lds, r, has_range, r2, w);
+    else return occluded_brute<kCount>(sc, sc.spheres, r, has_range, r2, w);
 }
 
-template <int kSrc, bool kCam>
+// One atomic per wave into totals[at], totals[at + 1].
+template <bool kCount>
+__device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
+    if constexpr (kCount) {
+        unsigned long long bx = w.boxes, sp = w.spheres;
+        for (int off = 32; off > 0; off >>= 1) {
+            bx += __shfl_xor(bx, off, 64);
+            sp += __shfl_xor(sp, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&b.totals[at], bx);
+            atomicAdd(&b.totals[at + 1], sp);
+        }
+    }
+}
+
+template <int kSrc, bool kCam, bool kCount>
 __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    Work w;
     extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
     if constexpr (kSrc == kSrcLds) {
         for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
@@ -207,7 +224,7 @@ __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp
             if (!entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
                 b.hit_obj[i] = -2;                    // padding slot of a partial 8x8 tile
             } else {
-                const Hit h = nearest_any<kSrc>(sc, lds_spheres, r);
+                const Hit h = nearest_any<kSrc, kCount>(sc, lds_spheres, r, &w);
                 b.hit_t[i] = h.t;
                 b.hit_obj[i] = h.obj;
                 b.hit_prim[i] = h.prim;
@@ -223,10 +240,12 @@ __global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp
             if (shade) b.shade_list[slot] = i;
         }
     }
+    flush_work<kCount>(b, 2, w);
 }
 
-template <int kSrc, bool kCam>
+template <int kSrc, bool kCam, bool kCount>
 __global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    Work w;
     extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
     if constexpr (kSrc == kSrcLds) {
         for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
@@ -246,28 +265,36 @@ __global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams 
             double lx, ly, lz, r2;
             const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
             const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-            const bool occ = occluded_any<kSrc>(sc, lds_spheres, sray, has_range, r2);
+            const bool occ = occluded_any<kSrc, kCount>(sc, lds_spheres, sray, has_range, r2, &w);
             mask |= static_cast<uint32_t>(occ) << l;
         }
         b.occ[j] = mask;
     }
+    flush_work<kCount>(b, 4, w);
 }
 
-template <bool kCam>
+// Shading of generation k, in two dense passes:
+//   kList = true : the shade list (hits that evaluate lights; the heavy part:
+//                  normals, light directions, pow) -- every lane busy;
+//   kList = false: every other queue entry (misses, depth cut-offs, hits whose
+//                  significance switched lighting off) -- cheap.
+template <bool kCam, bool kList>
 __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    const uint32_t n = kCam ? b.slots : b.cnt[kCntQ + k];
+    const uint32_t n = kList ? b.cnt[kCntS + k] : (kCam ? b.slots : b.cnt[kCntQ + k]);
     const int qn = (k + 1) & 1;
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-        const uint32_t i = base + threadIdx.x;
+        const uint32_t j = base + threadIdx.x;
         bool refl = false;
         Ray rr{};
         double nsig = 0.0;
         uint32_t p = 0;
-        if (i < n) {
+        if (j < n) {
+            const uint32_t i = kList ? b.shade_list[j] : j;
             const int32_t obj = b.hit_obj[i];
             Ray r;
             double sig;
-            if (obj != -2 && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
+            const bool mine = kList || b.shade_slot[i] < 0;
+            if (mine && obj != -2 && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
                 Col res;
                 bool done = true;
                 if (obj == INT32_MAX) {
@@ -278,29 +305,31 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
                     if (static_cast<uint32_t>(k) <= fp.max_depth) {          // raytrace.rs:33
                         const double t = b.hit_t[i];
                         const double ptx = r.ox + r.dx * t, pty = r.oy + r.dy * t, ptz = r.oz + r.dz * t;
-                        double nx, ny, nz;
-                        hit_normal(sc, sc.spheres, b.hit_prim[i], ptx, pty, ptz, nx, ny, nz);
                         const bool diffuse = m.kd_sig * sig > kMinSignificance;
                         const bool specular = m.ks_sig * sig > kMinSignificance;
-                        if (nx * r.dx + ny * r.dy + nz * r.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
-                        if ((diffuse || specular) && sc.n_lights > 0) {
-                            const uint32_t mask = b.occ[b.shade_slot[i]];
-                            for (int l = 0; l < sc.n_lights; ++l) {
-                                if ((mask >> l) & 1u) continue;              // shadowed (raytrace.rs:42-49)
-                                const DevLight& L = sc.lights[l];
-                                double lx, ly, lz, r2;
-                                light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
-                                add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, r.dx, r.dy, r.dz);
+                        if (kList || specular) {
+                            double nx, ny, nz;
+                            hit_normal(sc, sc.spheres, b.hit_prim[i], ptx, pty, ptz, nx, ny, nz);
+                            if (nx * r.dx + ny * r.dy + nz * r.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+                            if (kList) {                                     // diffuse || specular, lights > 0
+                                const uint32_t mask = b.occ[j];
+                                for (int l = 0; l < sc.n_lights; ++l) {
+                                    if ((mask >> l) & 1u) continue;          // shadowed (raytrace.rs:42-49)
+                                    const DevLight& L = sc.lights[l];
+                                    double lx, ly, lz, r2;
+                                    light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
+                                    add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, r.dx, r.dy, r.dz);
+                                }
                             }
-                        }
-                        if (specular) {                                      // raytrace.rs:58-64
-                            const size_t at = static_cast<size_t>(k) * b.cap + p;
-                            b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
-                            b.st_obj[at] = obj;
-                            rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
-                            nsig = sig * m.ks_sig;
-                            refl = true;
-                            done = false;
+                            if (specular) {                                  // raytrace.rs:58-64
+                                const size_t at = static_cast<size_t>(k) * b.cap + p;
+                                b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
+                                b.st_obj[at] = obj;
+                                rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
+                                nsig = sig * m.ks_sig;
+                                refl = true;
+                                done = false;
+                            }
                         }
                     }
                 }
@@ -320,19 +349,54 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
     }
 }
 
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p) {
+    Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
+    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc (raytrace.rs:63)
+        const size_t at = static_cast<size_t>(k) * b.cap + p;
+        const DevMaterial& m = sc.mats[b.st_obj[at]];
+        acc.r = b.st[0][at] + m.ks[0] * acc.r;
+        acc.g = b.st[1][at] + m.ks[1] * acc.g;
+        acc.b = b.st[2][at] + m.ks[2] * acc.b;
+    }
+    return acc;
+}
+
+// kStaged: every group of 256 pixels lies in one output row (tile_w % 256 == 0,
+// BGR rows unpadded and dword aligned): the block assembles its 3 KiB of RGB
+// and 768 B of BGR in LDS and stores them as whole dwords.
+template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
+    __shared__ float s_rgb[3 * kBlock];
+    __shared__ uint32_t s_bgr[3 * kBlock / 4];
     const uint32_t npix = fp.tile_w * fp.rows;
-    for (uint32_t p = blockIdx.x * kBlock + threadIdx.x; p < npix; p += gridDim.x * kBlock) {
-        Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
-        for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {   // res_k + ks_k * acc (raytrace.rs:63)
-            const size_t at = static_cast<size_t>(k) * b.cap + p;
-            const DevMaterial& m = sc.mats[b.st_obj[at]];
-            acc.r = b.st[0][at] + m.ks[0] * acc.r;
-            acc.g = b.st[1][at] + m.ks[1] * acc.g;
-            acc.b = b.st[2][at] + m.ks[2] * acc.b;
+    for (uint32_t base = blockIdx.x * kBlock; base < npix; base += gridDim.x * kBlock) {
+        const uint32_t p = base + threadIdx.x;
+        if constexpr (!kStaged) {
+            if (p < npix) {
+                const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
+                write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res);
+            }
+        } else {
+            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
+            s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
+            s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
+            s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
+            uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr);
+            sb[3 * threadIdx.x + 0] = to_srgb(res.b);
+            sb[3 * threadIdx.x + 1] = to_srgb(res.g);
+            sb[3 * threadIdx.x + 2] = to_srgb(res.r);
+            __syncthreads();
+            const uint32_t row = fp.row0 + base / fp.tile_w, lx0 = base % fp.tile_w;
+            if (fp.out_rgb) {
+                float* dst = fp.out_rgb + (static_cast<size_t>(row) * fp.tile_w + lx0) * 3;
+                for (int q = threadIdx.x; q < 3 * kBlock; q += kBlock) dst[q] = s_rgb[q];
+            }
+            if (fp.out_bgr && threadIdx.x < 3 * kBlock / 4) {
+                uint32_t* dst = reinterpret_cast<uint32_t*>(fp.out_bgr + static_cast<size_t>(row) * fp.bgr_pitch + 3 * lx0);
+                dst[threadIdx.x] = s_bgr[threadIdx.x];
+            }
+            __syncthreads();
         }
-        const uint32_t lx = p % fp.tile_w, ly = p / fp.tile_w;
-        write_pixel(fp, lx, fp.row0 + ly, average_samples(acc, fp.spp));
     }
 }
 
@@ -370,33 +434,45 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 
 // One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
 // must be zero on entry (the caller memsets them).
-template <int kSrc>
+template <int kSrc, bool kCount>
 void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s) {
     const size_t lds_bytes = kSrc == kSrcLds ? static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere) : 0;
     const int gq = blocks_for(b.slots, 1024), gs = blocks_for(b.slots, 2048);
     if (k == 0) {
-        hipLaunchKernelGGL((wf_nearest<kSrc, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_occlusion<kSrc, true>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_occlusion<kSrc, true, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<true, true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<true, false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
     } else {
-        hipLaunchKernelGGL((wf_nearest<kSrc, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_occlusion<kSrc, false>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_occlusion<kSrc, false, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<false, true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+        hipLaunchKernelGGL((wf_shade<false, false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
     }
 }
 
 // One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
 // must be zero on entry (the caller memsets them).  src: 0 brute/global,
 // 1 brute/LDS, 2 BVH.
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, hipStream_t s) {
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
+                            hipStream_t s) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
-        if (src == kSrcBvh) launch_generation<kSrcBvh>(sc, fp, b, k, s);
-        else if (src == kSrcLds) launch_generation<kSrcLds>(sc, fp, b, k, s);
-        else launch_generation<kSrcGlobal>(sc, fp, b, k, s);
+        if (count) {
+            if (src == kSrcBvh) launch_generation<kSrcBvh, true>(sc, fp, b, k, s);
+            else if (src == kSrcLds) launch_generation<kSrcLds, true>(sc, fp, b, k, s);
+            else launch_generation<kSrcGlobal, true>(sc, fp, b, k, s);
+        } else {
+            if (src == kSrcBvh) launch_generation<kSrcBvh, false>(sc, fp, b, k, s);
+            else if (src == kSrcLds) launch_generation<kSrcLds, false>(sc, fp, b, k, s);
+            else launch_generation<kSrcGlobal, false>(sc, fp, b, k, s);
+        }
     }
-    hipLaunchKernelGGL(wf_fold, dim3(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048)), dim3(kBlock), 0, s,
-                       sc, fp, b);
+    const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
+                        (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
+    const dim3 gf(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048));
+    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(1), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }

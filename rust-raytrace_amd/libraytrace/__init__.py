@@ -27,7 +27,7 @@ RT_MAT_PHONG, RT_MAT_INDIRECT_PHONG, RT_MAT_FRESNEL, RT_MAT_TRANSPARENT = 0, 1, 
 RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AREA = 0, 1, 2
 RT_CAMERA_SIMPLE, RT_CAMERA_DOF = 0, 1
 RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
-RT_OUT_RGB_F32, RT_OUT_BGR_U8 = 1, 2
+RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK = 1, 2, 4
 RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL, RT_ALGO_WAVEFRONT, RT_ALGO_WAVEFRONT_BRUTE = 0, 1, 2, 3, 4
 RT_MAX_DEPTH_LIMIT = 30
 
@@ -74,7 +74,8 @@ class rt_render_opts(C.Structure):
 
 class rt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64),
-                ("kernel_ms", C.c_double)]
+                ("kernel_ms", C.c_double), ("box_tests", C.c_uint64), ("sphere_tests", C.c_uint64),
+                ("shadow_box_tests", C.c_uint64), ("shadow_sphere_tests", C.c_uint64)]
 
 
 def _load():
@@ -103,6 +104,7 @@ def _load():
         "rt_render": (C.c_int, [C.c_void_p, P(rt_render_opts), P(C.c_float), P(C.c_uint8), P(rt_stats)]),
         "rt_render_device": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_void_p, C.c_void_p, C.c_void_p]),
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
+        "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -256,6 +258,12 @@ class Context:
         st = rt_stats()
         _check(lib.rt_ctx_stats(self._h, C.byref(st)), self._h)
         return st
+
+    def generation_counts(self, n=34):
+        q = (C.c_uint32 * n)()
+        s = (C.c_uint32 * n)()
+        _check(lib.rt_ctx_generation_counts(self._h, q, s, n), self._h)
+        return list(q), list(s)
 
     def close(self):
         if self._h:

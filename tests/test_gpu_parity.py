@@ -278,3 +278,24 @@ def test_bvh_matches_brute_force_bit_for_bit_full_frame(gpu_ctx):
     assert np.array_equal(a[1], b[1])
     assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
     assert a[2].rays == b[2].rays and a[2].shadow_rays == b[2].shadow_rays
+
+
+def test_work_counters(gpu_ctx):
+    """RT_COUNT_WORK: identical image; brute force tests every sphere for every
+    nearest query; the BVH tests a subset."""
+    spec = scenes.config3(64, 48)
+    sc = lr.Scene.deserialize(spec.to_text())
+    gpu_ctx.upload(sc)
+    base = dict(max_depth=8, spp=1)
+    plain = gpu_ctx.render(lr.render_opts(64, 48, algo=lr.RT_ALGO_WAVEFRONT, **base))
+    counted = gpu_ctx.render(lr.render_opts(64, 48, algo=lr.RT_ALGO_WAVEFRONT, flags=7, **base))
+    assert np.array_equal(plain[1], counted[1]) and plain[2].rays == counted[2].rays
+    brute = gpu_ctx.render(lr.render_opts(64, 48, algo=lr.RT_ALGO_WAVEFRONT_BRUTE, flags=7, **base))[2]
+    nearest = brute.rays - brute.shadow_rays
+    assert brute.sphere_tests - brute.shadow_sphere_tests == nearest * 1000
+    assert brute.box_tests == 0
+    bvh = counted[2]
+    assert 0 < bvh.sphere_tests < brute.sphere_tests
+    assert bvh.box_tests > 0
+    q, s = gpu_ctx.generation_counts()
+    assert sum(q[1:]) + 64 * 48 == nearest

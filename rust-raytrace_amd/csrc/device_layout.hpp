@@ -84,22 +84,26 @@ struct WfBufs {
     double* qd[2][3];               // ray direction
     double* qsig[2];                // significance passed down (raytrace.rs:63)
     uint32_t* qpix[2];              // owning pixel (chunk-local index)
-    double* hit_t;                  // per queue entry of the current generation
-    int32_t* hit_obj;               // object id; INT32_MAX = miss; -2 = dead slot
-    int32_t* hit_prim;              // sphere index >= 0, ~plane index < 0
-    int32_t* shade_slot;            // index into shade_list, or -1
-    uint32_t* shade_list;           // queue entries that need light evaluation
-    uint32_t* occ;                  // per shade entry: bit l set = light l shadowed
+    // Shade records of the current generation: the hits that go on to light
+    // evaluation and/or reflection, written densely by wf_nearest.
+    double* sr_pt[3];               // hit point ray.cast(t)
+    double* sr_d[3];                // incoming direction
+    double* sr_sig;                 // significance
+    int32_t* sr_obj;                // object id
+    int32_t* sr_prim;               // sphere index >= 0, ~plane index < 0
+    uint32_t* sr_pix;               // owning pixel
+    uint32_t* occ;                  // per shade record: bit l set = light l shadowed
     double* st[3];                  // per-level local colour, [level * cap + p]
     int32_t* st_obj;                // per-level object id (its specular colour is the fold factor)
     double* term[3];                // terminal colour of each pixel's chain
     uint8_t* nlev;                  // levels pushed per pixel
-    uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: |shade list_k|
+    uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: shade records of generation k
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     uint32_t cap;                   // pixel capacity (stack stride)
     uint32_t slots;                 // generation-0 slots (8x8-tiled, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
+    int32_t lds_nodes;              // BVH nodes (breadth-first prefix) staged in LDS by the BVH kernels
 };
 
 constexpr int kCntQ = 0;

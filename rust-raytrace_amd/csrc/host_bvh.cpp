@@ -166,6 +166,27 @@ BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<doub
     res.nodes.reserve(2 * n / kLeafMax + 2);
     Builder bld{prims, res.nodes, pad};
     res.root = bld.build(0, static_cast<int>(n), 0);
+    // Renumber breadth-first so the top levels are a prefix of the array: the
+    // traversal kernels keep the first nodes that fit in LDS.
+    if (res.root >= 0 && !res.nodes.empty()) {
+        std::vector<int32_t> order, remap(res.nodes.size(), -1);
+        order.reserve(res.nodes.size());
+        order.push_back(res.root);
+        for (size_t h = 0; h < order.size(); ++h) {
+            const BvhNodeHost& nd = res.nodes[order[h]];
+            if (nd.c0 >= 0) order.push_back(nd.c0);
+            if (nd.c1 >= 0) order.push_back(nd.c1);
+        }
+        for (size_t k = 0; k < order.size(); ++k) remap[order[k]] = static_cast<int32_t>(k);
+        std::vector<BvhNodeHost> bfs(order.size());
+        for (size_t k = 0; k < order.size(); ++k) {
+            bfs[k] = res.nodes[order[k]];
+            if (bfs[k].c0 >= 0) bfs[k].c0 = remap[bfs[k].c0];
+            if (bfs[k].c1 >= 0) bfs[k].c1 = remap[bfs[k].c1];
+        }
+        res.nodes.swap(bfs);
+        res.root = 0;
+    }
     res.order.resize(n);
     for (size_t i = 0; i < n; ++i) res.order[i] = prims[i].idx;
     return res;

@@ -91,11 +91,12 @@ int ensure_wf(rt_ctx* c, uint32_t cap, uint32_t slots, uint32_t levels) {
         add(reinterpret_cast<void**>(&b.qsig[g]), q * 8);
         add(reinterpret_cast<void**>(&b.qpix[g]), q * 4);
     }
-    add(reinterpret_cast<void**>(&b.hit_t), q * 8);
-    add(reinterpret_cast<void**>(&b.hit_obj), q * 4);
-    add(reinterpret_cast<void**>(&b.hit_prim), q * 4);
-    add(reinterpret_cast<void**>(&b.shade_slot), q * 4);
-    add(reinterpret_cast<void**>(&b.shade_list), q * 4);
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_pt[a]), q * 8);
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_d[a]), q * 8);
+    add(reinterpret_cast<void**>(&b.sr_sig), q * 8);
+    add(reinterpret_cast<void**>(&b.sr_obj), q * 4);
+    add(reinterpret_cast<void**>(&b.sr_prim), q * 4);
+    add(reinterpret_cast<void**>(&b.sr_pix), q * 4);
     add(reinterpret_cast<void**>(&b.occ), q * 4);
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.st[a]), static_cast<size_t>(levels) * cap * 8);
     add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
@@ -342,7 +343,25 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     c->last_stream = st;
     if (o->tile_w == 0 || o->tile_h == 0) { c->last_timed = false; return RT_OK; }
     if (mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) {
-        const int src = mode == RT_ALGO_WAVEFRONT ? 2 : (fits_lds ? 1 : 0);
+        // LDS per traversal workgroup (1024 threads, two resident per CU): the
+        // whole BVH + sphere list when they fit, else the top of the tree.
+        constexpr size_t kLdsBudget = 72 * 1024;
+        const size_t node_bytes = static_cast<size_t>(c->dsc.n_bvh) * sizeof(DevBvhNode);
+        const size_t sph_bytes = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
+        int src;
+        int32_t lds_nodes = 0;
+        const char* force = std::getenv("RT_WF_SRC");          // experiment override: 2 or 3
+        if (mode == RT_ALGO_WAVEFRONT) {
+            const bool all = node_bytes + sph_bytes <= kLdsBudget && !(force && std::atoi(force) == 2);
+            if (all) { src = 3; lds_nodes = c->dsc.n_bvh; }
+            else {
+                // top of the tree only (256-thread groups): <= 32 KB keeps 5 groups per CU
+                src = 2;
+                lds_nodes = static_cast<int32_t>(std::min<size_t>(c->dsc.n_bvh, 32 * 1024 / sizeof(DevBvhNode)));
+            }
+        } else {
+            src = fits_lds ? 1 : 0;
+        }
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
@@ -352,6 +371,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         int rc2 = ensure_wf(c, cap, slots, o->max_depth + 1);
         if (rc2 != RT_OK) return rc2;
         c->wf.tiles_x = tiles_x;
+        c->wf.lds_nodes = lds_nodes;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         for (uint32_t r0 = 0; r0 < o->tile_h; r0 += chunk_rows) {
             FrameParams f = fp;
@@ -416,7 +436,7 @@ int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_b
     if (rc != RT_OK) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     rt_render_opts oo = *o;
-    oo.flags = (out_rgb ? RT_OUT_RGB_F32 : 0) | (out_bgr ? RT_OUT_BGR_U8 : 0);
+    oo.flags = (o->flags & ~(RT_OUT_RGB_F32 | RT_OUT_BGR_U8)) | (out_rgb ? RT_OUT_RGB_F32 : 0) | (out_bgr ? RT_OUT_BGR_U8 : 0);
     const size_t rgb_bytes = static_cast<size_t>(o->tile_w) * o->tile_h * 3 * sizeof(float);
     const size_t bgr_bytes = static_cast<size_t>(pitch) * o->tile_h;
     if (out_rgb && rgb_bytes > c->rgb_cap) {

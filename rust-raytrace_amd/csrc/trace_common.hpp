@@ -224,32 +224,93 @@ __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) 
     return h;
 }
 
+// Where the traversal reads its data: the first `nl` BVH nodes (breadth-first
+// order, i.e. the top of the tree) from an LDS copy, the rest from HBM/L2;
+// spheres and their object ids from LDS when the whole list fits, else HBM.
+struct BvhView {
+    const DevBvhNode* lnodes;
+    int32_t nl;
+    const DevBvhNode* gnodes;
+    const DevSphere* sph;
+    const int32_t* obj;
+};
+
+template <bool kAllLds>
+__device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
+    if constexpr (kAllLds) {
+        return v.lnodes[i];
+    } else {
+        if (i < v.nl) return v.lnodes[i];
+        return v.gnodes[i];
+    }
+}
+
+// Traversal stack: the top kRegStack entries live in registers (shifted with
+// v_mov on push/pop, no memory latency); deeper entries spill to a private
+// array.  The host bounds the tree depth, so kBvhStack entries always suffice.
+constexpr int kRegStack = 8;
+
+template <bool kWithT>
+struct ShortStack {
+    int32_t p[kRegStack];
+    float t[kRegStack];
+    int32_t sp[kBvhStack - kRegStack];
+    float st[kBvhStack - kRegStack];
+    int n = 0;
+
+    __device__ __forceinline__ void push(int32_t v, float tv) {
+        if (n >= kRegStack) {
+            sp[n - kRegStack] = p[kRegStack - 1];
+            if constexpr (kWithT) st[n - kRegStack] = t[kRegStack - 1];
+        }
+#pragma unroll
+        for (int k = kRegStack - 1; k > 0; --k) {
+            p[k] = p[k - 1];
+            if constexpr (kWithT) t[k] = t[k - 1];
+        }
+        p[0] = v;
+        if constexpr (kWithT) t[0] = tv;
+        ++n;
+    }
+    __device__ __forceinline__ int32_t pop(float& tv) {
+        const int32_t v = p[0];
+        if constexpr (kWithT) tv = t[0];
+#pragma unroll
+        for (int k = 0; k < kRegStack - 1; ++k) {
+            p[k] = p[k + 1];
+            if constexpr (kWithT) t[k] = t[k + 1];
+        }
+        --n;
+        if (n >= kRegStack) {
+            p[kRegStack - 1] = sp[n - kRegStack];
+            if constexpr (kWithT) t[kRegStack - 1] = st[n - kRegStack];
+        }
+        return v;
+    }
+};
+
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r, Work* w = nullptr) {
+template <bool kCount = false, bool kAllLds = false>
+__device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    int32_t st_ptr[kBvhStack];
-    float st_t[kBvhStack];
-    int sp = 0;
+    ShortStack<true> stk;
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
-            const DevBvhNode nd = sc.bvh[cur];
+            const DevBvhNode nd = fetch_node<kAllLds>(v, cur);
             if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                st_ptr[sp] = first0 ? nd.c1 : nd.c0;
-                st_t[sp] = first0 ? t1 : t0;
-                ++sp;
+                stk.push(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -260,8 +321,8 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r, Wor
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(sc.spheres[k], r, a2, a4, t)) {
-                    const int32_t obj = sc.sphere_obj[k];
+                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                    const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
                         tlim = t_limit(t);
@@ -270,19 +331,19 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const Ray& r, Wor
             }
         }
         // pop, skipping entries that the current best already rules out
+        float tn = 0.0f;
         for (;;) {
-            if (sp == 0) return h;
-            --sp;
-            if (st_t[sp] <= tlim) break;
+            if (stk.n == 0) return h;
+            cur = stk.pop(tn);
+            if (tn <= tlim) break;
         }
-        cur = st_ptr[sp];
     }
 }
 
 // The shadow query (see occluded_brute for the any-hit equivalence).
-template <bool kCount = false>
-__device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, bool has_range, double r2,
-                                             Work* w = nullptr) {
+template <bool kCount = false, bool kAllLds = false>
+__device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
+                                             double r2, Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -298,19 +359,18 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, b
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
-    int32_t st_ptr[kBvhStack];
-    int sp = 0;
+    ShortStack<false> stk;
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
-            const DevBvhNode nd = sc.bvh[cur];
+            const DevBvhNode nd = fetch_node<kAllLds>(v, cur);
             if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                st_ptr[sp++] = first0 ? nd.c1 : nd.c0;
+                stk.push(first0 ? nd.c1 : nd.c0, 0.0f);
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -321,11 +381,12 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const Ray& r, b
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(sc.spheres[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+                if (sphere_t(v.sph[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
             }
         }
-        if (sp == 0) return false;
-        cur = st_ptr[--sp];
+        if (stk.n == 0) return false;
+        float tn;
+        cur = stk.pop(tn);
     }
 }
 

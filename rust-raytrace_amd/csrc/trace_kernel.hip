@@ -22,6 +22,7 @@
 //    path length, small kernels, high occupancy.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -172,21 +173,52 @@ __device__ __forceinline__ bool entry_ray(const DevScene& sc, const FrameParams&
 // Sphere sources of the wavefront intersection kernels.
 constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
-constexpr int kSrcBvh = 2;          // BVH (conservative f32 boxes, exact f64 leaves)
+constexpr int kSrcBvh = 2;          // BVH: top of the tree in LDS, spheres through the caches
+constexpr int kSrcBvhLds = 3;       // BVH: top of the tree and every sphere in LDS
 
-template <int kSrc, bool kCount>
-__device__ __forceinline__ Hit nearest_any(const DevScene& sc, const DevSphere* lds, const Ray& r, Work* w) {
-    if constexpr (kSrc == kSrcBvh) return nearest_bvh<kCount>(sc, r, w);
-    else if constexpr (kSrc == kSrcLds) return nearest_brute<kCount>(sc, lds, r, w);
-    else return nearest_brute<kCount>(sc, sc.spheres, r, w);
+// kSrcBvhLds stages ~60 KB per workgroup: 1024-thread groups share one copy
+// between 16 waves.  kSrcBvh stages only the top of the tree: 256 threads.
+template <int kSrc>
+constexpr int threads_of() { return kSrc == kSrcBvhLds ? 1024 : kBlock; }
+
+// Stage what the source keeps in LDS; returns the view the queries use.
+template <int kSrc>
+__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b, unsigned char* lds) {
+    constexpr int T = threads_of<kSrc>();
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj};
+    if constexpr (kSrc == kSrcLds) {
+        DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
+        for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
+        v.sph = ls;
+        __syncthreads();
+    } else if constexpr (kSrc >= kSrcBvh) {
+        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
+        for (int i = threadIdx.x; i < b.lds_nodes; i += T) ln[i] = sc.bvh[i];
+        v.lnodes = ln;
+        v.nl = b.lds_nodes;
+        if constexpr (kSrc == kSrcBvhLds) {
+            DevSphere* ls = reinterpret_cast<DevSphere*>(lds + static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode));
+            int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
+            for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
+            v.sph = ls;
+            v.obj = lo;
+        }
+        __syncthreads();
+    }
+    return v;
 }
 
 template <int kSrc, bool kCount>
-__device__ __forceinline__ bool occluded_any(const DevScene& sc, const DevSphere* lds, const Ray& r, bool has_range,
+__device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
+    if constexpr (kSrc >= kSrcBvh) return nearest_bvh<kCount, kSrc == kSrcBvhLds>(sc, v, r, w);
+    else return nearest_brute<kCount>(sc, v.sph, r, w);
+}
+
+template <int kSrc, bool kCount>
+__device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w) {
-    if constexpr (kSrc == kSrcBvh) return occluded_bvh<kCount>(sc, r, has_range, r2, w);
-    else if constexpr (kSrc == kSrcLds) return occluded_brute<kCount>(sc, lds, r, has_range, r2, w);
-    else return occluded_brute<kCount>(sc, sc.spheres, r, has_range, r2, w);
+    if constexpr (kSrc >= kSrcBvh) return occluded_bvh<kCount, kSrc == kSrcBvhLds>(sc, v, r, has_range, r2, w);
+    else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
 // One atomic per wave into totals[at], totals[at + 1].
@@ -205,82 +237,85 @@ __device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
     }
 }
 
+__device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
+    b.term[0][p] = c.r; b.term[1][p] = c.g; b.term[2][p] = c.b;
+    b.nlev[p] = static_cast<uint8_t>(k);
+}
+
+// Scene::intersect for every ray of Q_k (generation 0: the camera rays of the
+// chunk, computed here).  Outcomes that end the chain without lighting are
+// resolved on the spot (miss -> background; depth cut-off or insignificant
+// surface -> ambient, raytrace.rs:32-35); the rest become dense shade records.
 template <int kSrc, bool kCam, bool kCount>
-__global__ __launch_bounds__(kBlock) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
+__global__ __launch_bounds__(threads_of<kSrc>()) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    constexpr int T = threads_of<kSrc>();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const BvhView v = stage_lds<kSrc>(sc, b, lds);
     Work w;
-    extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
-    if constexpr (kSrc == kSrcLds) {
-        for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
-        __syncthreads();
-    }
     const uint32_t n = kCam ? b.slots : b.cnt[kCntQ + k];
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    for (uint32_t base = blockIdx.x * T; base < n; base += gridDim.x * T) {
         const uint32_t i = base + threadIdx.x;
         bool shade = false;
-        if (i < n) {
-            Ray r;
-            double sig;
-            uint32_t p;
-            if (!entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
-                b.hit_obj[i] = -2;                    // padding slot of a partial 8x8 tile
+        Ray r{};
+        double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0;
+        uint32_t p = 0;
+        Hit h{};
+        if (i < n && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
+            h = nearest_any<kSrc, kCount>(sc, v, r, &w);
+            if (h.obj == INT32_MAX) {
+                set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);          // raytrace.rs:265, 228-232
             } else {
-                const Hit h = nearest_any<kSrc, kCount>(sc, lds_spheres, r, &w);
-                b.hit_t[i] = h.t;
-                b.hit_obj[i] = h.obj;
-                b.hit_prim[i] = h.prim;
-                if (h.obj != INT32_MAX && static_cast<uint32_t>(k) <= fp.max_depth && sc.n_lights > 0) {
-                    const DevMaterial& m = sc.mats[h.obj];
-                    shade = m.kd_sig * sig > kMinSignificance || m.ks_sig * sig > kMinSignificance;
+                const DevMaterial& m = sc.mats[h.obj];
+                const bool lit = static_cast<uint32_t>(k) <= fp.max_depth &&       // raytrace.rs:33
+                                 (m.kd_sig * sig > kMinSignificance || m.ks_sig * sig > kMinSignificance);
+                if (!lit) {
+                    set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+                } else {
+                    shade = true;
+                    ptx = r.ox + r.dx * h.t; pty = r.oy + r.dy * h.t; ptz = r.oz + r.dz * h.t;   // ray.cast(t)
                 }
             }
         }
         const uint32_t slot = wave_append(&b.cnt[kCntS + k], shade);
-        if (i < n) {
-            b.shade_slot[i] = shade ? static_cast<int32_t>(slot) : -1;
-            if (shade) b.shade_list[slot] = i;
+        if (shade) {
+            b.sr_pt[0][slot] = ptx; b.sr_pt[1][slot] = pty; b.sr_pt[2][slot] = ptz;
+            b.sr_d[0][slot] = r.dx; b.sr_d[1][slot] = r.dy; b.sr_d[2][slot] = r.dz;
+            b.sr_sig[slot] = sig;
+            b.sr_obj[slot] = h.obj;
+            b.sr_prim[slot] = h.prim;
+            b.sr_pix[slot] = p;
         }
     }
     flush_work<kCount>(b, 2, w);
 }
 
-template <int kSrc, bool kCam, bool kCount>
-__global__ __launch_bounds__(kBlock) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+// The shadow queries of every shade record (raytrace.rs:39-49), one bit per light.
+template <int kSrc, bool kCount>
+__global__ __launch_bounds__(threads_of<kSrc>()) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    constexpr int T = threads_of<kSrc>();
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const BvhView v = stage_lds<kSrc>(sc, b, lds);
     Work w;
-    extern __shared__ __attribute__((aligned(16))) DevSphere lds_spheres[];
-    if constexpr (kSrc == kSrcLds) {
-        for (int i = threadIdx.x; i < sc.n_spheres; i += kBlock) lds_spheres[i] = sc.spheres[i];
-        __syncthreads();
-    }
     const uint32_t n = b.cnt[kCntS + k];
-    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
-        const uint32_t i = b.shade_list[j];
-        Ray r;
-        double sig;
-        uint32_t p;
-        entry_ray<kCam>(sc, fp, b, k, i, r, sig, p);
-        const double t = b.hit_t[i];
-        const double ptx = r.ox + r.dx * t, pty = r.oy + r.dy * t, ptz = r.oz + r.dz * t;
+    for (uint32_t j = blockIdx.x * T + threadIdx.x; j < n; j += gridDim.x * T) {
+        const double ptx = b.sr_pt[0][j], pty = b.sr_pt[1][j], ptz = b.sr_pt[2][j];
         uint32_t mask = 0;
         for (int l = 0; l < sc.n_lights; ++l) {
             double lx, ly, lz, r2;
             const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
             const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-            const bool occ = occluded_any<kSrc, kCount>(sc, lds_spheres, sray, has_range, r2, &w);
-            mask |= static_cast<uint32_t>(occ) << l;
+            mask |= static_cast<uint32_t>(occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) << l;
         }
         b.occ[j] = mask;
     }
     flush_work<kCount>(b, 4, w);
 }
 
-// Shading of generation k, in two dense passes:
-//   kList = true : the shade list (hits that evaluate lights; the heavy part:
-//                  normals, light directions, pow) -- every lane busy;
-//   kList = false: every other queue entry (misses, depth cut-offs, hits whose
-//                  significance switched lighting off) -- cheap.
-template <bool kCam, bool kList>
+// The Phong sum of every shade record (raytrace.rs:31-56), then either the
+// level push + reflection ray into Q_{k+1} (raytrace.rs:58-64) or the end of
+// the chain.
 __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    const uint32_t n = kList ? b.cnt[kCntS + k] : (kCam ? b.slots : b.cnt[kCntQ + k]);
+    const uint32_t n = b.cnt[kCntS + k];
     const int qn = (k + 1) & 1;
     for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
         const uint32_t j = base + threadIdx.x;
@@ -289,54 +324,37 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
         double nsig = 0.0;
         uint32_t p = 0;
         if (j < n) {
-            const uint32_t i = kList ? b.shade_list[j] : j;
-            const int32_t obj = b.hit_obj[i];
-            Ray r;
-            double sig;
-            const bool mine = kList || b.shade_slot[i] < 0;
-            if (mine && obj != -2 && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
-                Col res;
-                bool done = true;
-                if (obj == INT32_MAX) {
-                    res = Col{sc.bg[0], sc.bg[1], sc.bg[2]};                // raytrace.rs:265, 228-232
-                } else {
-                    const DevMaterial& m = sc.mats[obj];
-                    res = Col{m.amb[0], m.amb[1], m.amb[2]};                // raytrace.rs:32
-                    if (static_cast<uint32_t>(k) <= fp.max_depth) {          // raytrace.rs:33
-                        const double t = b.hit_t[i];
-                        const double ptx = r.ox + r.dx * t, pty = r.oy + r.dy * t, ptz = r.oz + r.dz * t;
-                        const bool diffuse = m.kd_sig * sig > kMinSignificance;
-                        const bool specular = m.ks_sig * sig > kMinSignificance;
-                        if (kList || specular) {
-                            double nx, ny, nz;
-                            hit_normal(sc, sc.spheres, b.hit_prim[i], ptx, pty, ptz, nx, ny, nz);
-                            if (nx * r.dx + ny * r.dy + nz * r.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
-                            if (kList) {                                     // diffuse || specular, lights > 0
-                                const uint32_t mask = b.occ[j];
-                                for (int l = 0; l < sc.n_lights; ++l) {
-                                    if ((mask >> l) & 1u) continue;          // shadowed (raytrace.rs:42-49)
-                                    const DevLight& L = sc.lights[l];
-                                    double lx, ly, lz, r2;
-                                    light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
-                                    add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, r.dx, r.dy, r.dz);
-                                }
-                            }
-                            if (specular) {                                  // raytrace.rs:58-64
-                                const size_t at = static_cast<size_t>(k) * b.cap + p;
-                                b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
-                                b.st_obj[at] = obj;
-                                rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
-                                nsig = sig * m.ks_sig;
-                                refl = true;
-                                done = false;
-                            }
-                        }
-                    }
+            const double ptx = b.sr_pt[0][j], pty = b.sr_pt[1][j], ptz = b.sr_pt[2][j];
+            const double dx = b.sr_d[0][j], dy = b.sr_d[1][j], dz = b.sr_d[2][j];
+            const double sig = b.sr_sig[j];
+            const int32_t obj = b.sr_obj[j];
+            p = b.sr_pix[j];
+            const DevMaterial& m = sc.mats[obj];
+            Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
+            const bool diffuse = m.kd_sig * sig > kMinSignificance;
+            const bool specular = m.ks_sig * sig > kMinSignificance;
+            double nx, ny, nz;
+            hit_normal(sc, sc.spheres, b.sr_prim[j], ptx, pty, ptz, nx, ny, nz);
+            if (nx * dx + ny * dy + nz * dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+            if (sc.n_lights > 0) {
+                const uint32_t mask = b.occ[j];
+                for (int l = 0; l < sc.n_lights; ++l) {
+                    if ((mask >> l) & 1u) continue;                              // shadowed (raytrace.rs:42-49)
+                    const DevLight& L = sc.lights[l];
+                    double lx, ly, lz, r2;
+                    light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
+                    add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, dx, dy, dz);
                 }
-                if (done) {
-                    b.term[0][p] = res.r; b.term[1][p] = res.g; b.term[2][p] = res.b;
-                    b.nlev[p] = static_cast<uint8_t>(k);
-                }
+            }
+            if (specular) {
+                const size_t at = static_cast<size_t>(k) * b.cap + p;
+                b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
+                b.st_obj[at] = obj;
+                rr = reflect_ray(Ray{0, 0, 0, dx, dy, dz}, ptx, pty, ptz, nx, ny, nz);
+                nsig = sig * m.ks_sig;
+                refl = true;
+            } else {
+                set_terminal(b, p, res, k);
             }
         }
         const uint32_t slot = wave_append(&b.cnt[kCntQ + k + 1], refl);
@@ -434,21 +452,29 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 
 // One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
 // must be zero on entry (the caller memsets them).
+template <int kSrc>
+size_t lds_bytes_of(const DevScene& sc, const WfBufs& b) {
+    if constexpr (kSrc == kSrcLds) return static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    else if constexpr (kSrc == kSrcBvh) return static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode);
+    else if constexpr (kSrc == kSrcBvhLds)
+        return static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode) +
+               static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
+    else return 0;
+}
+
 template <int kSrc, bool kCount>
 void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s) {
-    const size_t lds_bytes = kSrc == kSrcLds ? static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere) : 0;
-    const int gq = blocks_for(b.slots, 1024), gs = blocks_for(b.slots, 2048);
-    if (k == 0) {
-        hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_occlusion<kSrc, true, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<true, true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<true, false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-    } else {
-        hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_occlusion<kSrc, false, kCount>), dim3(gq), dim3(kBlock), lds_bytes, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<false, true>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-        hipLaunchKernelGGL((wf_shade<false, false>), dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
-    }
+    constexpr int T = threads_of<kSrc>();
+    const size_t lds = lds_bytes_of<kSrc>(sc, b);
+    // Workgroups that stage LDS are kept resident-sized (the copy is per block);
+    // the others fill every SIMD.
+    const uint64_t cap = kSrc == kSrcGlobal ? 16384 : kSrc == kSrcBvhLds ? 512 : kSrc == kSrcBvh ? 2048 : 1024;
+    const int gq = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((b.slots + T - 1) / T, cap)));
+    const int gs = blocks_for(b.slots, 8192);
+    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
+    else hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
+    if (sc.n_lights > 0) hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
+    hipLaunchKernelGGL(wf_shade, dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
 }
 
 // One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
@@ -459,11 +485,13 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
         if (count) {
-            if (src == kSrcBvh) launch_generation<kSrcBvh, true>(sc, fp, b, k, s);
+            if (src == kSrcBvhLds) launch_generation<kSrcBvhLds, true>(sc, fp, b, k, s);
+            else if (src == kSrcBvh) launch_generation<kSrcBvh, true>(sc, fp, b, k, s);
             else if (src == kSrcLds) launch_generation<kSrcLds, true>(sc, fp, b, k, s);
             else launch_generation<kSrcGlobal, true>(sc, fp, b, k, s);
         } else {
-            if (src == kSrcBvh) launch_generation<kSrcBvh, false>(sc, fp, b, k, s);
+            if (src == kSrcBvhLds) launch_generation<kSrcBvhLds, false>(sc, fp, b, k, s);
+            else if (src == kSrcBvh) launch_generation<kSrcBvh, false>(sc, fp, b, k, s);
             else if (src == kSrcLds) launch_generation<kSrcLds, false>(sc, fp, b, k, s);
             else launch_generation<kSrcGlobal, false>(sc, fp, b, k, s);
         }

@@ -350,15 +350,16 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const size_t sph_bytes = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
         int src;
         int32_t lds_nodes = 0;
-        const char* force = std::getenv("RT_WF_SRC");          // experiment override: 2 or 3
+        // sources: 2 BVH/L2 + scratch stack, 3 BVH/L2 + register stack, 4 BVH+spheres in LDS +
+        // scratch stack, 5 the same + register stack, 6 top of BVH in LDS + register stack
+        const char* force = std::getenv("RT_WF_SRC");          // experiment override
         if (mode == RT_ALGO_WAVEFRONT) {
-            const bool all = node_bytes + sph_bytes <= kLdsBudget && !(force && std::atoi(force) == 2);
-            if (all) { src = 3; lds_nodes = c->dsc.n_bvh; }
-            else {
-                // top of the tree only (256-thread groups): <= 32 KB keeps 5 groups per CU
-                src = 2;
+            const bool all_fit = node_bytes + sph_bytes <= kLdsBudget;
+            src = force ? std::atoi(force) : 2;
+            if (src < 2 || src > 6 || ((src == 4 || src == 5) && !all_fit)) src = 2;
+            if (src == 4 || src == 5) lds_nodes = c->dsc.n_bvh;
+            else if (src == 6)
                 lds_nodes = static_cast<int32_t>(std::min<size_t>(c->dsc.n_bvh, 32 * 1024 / sizeof(DevBvhNode)));
-            }
         } else {
             src = fits_lds ? 1 : 0;
         }

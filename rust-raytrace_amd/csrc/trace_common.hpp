@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "device_layout.hpp"
 
@@ -235,20 +236,41 @@ struct BvhView {
     const int32_t* obj;
 };
 
-template <bool kAllLds>
+// kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS
+template <int kNodes>
 __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
-    if constexpr (kAllLds) {
+    if constexpr (kNodes == 2) {
         return v.lnodes[i];
-    } else {
+    } else if constexpr (kNodes == 1) {
         if (i < v.nl) return v.lnodes[i];
+        return v.gnodes[i];
+    } else {
         return v.gnodes[i];
     }
 }
 
-// Traversal stack: the top kRegStack entries live in registers (shifted with
-// v_mov on push/pop, no memory latency); deeper entries spill to a private
-// array.  The host bounds the tree depth, so kBvhStack entries always suffice.
+// Traversal stacks.  MemStack: a private array (scratch, cached in L1/L2).
+// ShortStack: the top kRegStack entries live in registers (shifted with v_mov
+// on push/pop, no memory latency); deeper entries spill to a private array.
+// The host bounds the tree depth, so kBvhStack entries always suffice.
 constexpr int kRegStack = 8;
+
+template <bool kWithT>
+struct MemStack {
+    int32_t p[kBvhStack];
+    float t[kBvhStack];
+    int n = 0;
+    __device__ __forceinline__ void push(int32_t v, float tv) {
+        p[n] = v;
+        if constexpr (kWithT) t[n] = tv;
+        ++n;
+    }
+    __device__ __forceinline__ int32_t pop(float& tv) {
+        --n;
+        if constexpr (kWithT) tv = t[n];
+        return p[n];
+    }
+};
 
 template <bool kWithT>
 struct ShortStack {
@@ -291,7 +313,7 @@ struct ShortStack {
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
-template <bool kCount = false, bool kAllLds = false>
+template <bool kCount = false, int kNodes = 0, bool kShort = false>
 __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
@@ -299,11 +321,11 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    ShortStack<true> stk;
+    typename std::conditional<kShort, ShortStack<true>, MemStack<true>>::type stk;
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
-            const DevBvhNode nd = fetch_node<kAllLds>(v, cur);
+            const DevBvhNode nd = fetch_node<kNodes>(v, cur);
             if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
@@ -341,7 +363,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 }
 
 // The shadow query (see occluded_brute for the any-hit equivalence).
-template <bool kCount = false, bool kAllLds = false>
+template <bool kCount = false, int kNodes = 0, bool kShort = false>
 __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w = nullptr) {
     bool plane_block = false;
@@ -359,11 +381,11 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
-    ShortStack<false> stk;
+    typename std::conditional<kShort, ShortStack<false>, MemStack<false>>::type stk;
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
-            const DevBvhNode nd = fetch_node<kAllLds>(v, cur);
+            const DevBvhNode nd = fetch_node<kNodes>(v, cur);
             if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);

@@ -173,13 +173,24 @@ __device__ __forceinline__ bool entry_ray(const DevScene& sc, const FrameParams&
 // Sphere sources of the wavefront intersection kernels.
 constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
-constexpr int kSrcBvh = 2;          // BVH: top of the tree in LDS, spheres through the caches
-constexpr int kSrcBvhLds = 3;       // BVH: top of the tree and every sphere in LDS
+constexpr int kSrcBvhG = 2;         // BVH from HBM/L2, scratch stack
+constexpr int kSrcBvhGS = 3;        // BVH from HBM/L2, register short stack
+constexpr int kSrcBvhL = 4;         // BVH + spheres in LDS, scratch stack
+constexpr int kSrcBvhLS = 5;        // BVH + spheres in LDS, register short stack
+constexpr int kSrcBvhP = 6;         // top of the BVH in LDS, spheres from HBM/L2, register short stack
 
-// kSrcBvhLds stages ~60 KB per workgroup: 1024-thread groups share one copy
-// between 16 waves.  kSrcBvh stages only the top of the tree: 256 threads.
 template <int kSrc>
-constexpr int threads_of() { return kSrc == kSrcBvhLds ? 1024 : kBlock; }
+struct Src {
+    static constexpr bool bvh = kSrc >= kSrcBvhG;
+    static constexpr bool sph_lds = kSrc == kSrcLds || kSrc == kSrcBvhL || kSrc == kSrcBvhLS;
+    static constexpr int nodes = (kSrc == kSrcBvhL || kSrc == kSrcBvhLS) ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
+    static constexpr bool short_stack = kSrc == kSrcBvhGS || kSrc == kSrcBvhLS || kSrc == kSrcBvhP;
+    // all-LDS staging is ~60 KB per workgroup: 1024-thread groups share one copy between 16 waves
+    static constexpr int threads = nodes == 2 ? 1024 : 256;
+};
+
+template <int kSrc>
+constexpr int threads_of() { return Src<kSrc>::threads; }
 
 // Stage what the source keeps in LDS; returns the view the queries use.
 template <int kSrc>
@@ -191,12 +202,12 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
         __syncthreads();
-    } else if constexpr (kSrc >= kSrcBvh) {
+    } else if constexpr (Src<kSrc>::nodes > 0) {
         DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
         for (int i = threadIdx.x; i < b.lds_nodes; i += T) ln[i] = sc.bvh[i];
         v.lnodes = ln;
         v.nl = b.lds_nodes;
-        if constexpr (kSrc == kSrcBvhLds) {
+        if constexpr (Src<kSrc>::sph_lds) {
             DevSphere* ls = reinterpret_cast<DevSphere*>(lds + static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode));
             int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
             for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
@@ -210,14 +221,15 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
-    if constexpr (kSrc >= kSrcBvh) return nearest_bvh<kCount, kSrc == kSrcBvhLds>(sc, v, r, w);
+    if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::short_stack>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w) {
-    if constexpr (kSrc >= kSrcBvh) return occluded_bvh<kCount, kSrc == kSrcBvhLds>(sc, v, r, has_range, r2, w);
+    if constexpr (Src<kSrc>::bvh)
+        return occluded_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::short_stack>(sc, v, r, has_range, r2, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
@@ -454,12 +466,12 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 // must be zero on entry (the caller memsets them).
 template <int kSrc>
 size_t lds_bytes_of(const DevScene& sc, const WfBufs& b) {
-    if constexpr (kSrc == kSrcLds) return static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
-    else if constexpr (kSrc == kSrcBvh) return static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode);
-    else if constexpr (kSrc == kSrcBvhLds)
-        return static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode) +
-               static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
-    else return 0;
+    size_t bytes = 0;
+    if constexpr (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if constexpr (Src<kSrc>::nodes > 0) bytes = static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode);
+    if constexpr (Src<kSrc>::bvh && Src<kSrc>::sph_lds)
+        bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
+    return bytes;
 }
 
 template <int kSrc, bool kCount>
@@ -468,7 +480,7 @@ void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& 
     const size_t lds = lds_bytes_of<kSrc>(sc, b);
     // Workgroups that stage LDS are kept resident-sized (the copy is per block);
     // the others fill every SIMD.
-    const uint64_t cap = kSrc == kSrcGlobal ? 16384 : kSrc == kSrcBvhLds ? 512 : kSrc == kSrcBvh ? 2048 : 1024;
+    const uint64_t cap = kSrc == kSrcLds ? 1024 : Src<kSrc>::nodes == 2 ? 512 : 16384;
     const int gq = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((b.slots + T - 1) / T, cap)));
     const int gs = blocks_for(b.slots, 8192);
     if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
@@ -484,17 +496,17 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
                             hipStream_t s) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
-        if (count) {
-            if (src == kSrcBvhLds) launch_generation<kSrcBvhLds, true>(sc, fp, b, k, s);
-            else if (src == kSrcBvh) launch_generation<kSrcBvh, true>(sc, fp, b, k, s);
-            else if (src == kSrcLds) launch_generation<kSrcLds, true>(sc, fp, b, k, s);
-            else launch_generation<kSrcGlobal, true>(sc, fp, b, k, s);
-        } else {
-            if (src == kSrcBvhLds) launch_generation<kSrcBvhLds, false>(sc, fp, b, k, s);
-            else if (src == kSrcBvh) launch_generation<kSrcBvh, false>(sc, fp, b, k, s);
-            else if (src == kSrcLds) launch_generation<kSrcLds, false>(sc, fp, b, k, s);
-            else launch_generation<kSrcGlobal, false>(sc, fp, b, k, s);
+#define RT_GEN(S) (count ? launch_generation<S, true>(sc, fp, b, k, s) : launch_generation<S, false>(sc, fp, b, k, s))
+        switch (src) {
+        case kSrcGlobal: RT_GEN(kSrcGlobal); break;
+        case kSrcLds: RT_GEN(kSrcLds); break;
+        case kSrcBvhG: RT_GEN(kSrcBvhG); break;
+        case kSrcBvhGS: RT_GEN(kSrcBvhGS); break;
+        case kSrcBvhL: RT_GEN(kSrcBvhL); break;
+        case kSrcBvhLS: RT_GEN(kSrcBvhLS); break;
+        default: RT_GEN(kSrcBvhP); break;
         }
+#undef RT_GEN
     }
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;

@@ -100,6 +100,7 @@ struct WfBufs {
     uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: shade records of generation k
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
+    unsigned long long* gen_totals; // cnt[] summed over the chunks of a render
     uint32_t cap;                   // pixel capacity (stack stride)
     uint32_t slots;                 // generation-0 slots (8x8-tiled, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk

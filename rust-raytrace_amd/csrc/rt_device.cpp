@@ -18,7 +18,7 @@
 namespace rtamd {
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
-                            hipStream_t s);
+                            hipStream_t s, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
 }  // namespace rtamd
 
@@ -40,10 +40,20 @@ struct rt_ctx {
     uint64_t last_pixels = 0;
     bool last_timed = false;
     hipStream_t last_stream = nullptr;
-    // wavefront working set (grown on demand, kept across renders)
-    void* wf_mem = nullptr;
-    size_t wf_bytes = 0;
-    WfBufs wf{};
+    // Wavefront lanes: each owns a stream and a working set (grown on demand,
+    // kept across renders).  Row chunks of a render are dealt round-robin over
+    // the lanes; chunk c+1 starts once chunk c has passed its bulk generations,
+    // so its big launches overlap chunk c's latency-bound tail.
+    struct Lane {
+        hipStream_t s = nullptr;
+        hipEvent_t mark = nullptr, done = nullptr;
+        void* mem = nullptr;
+        size_t bytes = 0;
+        WfBufs b{};
+    };
+    std::vector<Lane> lanes;
+    hipEvent_t fork = nullptr;
+    bool wf_used = false;
     std::string err;
 };
 
@@ -68,19 +78,38 @@ int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // counters: [0, 256) rays per shard (megakernel), [256, 512) shadow rays per
-// shard, [512..] wavefront totals (see WfBufs::totals)
-constexpr int kCounterWords = 2 * kCounterShards + 8;
+// shard, [512, 520) wavefront totals (see WfBufs::totals), [520, 520 + kCntWords)
+// per-generation queue sizes summed over chunks
+constexpr int kTotals = 2 * kCounterShards;
+constexpr int kGenTotals = kTotals + 8;
+constexpr int kCounterWords = kGenTotals + kCntWords;
+
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
 
 uint32_t wf_chunk_pixels() {
     const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
     long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<uint32_t>(v) : (1u << 24);
+    return v > 0 ? static_cast<uint32_t>(v) : (1u << 22);
 }
 
-// Carve the wavefront working set for chunks of up to `cap` pixels in
+int ensure_lanes(rt_ctx* c, int n) {
+    while (static_cast<int>(c->lanes.size()) < n) {
+        rt_ctx::Lane L;
+        HIP_TRY(c, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&L.mark, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+        c->lanes.push_back(L);
+    }
+    return RT_OK;
+}
+
+// Carve a lane's wavefront working set for chunks of up to `cap` pixels in
 // `slots` generation-0 slots with `levels` stack levels.
-int ensure_wf(rt_ctx* c, uint32_t cap, uint32_t slots, uint32_t levels) {
-    WfBufs& b = c->wf;
+int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t slots, uint32_t levels) {
+    WfBufs& b = L.b;
     size_t off = 0;
     std::vector<std::pair<void**, size_t>> parts;
     auto add = [&](void** p, size_t bytes) { parts.emplace_back(p, off); off = align_up(off + bytes, 256); };
@@ -103,16 +132,17 @@ int ensure_wf(rt_ctx* c, uint32_t cap, uint32_t slots, uint32_t levels) {
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.term[a]), static_cast<size_t>(cap) * 8);
     add(reinterpret_cast<void**>(&b.nlev), cap);
     add(reinterpret_cast<void**>(&b.cnt), kCntWords * 4);
-    if (off > c->wf_bytes) {
-        if (c->wf_mem) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->wf_mem); }
-        c->wf_mem = nullptr;
-        c->wf_bytes = 0;
-        HIP_TRY(c, hipMalloc(&c->wf_mem, off));
-        c->wf_bytes = off;
+    if (off > L.bytes) {
+        if (L.mem) { (void)hipStreamSynchronize(L.s); (void)hipFree(L.mem); }
+        L.mem = nullptr;
+        L.bytes = 0;
+        HIP_TRY(c, hipMalloc(&L.mem, off));
+        L.bytes = off;
     }
-    auto* base = static_cast<uint8_t*>(c->wf_mem);
+    auto* base = static_cast<uint8_t*>(L.mem);
     for (auto& pr : parts) *pr.first = base + pr.second;
-    b.totals = c->d_counters + 2 * kCounterShards;
+    b.totals = c->d_counters + kTotals;
+    b.gen_totals = c->d_counters + kGenTotals;
     b.cap = cap;
     b.slots = slots;
     return RT_OK;
@@ -147,6 +177,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, RT_E_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         upload_srgb_table(srgb_average_table()) != hipSuccess)
         return cleanup(fail(nullptr, RT_E_HIP, "context initialisation failed"));
@@ -162,7 +193,14 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_bgr) (void)hipFree(c->d_bgr);
-    if (c->wf_mem) (void)hipFree(c->wf_mem);
+    for (auto& L : c->lanes) {
+        if (L.s) (void)hipStreamSynchronize(L.s);
+        if (L.mem) (void)hipFree(L.mem);
+        if (L.mark) (void)hipEventDestroy(L.mark);
+        if (L.done) (void)hipEventDestroy(L.done);
+        if (L.s) (void)hipStreamDestroy(L.s);
+    }
+    if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -355,7 +393,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const char* force = std::getenv("RT_WF_SRC");          // experiment override
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool all_fit = node_bytes + sph_bytes <= kLdsBudget;
-            src = force ? std::atoi(force) : 2;
+            src = force ? std::atoi(force) : (all_fit ? 4 : 2);
             if (src < 2 || src > 6 || ((src == 4 || src == 5) && !all_fit)) src = 2;
             if (src == 4 || src == 5) lds_nodes = c->dsc.n_bvh;
             else if (src == 6)
@@ -366,24 +404,41 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
+        const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
+        const int n_lanes = std::max(1, std::min<int>(env_int("RT_WF_STREAMS", 2), static_cast<int>(n_chunks)));
+        const int mark_gen = std::max(0, std::min<int>(env_int("RT_WF_STAGGER_GEN", 1), static_cast<int>(o->max_depth) + 1));
+        int rc2 = ensure_lanes(c, n_lanes);
+        if (rc2 != RT_OK) return rc2;
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
         const uint32_t cap = o->tile_w * chunk_rows;
-        int rc2 = ensure_wf(c, cap, slots, o->max_depth + 1);
-        if (rc2 != RT_OK) return rc2;
-        c->wf.tiles_x = tiles_x;
-        c->wf.lds_nodes = lds_nodes;
+        for (int l = 0; l < n_lanes; ++l) {
+            rc2 = ensure_wf(c, c->lanes[l], cap, slots, o->max_depth + 1);
+            if (rc2 != RT_OK) return rc2;
+            c->lanes[l].b.tiles_x = tiles_x;
+            c->lanes[l].b.lds_nodes = lds_nodes;
+        }
+        const bool count = (o->flags & RT_COUNT_WORK) != 0;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
-        for (uint32_t r0 = 0; r0 < o->tile_h; r0 += chunk_rows) {
+        HIP_TRY(c, hipEventRecord(c->fork, st));
+        for (int l = 0; l < n_lanes; ++l) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
+        for (uint32_t ci = 0; ci < n_chunks; ++ci) {
+            rt_ctx::Lane& L = c->lanes[ci % n_lanes];
+            if (ci > 0 && n_lanes > 1) HIP_TRY(c, hipStreamWaitEvent(L.s, c->lanes[(ci - 1) % n_lanes].mark, 0));
             FrameParams f = fp;
-            f.row0 = r0;
-            f.rows = std::min(chunk_rows, o->tile_h - r0);
-            WfBufs b = c->wf;
+            f.row0 = ci * chunk_rows;
+            f.rows = std::min(chunk_rows, o->tile_h - f.row0);
+            WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
-            HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), st));
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, (o->flags & RT_COUNT_WORK) != 0, st));
+            HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), L.s));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, count, L.s, L.mark, mark_gen));
+        }
+        for (int l = 0; l < n_lanes; ++l) {
+            HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));
+            HIP_TRY(c, hipStreamWaitEvent(st, c->lanes[l].done, 0));
         }
         HIP_TRY(c, hipEventRecord(c->ev1, st));
+        c->wf_used = true;
     } else {
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
@@ -402,12 +457,12 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     std::memset(s, 0, sizeof *s);
     for (int i = 0; i < kCounterShards; ++i) { s->rays += h[i]; s->shadow_rays += h[kCounterShards + i]; }
-    s->rays += h[2 * kCounterShards] + h[2 * kCounterShards + 1];
-    s->shadow_rays += h[2 * kCounterShards + 1];
-    s->box_tests = h[2 * kCounterShards + 2] + h[2 * kCounterShards + 4];
-    s->sphere_tests = h[2 * kCounterShards + 3] + h[2 * kCounterShards + 5];
-    s->shadow_box_tests = h[2 * kCounterShards + 4];
-    s->shadow_sphere_tests = h[2 * kCounterShards + 5];
+    s->rays += h[kTotals] + h[kTotals + 1];
+    s->shadow_rays += h[kTotals + 1];
+    s->box_tests = h[kTotals + 2] + h[kTotals + 4];
+    s->sphere_tests = h[kTotals + 3] + h[kTotals + 5];
+    s->shadow_box_tests = h[kTotals + 4];
+    s->shadow_sphere_tests = h[kTotals + 5];
     s->pixels = c->last_pixels;
     if (c->last_timed) {
         float ms = 0.f;
@@ -420,13 +475,16 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
 
 int rt_ctx_generation_counts(rt_ctx* c, uint32_t* queue, uint32_t* shaded, int n) {
     if (!c || n < 0 || (n && (!queue || !shaded))) return RT_E_INVALID;
-    if (!c->wf_mem) return fail(c, RT_E_NOSCENE, "no wavefront render yet");
+    if (!c->wf_used) return fail(c, RT_E_NOSCENE, "no wavefront render yet");
     HIP_TRY(c, hipSetDevice(c->device));
     if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
-    uint32_t h[kCntWords];
-    HIP_TRY(c, hipMemcpyAsync(h, c->wf.cnt, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long h[kCntWords];
+    HIP_TRY(c, hipMemcpyAsync(h, c->d_counters + kGenTotals, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (int k = 0; k < n && k < kCntS; ++k) { queue[k] = h[kCntQ + k]; shaded[k] = h[kCntS + k]; }
+    for (int k = 0; k < n && k < kCntS; ++k) {
+        queue[k] = static_cast<uint32_t>(h[kCntQ + k]);
+        shaded[k] = static_cast<uint32_t>(h[kCntS + k]);
+    }
     return RT_OK;
 }
 

@@ -432,12 +432,14 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
 
 // Scene::intersect calls of this chunk: every pixel's camera ray, every later
 // queue entry, and one shadow query per light per shaded hit.
+// (atomics: chunks on different streams finish concurrently)
 __global__ void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
     unsigned long long nearest = static_cast<unsigned long long>(fp.tile_w) * fp.rows, shadow = 0;
     for (int k = 1; k < generations; ++k) nearest += b.cnt[kCntQ + k];
     for (int k = 0; k < generations; ++k) shadow += static_cast<unsigned long long>(b.cnt[kCntS + k]) * n_lights;
-    b.totals[0] += nearest * fp.spp;
-    b.totals[1] += shadow * fp.spp;
+    atomicAdd(&b.totals[0], nearest * fp.spp);
+    atomicAdd(&b.totals[1], shadow * fp.spp);
+    for (int k = 0; k < kCntWords; ++k) atomicAdd(&b.gen_totals[k], static_cast<unsigned long long>(b.cnt[k]));
 }
 
 inline int blocks_for(uint64_t items, int cap_blocks) {
@@ -493,7 +495,7 @@ void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& 
 // must be zero on entry (the caller memsets them).  src: 0 brute/global,
 // 1 brute/LDS, 2 BVH.
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
-                            hipStream_t s) {
+                            hipStream_t s, hipEvent_t mark, int mark_gen) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
 #define RT_GEN(S) (count ? launch_generation<S, true>(sc, fp, b, k, s) : launch_generation<S, false>(sc, fp, b, k, s))
@@ -507,6 +509,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         default: RT_GEN(kSrcBvhP); break;
         }
 #undef RT_GEN
+        if (mark && k == mark_gen) {
+            const hipError_t e = hipEventRecord(mark, s);
+            if (e != hipSuccess) return e;
+        }
     }
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;

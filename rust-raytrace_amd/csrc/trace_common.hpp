@@ -249,67 +249,59 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
     }
 }
 
-// Traversal stacks.  MemStack: a private array (scratch, cached in L1/L2).
-// ShortStack: the top kRegStack entries live in registers (shifted with v_mov
-// on push/pop, no memory latency); deeper entries spill to a private array.
+// Traversal stacks, declared as plain locals so the compiler keeps the stack
+// pointer (and, for the short stack, the top entries) in registers.
+//  * memory stack: entries in a private array (scratch, cached in L1/L2);
+//  * short stack: the top kRegStack entries in registers, shifted with v_mov
+//    on push/pop (constant indices after unrolling); deeper entries spill to
+//    a private array.
 // The host bounds the tree depth, so kBvhStack entries always suffice.
 constexpr int kRegStack = 8;
 
-template <bool kWithT>
-struct MemStack {
-    int32_t p[kBvhStack];
-    float t[kBvhStack];
-    int n = 0;
-    __device__ __forceinline__ void push(int32_t v, float tv) {
-        p[n] = v;
-        if constexpr (kWithT) t[n] = tv;
-        ++n;
+#define RT_STACK_DECL(kShort, kWithT)                                                  \
+    int32_t stk_p[kShort ? kRegStack : kBvhStack];                                     \
+    float stk_t[kShort ? kRegStack : kBvhStack];                                       \
+    int32_t ovf_p[kShort ? kBvhStack - kRegStack : 1];                                 \
+    float ovf_t[kShort ? kBvhStack - kRegStack : 1];                                   \
+    int stk_n = 0;                                                                     \
+    auto stk_push = [&](int32_t v, float tv) {                                         \
+        if constexpr (kShort) {                                                        \
+            if (stk_n >= kRegStack) {                                                  \
+                ovf_p[stk_n - kRegStack] = stk_p[kRegStack - 1];                       \
+                if constexpr (kWithT) ovf_t[stk_n - kRegStack] = stk_t[kRegStack - 1]; \
+            }                                                                          \
+            _Pragma("unroll") for (int q = kRegStack - 1; q > 0; --q) {                \
+                stk_p[q] = stk_p[q - 1];                                               \
+                if constexpr (kWithT) stk_t[q] = stk_t[q - 1];                         \
+            }                                                                          \
+            stk_p[0] = v;                                                              \
+            if constexpr (kWithT) stk_t[0] = tv;                                       \
+        } else {                                                                       \
+            stk_p[stk_n] = v;                                                          \
+            if constexpr (kWithT) stk_t[stk_n] = tv;                                   \
+        }                                                                              \
+        ++stk_n;                                                                       \
+    };                                                                                 \
+    auto stk_pop = [&](float& tv) -> int32_t {                                         \
+        --stk_n;                                                                       \
+        int32_t v;                                                                     \
+        if constexpr (kShort) {                                                        \
+            v = stk_p[0];                                                              \
+            if constexpr (kWithT) tv = stk_t[0];                                       \
+            _Pragma("unroll") for (int q = 0; q < kRegStack - 1; ++q) {                \
+                stk_p[q] = stk_p[q + 1];                                               \
+                if constexpr (kWithT) stk_t[q] = stk_t[q + 1];                         \
+            }                                                                          \
+            if (stk_n >= kRegStack) {                                                  \
+                stk_p[kRegStack - 1] = ovf_p[stk_n - kRegStack];                       \
+                if constexpr (kWithT) stk_t[kRegStack - 1] = ovf_t[stk_n - kRegStack]; \
+            }                                                                          \
+        } else {                                                                       \
+            v = stk_p[stk_n];                                                          \
+            if constexpr (kWithT) tv = stk_t[stk_n];                                   \
+        }                                                                              \
+        return v;                                                                      \
     }
-    __device__ __forceinline__ int32_t pop(float& tv) {
-        --n;
-        if constexpr (kWithT) tv = t[n];
-        return p[n];
-    }
-};
-
-template <bool kWithT>
-struct ShortStack {
-    int32_t p[kRegStack];
-    float t[kRegStack];
-    int32_t sp[kBvhStack - kRegStack];
-    float st[kBvhStack - kRegStack];
-    int n = 0;
-
-    __device__ __forceinline__ void push(int32_t v, float tv) {
-        if (n >= kRegStack) {
-            sp[n - kRegStack] = p[kRegStack - 1];
-            if constexpr (kWithT) st[n - kRegStack] = t[kRegStack - 1];
-        }
-#pragma unroll
-        for (int k = kRegStack - 1; k > 0; --k) {
-            p[k] = p[k - 1];
-            if constexpr (kWithT) t[k] = t[k - 1];
-        }
-        p[0] = v;
-        if constexpr (kWithT) t[0] = tv;
-        ++n;
-    }
-    __device__ __forceinline__ int32_t pop(float& tv) {
-        const int32_t v = p[0];
-        if constexpr (kWithT) tv = t[0];
-#pragma unroll
-        for (int k = 0; k < kRegStack - 1; ++k) {
-            p[k] = p[k + 1];
-            if constexpr (kWithT) t[k] = t[k + 1];
-        }
-        --n;
-        if (n >= kRegStack) {
-            p[kRegStack - 1] = sp[n - kRegStack];
-            if constexpr (kWithT) t[kRegStack - 1] = st[n - kRegStack];
-        }
-        return v;
-    }
-};
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
@@ -321,7 +313,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    typename std::conditional<kShort, ShortStack<true>, MemStack<true>>::type stk;
+    RT_STACK_DECL(kShort, true);
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
@@ -332,7 +324,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                stk.push(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
+                stk_push(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -355,8 +347,8 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
         // pop, skipping entries that the current best already rules out
         float tn = 0.0f;
         for (;;) {
-            if (stk.n == 0) return h;
-            cur = stk.pop(tn);
+            if (stk_n == 0) return h;
+            cur = stk_pop(tn);
             if (tn <= tlim) break;
         }
     }
@@ -381,7 +373,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
-    typename std::conditional<kShort, ShortStack<false>, MemStack<false>>::type stk;
+    RT_STACK_DECL(kShort, false);
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
@@ -392,7 +384,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                stk.push(first0 ? nd.c1 : nd.c0, 0.0f);
+                stk_push(first0 ? nd.c1 : nd.c0, 0.0f);
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -406,9 +398,9 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
                 if (sphere_t(v.sph[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
             }
         }
-        if (stk.n == 0) return false;
+        if (stk_n == 0) return false;
         float tn;
-        cur = stk.pop(tn);
+        cur = stk_pop(tn);
     }
 }
 

@@ -9,7 +9,7 @@ rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 fi
 for v in ${VARIANTS:-default:X=1}; do
-  name=${v%%:*}; envs=${v#*:}
+  name=${v%%:*}; envs=${v#*:}; envs=${envs//+/ }
   if [ "${VTESTS:-0}" = "1" ]; then
     env $envs timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -x -m gpu \
         -k "config3 or axis_aligned or extreme or ten_thousand or bit_for_bit or golden" > gpurun_out/vtest_$name.log 2>&1

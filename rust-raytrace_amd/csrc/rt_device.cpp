@@ -92,7 +92,7 @@ int env_int(const char* name, int dflt) {
 uint32_t wf_chunk_pixels() {
     const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
     long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<uint32_t>(v) : (1u << 22);
+    return v > 0 ? static_cast<uint32_t>(v) : (1u << 24);
 }
 
 int ensure_lanes(rt_ctx* c, int n) {
@@ -405,7 +405,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
         const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
-        const int n_lanes = std::max(1, std::min<int>(env_int("RT_WF_STREAMS", 2), static_cast<int>(n_chunks)));
+        const int n_lanes = std::max(1, std::min<int>(env_int("RT_WF_STREAMS", 1), static_cast<int>(n_chunks)));
         const int mark_gen = std::max(0, std::min<int>(env_int("RT_WF_STAGGER_GEN", 1), static_cast<int>(o->max_depth) + 1));
         int rc2 = ensure_lanes(c, n_lanes);
         if (rc2 != RT_OK) return rc2;

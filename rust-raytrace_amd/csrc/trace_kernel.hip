@@ -296,29 +296,30 @@ __global__ __launch_bounds__(threads_of<kSrc>()) void wf_nearest(DevScene sc, Fr
             b.sr_obj[slot] = h.obj;
             b.sr_prim[slot] = h.prim;
             b.sr_pix[slot] = p;
+            b.occ[slot] = 0u;
         }
     }
     flush_work<kCount>(b, 2, w);
 }
 
-// The shadow queries of every shade record (raytrace.rs:39-49), one bit per light.
+// The shadow queries of every shade record (raytrace.rs:39-49): one work-item
+// per (record, light) pair -- the lights of one hit are independent queries --
+// setting bit l of the record's occlusion mask.
 template <int kSrc, bool kCount>
 __global__ __launch_bounds__(threads_of<kSrc>()) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     constexpr int T = threads_of<kSrc>();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const BvhView v = stage_lds<kSrc>(sc, b, lds);
     Work w;
-    const uint32_t n = b.cnt[kCntS + k];
-    for (uint32_t j = blockIdx.x * T + threadIdx.x; j < n; j += gridDim.x * T) {
+    const uint32_t L = static_cast<uint32_t>(sc.n_lights);
+    const uint32_t n = b.cnt[kCntS + k] * L;
+    for (uint32_t q = blockIdx.x * T + threadIdx.x; q < n; q += gridDim.x * T) {
+        const uint32_t j = q / L, l = q - j * L;
         const double ptx = b.sr_pt[0][j], pty = b.sr_pt[1][j], ptz = b.sr_pt[2][j];
-        uint32_t mask = 0;
-        for (int l = 0; l < sc.n_lights; ++l) {
-            double lx, ly, lz, r2;
-            const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
-            const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-            mask |= static_cast<uint32_t>(occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) << l;
-        }
-        b.occ[j] = mask;
+        double lx, ly, lz, r2;
+        const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) atomicOr(&b.occ[j], 1u << l);
     }
     flush_work<kCount>(b, 4, w);
 }
@@ -379,35 +380,55 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
     }
 }
 
-__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p) {
+// The fold factor of a level is the specular colour of its object
+// (raytrace.rs:63); it comes from an LDS table when the scene is small enough.
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, const double* ks_lds, uint32_t p) {
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
-    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc (raytrace.rs:63)
+    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc
         const size_t at = static_cast<size_t>(k) * b.cap + p;
-        const DevMaterial& m = sc.mats[b.st_obj[at]];
-        acc.r = b.st[0][at] + m.ks[0] * acc.r;
-        acc.g = b.st[1][at] + m.ks[1] * acc.g;
-        acc.b = b.st[2][at] + m.ks[2] * acc.b;
+        const int32_t obj = b.st_obj[at];
+        double k0, k1, k2;
+        if (ks_lds) {
+            k0 = ks_lds[3 * obj]; k1 = ks_lds[3 * obj + 1]; k2 = ks_lds[3 * obj + 2];
+        } else {
+            const DevMaterial& m = sc.mats[obj];
+            k0 = m.ks[0]; k1 = m.ks[1]; k2 = m.ks[2];
+        }
+        acc.r = b.st[0][at] + k0 * acc.r;
+        acc.g = b.st[1][at] + k1 * acc.g;
+        acc.b = b.st[2][at] + k2 * acc.b;
     }
     return acc;
 }
+
+constexpr int kFoldKsObjects = 2048;   // 48 KB table
 
 // kStaged: every group of 256 pixels lies in one output row (tile_w % 256 == 0,
 // BGR rows unpadded and dword aligned): the block assembles its 3 KiB of RGB
 // and 768 B of BGR in LDS and stores them as whole dwords.
 template <bool kStaged>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, int n_objects) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
+    __shared__ double s_ks[3 * kFoldKsObjects];
+    const double* ks_lds = nullptr;
+    if (n_objects <= kFoldKsObjects) {
+        for (int i = threadIdx.x; i < n_objects; i += kBlock) {
+            s_ks[3 * i] = sc.mats[i].ks[0]; s_ks[3 * i + 1] = sc.mats[i].ks[1]; s_ks[3 * i + 2] = sc.mats[i].ks[2];
+        }
+        __syncthreads();
+        ks_lds = s_ks;
+    }
     const uint32_t npix = fp.tile_w * fp.rows;
     for (uint32_t base = blockIdx.x * kBlock; base < npix; base += gridDim.x * kBlock) {
         const uint32_t p = base + threadIdx.x;
         if constexpr (!kStaged) {
             if (p < npix) {
-                const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
+                const Col res = average_samples(fold_pixel(sc, b, ks_lds, p), fp.spp);
                 write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res);
             }
         } else {
-            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
+            const Col res = average_samples(fold_pixel(sc, b, ks_lds, p), fp.spp);   // npix % 256 == 0 here
             s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
             s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
             s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
@@ -487,7 +508,11 @@ void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& 
     const int gs = blocks_for(b.slots, 8192);
     if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
     else hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
-    if (sc.n_lights > 0) hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
+    if (sc.n_lights > 0) {
+        const uint64_t items = static_cast<uint64_t>(b.slots) * sc.n_lights;
+        const int go = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((items + T - 1) / T, cap)));
+        hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), dim3(go), dim3(T), lds, s, sc, fp, b, k);
+    }
     hipLaunchKernelGGL(wf_shade, dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
 }
 
@@ -517,8 +542,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
     const dim3 gf(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048));
-    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
-    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    const int n_objects = sc.n_spheres + sc.n_planes;
+    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
+    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(1), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }

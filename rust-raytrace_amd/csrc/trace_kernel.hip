@@ -381,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
 }
 
 // The fold factor of a level is the specular colour of its object
-// (raytrace.rs:63); it comes from an LDS table when the scene is small enough.
+// (raytrace.rs:63).
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, const double* ks_lds, uint32_t p) {
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
     for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc
@@ -401,8 +401,6 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, c
     return acc;
 }
 
-constexpr int kFoldKsObjects = 2048;   // 48 KB table
-
 // kStaged: every group of 256 pixels lies in one output row (tile_w % 256 == 0,
 // BGR rows unpadded and dword aligned): the block assembles its 3 KiB of RGB
 // and 768 B of BGR in LDS and stores them as whole dwords.
@@ -410,15 +408,10 @@ template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, int n_objects) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
-    __shared__ double s_ks[3 * kFoldKsObjects];
+    // (an LDS table of the fold factors was measured slower: 52 KB per block
+    // cut occupancy more than the gathers it saved)
     const double* ks_lds = nullptr;
-    if (n_objects <= kFoldKsObjects) {
-        for (int i = threadIdx.x; i < n_objects; i += kBlock) {
-            s_ks[3 * i] = sc.mats[i].ks[0]; s_ks[3 * i + 1] = sc.mats[i].ks[1]; s_ks[3 * i + 2] = sc.mats[i].ks[2];
-        }
-        __syncthreads();
-        ks_lds = s_ks;
-    }
+    (void)n_objects;
     const uint32_t npix = fp.tile_w * fp.rows;
     for (uint32_t base = blockIdx.x * kBlock; base < npix; base += gridDim.x * kBlock) {
         const uint32_t p = base + threadIdx.x;
@@ -455,12 +448,15 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
 // queue entry, and one shadow query per light per shaded hit.
 // (atomics: chunks on different streams finish concurrently)
 __global__ void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
-    unsigned long long nearest = static_cast<unsigned long long>(fp.tile_w) * fp.rows, shadow = 0;
-    for (int k = 1; k < generations; ++k) nearest += b.cnt[kCntQ + k];
-    for (int k = 0; k < generations; ++k) shadow += static_cast<unsigned long long>(b.cnt[kCntS + k]) * n_lights;
-    atomicAdd(&b.totals[0], nearest * fp.spp);
-    atomicAdd(&b.totals[1], shadow * fp.spp);
-    for (int k = 0; k < kCntWords; ++k) atomicAdd(&b.gen_totals[k], static_cast<unsigned long long>(b.cnt[k]));
+    const int t = threadIdx.x;                                  // kCntWords threads
+    atomicAdd(&b.gen_totals[t], static_cast<unsigned long long>(b.cnt[t]));
+    if (t == 0) {
+        unsigned long long nearest = static_cast<unsigned long long>(fp.tile_w) * fp.rows, shadow = 0;
+        for (int k = 1; k < generations; ++k) nearest += b.cnt[kCntQ + k];
+        for (int k = 0; k < generations; ++k) shadow += static_cast<unsigned long long>(b.cnt[kCntS + k]) * n_lights;
+        atomicAdd(&b.totals[0], nearest * fp.spp);
+        atomicAdd(&b.totals[1], shadow * fp.spp);
+    }
 }
 
 inline int blocks_for(uint64_t items, int cap_blocks) {
@@ -545,7 +541,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const int n_objects = sc.n_spheres + sc.n_planes;
     if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
     else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
-    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(1), 0, s, fp, b, sc.n_lights, gens);
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kCntWords), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }
 

@@ -85,7 +85,7 @@ struct WfBufs {
     double* qsig[2];                // significance passed down (raytrace.rs:63)
     uint32_t* qpix[2];              // owning pixel (chunk-local index)
     // Shade records of the current generation: the hits that go on to light
-    // evaluation and/or reflection, written densely by wf_nearest.
+    // evaluation and/or reflection, in the same block-partitioned layout as the queues.
     double* sr_pt[3];               // hit point ray.cast(t)
     double* sr_d[3];                // incoming direction
     double* sr_sig;                 // significance
@@ -97,17 +97,23 @@ struct WfBufs {
     int32_t* st_obj;                // per-level object id (its specular colour is the fold factor)
     double* term[3];                // terminal colour of each pixel's chain
     uint8_t* nlev;                  // levels pushed per pixel
-    uint32_t* cnt;                  // [kCntQ + k]: |Q_k|, [kCntS + k]: shade records of generation k
+    uint32_t* rq;                   // [k * G + r]: entries in region r of Q_k (written by its producer)
+    uint32_t* rs;                   // [k * G + r]: shade records in region r of generation k
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
-    unsigned long long* gen_totals; // cnt[] summed over the chunks of a render
+    unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
     uint32_t cap;                   // pixel capacity (stack stride)
-    uint32_t slots;                 // generation-0 slots (8x8-tiled, >= pixels)
+    uint32_t G;                     // regions per queue
+    uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
+    uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
     int32_t lds_nodes;              // BVH nodes (breadth-first prefix) staged in LDS by the BVH kernels
 };
 
-constexpr int kCntQ = 0;
+constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
+constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G
+constexpr int kMaxGenerations = 34;   // RT_MAX_DEPTH_LIMIT + 2 generations, + 1 spare for the last producer
+constexpr int kCntQ = 0;              // gen_totals layout: [kCntQ + k] queue sizes, [kCntS + k] shade records
 constexpr int kCntS = 64;
 constexpr int kCntWords = 128;
 constexpr int kCounterShards = 256;

@@ -26,6 +26,7 @@ using namespace rtamd;
 
 struct rt_ctx {
     int device = 0;
+    int n_cu = 256;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     void* d_blob = nullptr;
@@ -106,14 +107,14 @@ int ensure_lanes(rt_ctx* c, int n) {
     return RT_OK;
 }
 
-// Carve a lane's wavefront working set for chunks of up to `cap` pixels in
-// `slots` generation-0 slots with `levels` stack levels.
-int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t slots, uint32_t levels) {
+// Carve a lane's wavefront working set for chunks of up to `cap` pixels: every
+// queue and shade-record array is G regions of R entries.
+int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels) {
     WfBufs& b = L.b;
     size_t off = 0;
     std::vector<std::pair<void**, size_t>> parts;
     auto add = [&](void** p, size_t bytes) { parts.emplace_back(p, off); off = align_up(off + bytes, 256); };
-    const size_t q = slots;                    // queue capacity (>= pixels)
+    const size_t q = static_cast<size_t>(G) * R;   // queue capacity (>= generation-0 slots)
     for (int g = 0; g < 2; ++g) {
         for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qo[g][a]), q * 8);
         for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qd[g][a]), q * 8);
@@ -131,7 +132,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t slots, uint32_t
     add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.term[a]), static_cast<size_t>(cap) * 8);
     add(reinterpret_cast<void**>(&b.nlev), cap);
-    add(reinterpret_cast<void**>(&b.cnt), kCntWords * 4);
+    add(reinterpret_cast<void**>(&b.rq), static_cast<size_t>(kMaxGenerations) * G * 4);
+    add(reinterpret_cast<void**>(&b.rs), static_cast<size_t>(kMaxGenerations) * G * 4);
     if (off > L.bytes) {
         if (L.mem) { (void)hipStreamSynchronize(L.s); (void)hipFree(L.mem); }
         L.mem = nullptr;
@@ -144,7 +146,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t slots, uint32_t
     b.totals = c->d_counters + kTotals;
     b.gen_totals = c->d_counters + kGenTotals;
     b.cap = cap;
-    b.slots = slots;
+    b.G = G;
+    b.R = R;
     return RT_OK;
 }
 
@@ -173,6 +176,8 @@ int rt_ctx_create(int device, rt_ctx** out) {
     auto* c = new (std::nothrow) rt_ctx();
     if (!c) return RT_E_NOMEM;
     c->device = device;
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu < 1)
+        c->n_cu = 256;
     auto cleanup = [&](int rc) { rt_ctx_destroy(c); return rc; };
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, RT_E_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -389,13 +394,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         int src;
         int32_t lds_nodes = 0;
         // sources: 2 BVH/L2 + scratch stack, 3 BVH/L2 + register stack, 4 BVH+spheres in LDS +
-        // scratch stack, 5 the same + register stack, 6 top of BVH in LDS + register stack
+        // scratch stack, 5 the same + register stack, 6 top of BVH in LDS + register stack,
+        // 7 = 4 held to 64 VGPRs (two workgroups per CU)
         const char* force = std::getenv("RT_WF_SRC");          // experiment override
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool all_fit = node_bytes + sph_bytes <= kLdsBudget;
             src = force ? std::atoi(force) : (all_fit ? 4 : 2);
-            if (src < 2 || src > 6 || ((src == 4 || src == 5) && !all_fit)) src = 2;
-            if (src == 4 || src == 5) lds_nodes = c->dsc.n_bvh;
+            if (src < 2 || src > 7 || ((src == 4 || src == 5 || src == 7) && !all_fit)) src = 2;
+            if (src == 4 || src == 5 || src == 7) lds_nodes = c->dsc.n_bvh;
             else if (src == 6)
                 lds_nodes = static_cast<int32_t>(std::min<size_t>(c->dsc.n_bvh, 32 * 1024 / sizeof(DevBvhNode)));
         } else {
@@ -412,8 +418,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
         const uint32_t cap = o->tile_w * chunk_rows;
+        // G regions: two resident 1024-thread workgroups per CU (the LDS-staged
+        // BVH allows no more), fewer for small chunks; R covers every slot.
+        const int g_env = env_int("RT_WF_REGIONS", 0);
+        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
+        G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
+        const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
         for (int l = 0; l < n_lanes; ++l) {
-            rc2 = ensure_wf(c, c->lanes[l], cap, slots, o->max_depth + 1);
+            rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1);
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.lds_nodes = lds_nodes;
@@ -430,7 +442,6 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             f.rows = std::min(chunk_rows, o->tile_h - f.row0);
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
-            HIP_TRY(c, hipMemsetAsync(b.cnt, 0, kCntWords * sizeof(uint32_t), L.s));
             HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, count, L.s, L.mark, mark_gen));
         }
         for (int l = 0; l < n_lanes; ++l) {

@@ -123,10 +123,21 @@ __global__ __launch_bounds__(kBlock) void trace_frame_kernel(DevScene sc, FrameP
 }
 
 // ---------------------------------------------------------------- wavefront
+//
+// Queues are BLOCK-PARTITIONED: a queue of generation k is G regions of R
+// entries, region r written only by workgroup r of the producing kernel
+// (appending through an LDS counter) and its size published in rq/rs[k*G+r].
+// No global atomic sits on the data path: a single global queue counter
+// serialises at ~88 atomics/us (MI355X_MICROARCH.md, "dequeue") and was the
+// measured bottleneck of the first version.  Consumers read the queue DENSELY:
+// each workgroup scans the G region sizes into LDS and maps item i to
+// (region, offset) by binary search, so small tail queues still fill whole
+// waves.  Every queue kernel runs exactly G workgroups of kWfThreads and
+// grid-strides over its items, so workgroup b produces at most R outputs.
 
-// Wave-aggregated append: one atomic per wave, lanes get consecutive slots in
-// lane order (keeps neighbouring rays neighbours).  All 64 lanes must call it.
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool want) {
+// Wave-aggregated append to an LDS counter: one LDS atomic per wave, lanes
+// get consecutive slots in lane order.  All 64 lanes must call it.
+__device__ __forceinline__ uint32_t lds_append(uint32_t* counter, bool want) {
     const unsigned long long mask = __ballot(want);
     if (mask == 0) return 0xFFFFFFFFu;
     const int lane = threadIdx.x & 63;
@@ -138,36 +149,59 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool want) {
     return want ? base + below : 0xFFFFFFFFu;
 }
 
-// Generation-0 slot i -> pixel of the chunk, in 8x8 tiles (one tile per wave).
-__device__ __forceinline__ bool slot_pixel(const WfBufs& b, const FrameParams& fp, uint32_t i, uint32_t& lx,
-                                           uint32_t& ly) {
-    const uint32_t tile = i >> 6, w = i & 63u;
+// Exclusive scan of the G region sizes `counts` into s_scan[0..G]
+// (s_scan[G] = queue size).  s_wave: 16 words.  Ends with a barrier.
+__device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan, uint32_t* s_wave) {
+    const uint32_t per = (G + kWfThreads - 1) / kWfThreads;       // 1 or 2
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t v[2] = {0, 0}, sum = 0;
+    for (uint32_t e = 0; e < per; ++e) {
+        const uint32_t i = t * per + e;
+        v[e] = i < G ? counts[i] : 0u;
+        sum += v[e];
+    }
+    uint32_t inc = sum;                                              // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off, 64);
+        if (lane >= static_cast<uint32_t>(off)) inc += o;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < kWfThreads / 64; ++w) { const uint32_t x = s_wave[w]; s_wave[w] = acc; acc += x; }
+    }
+    __syncthreads();
+    uint32_t run = s_wave[wave] + inc - sum;
+    for (uint32_t e = 0; e < per; ++e) {
+        const uint32_t i = t * per + e;
+        if (i < G) s_scan[i] = run;
+        run += v[e];
+    }
+    if (t == kWfThreads - 1) s_scan[G] = run;
+    __syncthreads();
+}
+
+// Dense item i (< s_scan[G]) -> its entry index region * R + offset.
+__device__ __forceinline__ size_t region_entry(const uint32_t* s_scan, uint32_t G, uint32_t R, uint32_t i) {
+    uint32_t lo = 0, hi = G - 1;                  // largest r with s_scan[r] <= i
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_scan[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return static_cast<size_t>(lo) * R + (i - s_scan[lo]);
+}
+
+// Generation-0 slot j of the chunk (8x8 tiles, row-major) -> local pixel.
+__device__ __forceinline__ bool slot_pixel(const WfBufs& b, const FrameParams& fp, uint32_t j, uint32_t& lx, uint32_t& ly) {
+    const uint32_t tile = j >> 6, w = j & 63u;
     lx = (tile % b.tiles_x) * 8u + (w & 7u);
     ly = (tile / b.tiles_x) * 8u + (w >> 3);
     return lx < fp.tile_w && ly < fp.rows;
 }
 
-__device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, uint32_t i) {
+__device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
     return Ray{b.qo[q][0][i], b.qo[q][1][i], b.qo[q][2][i], b.qd[q][0][i], b.qd[q][1][i], b.qd[q][2][i]};
-}
-
-// Ray of queue entry i of generation k (generation 0 is computed, not stored).
-template <bool kCam>
-__device__ __forceinline__ bool entry_ray(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, uint32_t i,
-                                          Ray& r, double& sig, uint32_t& p) {
-    if constexpr (kCam) {
-        uint32_t lx, ly;
-        if (!slot_pixel(b, fp, i, lx, ly)) return false;
-        r = camera_ray(sc, fp, lx, fp.row0 + ly);
-        sig = 1.0;                                    // raytrace.rs:273 via main.rs:54
-        p = ly * fp.tile_w + lx;
-    } else {
-        const int q = k & 1;
-        r = load_ray(b, q, i);
-        sig = b.qsig[q][i];
-        p = b.qpix[q][i];
-    }
-    return true;
 }
 
 // Sphere sources of the wavefront intersection kernels.
@@ -178,30 +212,36 @@ constexpr int kSrcBvhGS = 3;        // BVH from HBM/L2, register short stack
 constexpr int kSrcBvhL = 4;         // BVH + spheres in LDS, scratch stack
 constexpr int kSrcBvhLS = 5;        // BVH + spheres in LDS, register short stack
 constexpr int kSrcBvhP = 6;         // top of the BVH in LDS, spheres from HBM/L2, register short stack
+constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
 
 template <int kSrc>
 struct Src {
     static constexpr bool bvh = kSrc >= kSrcBvhG;
-    static constexpr bool sph_lds = kSrc == kSrcLds || kSrc == kSrcBvhL || kSrc == kSrcBvhLS;
-    static constexpr int nodes = (kSrc == kSrcBvhL || kSrc == kSrcBvhLS) ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
+    static constexpr bool sph_lds = kSrc == kSrcLds || kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc == kSrcBvhL8;
+    static constexpr int nodes = (kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc == kSrcBvhL8) ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
     static constexpr bool short_stack = kSrc == kSrcBvhGS || kSrc == kSrcBvhLS || kSrc == kSrcBvhP;
-    // all-LDS staging is ~60 KB per workgroup: 1024-thread groups share one copy between 16 waves
-    static constexpr int threads = nodes == 2 ? 1024 : 256;
+    static constexpr int waves = kSrc == kSrcBvhL8 ? 8 : 4;      // min waves per SIMD (__launch_bounds__)
 };
 
+// LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
-constexpr int threads_of() { return Src<kSrc>::threads; }
+__host__ __device__ inline size_t staged_bytes(int n_spheres, int lds_nodes) {
+    size_t bytes = 0;
+    if (kSrc == kSrcLds) bytes = static_cast<size_t>(n_spheres) * sizeof(DevSphere);
+    if (Src<kSrc>::nodes > 0) bytes = static_cast<size_t>(lds_nodes) * sizeof(DevBvhNode);
+    if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
+    return (bytes + 15) / 16 * 16;
+}
 
 // Stage what the source keeps in LDS; returns the view the queries use.
 template <int kSrc>
 __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b, unsigned char* lds) {
-    constexpr int T = threads_of<kSrc>();
+    constexpr int T = kWfThreads;
     BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj};
     if constexpr (kSrc == kSrcLds) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
-        __syncthreads();
     } else if constexpr (Src<kSrc>::nodes > 0) {
         DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
         for (int i = threadIdx.x; i < b.lds_nodes; i += T) ln[i] = sc.bvh[i];
@@ -214,7 +254,6 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b
             v.sph = ls;
             v.obj = lo;
         }
-        __syncthreads();
     }
     return v;
 }
@@ -233,7 +272,7 @@ __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& 
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
-// One atomic per wave into totals[at], totals[at + 1].
+// One atomic per wave into totals[at], totals[at + 1] (instrumented builds only).
 template <bool kCount>
 __device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
     if constexpr (kCount) {
@@ -254,31 +293,74 @@ __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c,
     b.nlev[p] = static_cast<uint8_t>(k);
 }
 
+// LDS of a queue kernel after its staged data.
+struct QueueLds {
+    uint32_t* scan;     // G + 1
+    uint32_t* wave;     // 16
+    uint32_t* count;    // 1
+};
+
+__device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
+    uint32_t* p = reinterpret_cast<uint32_t*>(at);
+    return QueueLds{p, p + G + 1, p + G + 1 + kWfThreads / 64};
+}
+
+__host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + 1) * 4u; }
+
 // Scene::intersect for every ray of Q_k (generation 0: the camera rays of the
 // chunk, computed here).  Outcomes that end the chain without lighting are
 // resolved on the spot (miss -> background; depth cut-off or insignificant
-// surface -> ambient, raytrace.rs:32-35); the rest become dense shade records.
+// surface -> ambient, raytrace.rs:32-35); the rest become shade records in
+// this workgroup's region.
 template <int kSrc, bool kCam, bool kCount>
-__global__ __launch_bounds__(threads_of<kSrc>()) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    constexpr int T = threads_of<kSrc>();
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const BvhView v = stage_lds<kSrc>(sc, b, lds);
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes), b.G);
+    if (threadIdx.x == 0) *ql.count = 0;
+    uint32_t n;
+    if constexpr (kCam) {
+        n = b.slots;
+        __syncthreads();                                   // publishes the LDS staging
+    } else {
+        region_scan(b.rq + k * b.G, b.G, ql.scan, ql.wave);
+        n = ql.scan[b.G];
+    }
     Work w;
-    const uint32_t n = kCam ? b.slots : b.cnt[kCntQ + k];
-    for (uint32_t base = blockIdx.x * T; base < n; base += gridDim.x * T) {
-        const uint32_t i = base + threadIdx.x;
+    const int q = k & 1;
+    const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
+    for (uint32_t base = blockIdx.x * kWfThreads; base < n; base += b.G * kWfThreads) {
+        const uint32_t j = base + threadIdx.x;
         bool shade = false;
         Ray r{};
         double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0;
         uint32_t p = 0;
         Hit h{};
-        if (i < n && entry_ray<kCam>(sc, fp, b, k, i, r, sig, p)) {
+        bool live = false;
+        if (j < n) {
+            if constexpr (kCam) {
+                uint32_t lx, ly;
+                if (slot_pixel(b, fp, j, lx, ly)) {
+                    r = camera_ray(sc, fp, lx, fp.row0 + ly);
+                    sig = 1.0;                              // raytrace.rs:273 via main.rs:54
+                    p = ly * fp.tile_w + lx;
+                    live = true;
+                }
+            } else {
+                const size_t at = region_entry(ql.scan, b.G, b.R, j);
+                r = load_ray(b, q, at);
+                sig = b.qsig[q][at];
+                p = b.qpix[q][at];
+                live = true;
+            }
+        }
+        if (live) {
             h = nearest_any<kSrc, kCount>(sc, v, r, &w);
             if (h.obj == INT32_MAX) {
-                set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);          // raytrace.rs:265, 228-232
+                set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);      // raytrace.rs:265, 228-232
             } else {
                 const DevMaterial& m = sc.mats[h.obj];
-                const bool lit = static_cast<uint32_t>(k) <= fp.max_depth &&       // raytrace.rs:33
+                const bool lit = static_cast<uint32_t>(k) <= fp.max_depth &&   // raytrace.rs:33
                                  (m.kd_sig * sig > kMinSignificance || m.ks_sig * sig > kMinSignificance);
                 if (!lit) {
                     set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
@@ -288,17 +370,20 @@ __global__ __launch_bounds__(threads_of<kSrc>()) void wf_nearest(DevScene sc, Fr
                 }
             }
         }
-        const uint32_t slot = wave_append(&b.cnt[kCntS + k], shade);
+        const uint32_t slot = lds_append(ql.count, shade);
         if (shade) {
-            b.sr_pt[0][slot] = ptx; b.sr_pt[1][slot] = pty; b.sr_pt[2][slot] = ptz;
-            b.sr_d[0][slot] = r.dx; b.sr_d[1][slot] = r.dy; b.sr_d[2][slot] = r.dz;
-            b.sr_sig[slot] = sig;
-            b.sr_obj[slot] = h.obj;
-            b.sr_prim[slot] = h.prim;
-            b.sr_pix[slot] = p;
-            b.occ[slot] = 0u;
+            const size_t at = obase + slot;
+            b.sr_pt[0][at] = ptx; b.sr_pt[1][at] = pty; b.sr_pt[2][at] = ptz;
+            b.sr_d[0][at] = r.dx; b.sr_d[1][at] = r.dy; b.sr_d[2][at] = r.dz;
+            b.sr_sig[at] = sig;
+            b.sr_obj[at] = h.obj;
+            b.sr_prim[at] = h.prim;
+            b.sr_pix[at] = p;
+            b.occ[at] = 0u;
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) b.rs[k * b.G + blockIdx.x] = *ql.count;
     flush_work<kCount>(b, 2, w);
 }
 
@@ -306,51 +391,60 @@ __global__ __launch_bounds__(threads_of<kSrc>()) void wf_nearest(DevScene sc, Fr
 // per (record, light) pair -- the lights of one hit are independent queries --
 // setting bit l of the record's occlusion mask.
 template <int kSrc, bool kCount>
-__global__ __launch_bounds__(threads_of<kSrc>()) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    constexpr int T = threads_of<kSrc>();
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const BvhView v = stage_lds<kSrc>(sc, b, lds);
-    Work w;
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes), b.G);
+    region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-    const uint32_t n = b.cnt[kCntS + k] * L;
-    for (uint32_t q = blockIdx.x * T + threadIdx.x; q < n; q += gridDim.x * T) {
-        const uint32_t j = q / L, l = q - j * L;
-        const double ptx = b.sr_pt[0][j], pty = b.sr_pt[1][j], ptz = b.sr_pt[2][j];
+    const uint32_t n = ql.scan[b.G] * L;
+    Work w;
+    for (uint32_t qi = blockIdx.x * kWfThreads + threadIdx.x; qi < n; qi += b.G * kWfThreads) {
+        const uint32_t j = qi / L, l = qi - j * L;
+        const size_t at = region_entry(ql.scan, b.G, b.R, j);
+        const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) atomicOr(&b.occ[j], 1u << l);
+        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) atomicOr(&b.occ[at], 1u << l);
     }
     flush_work<kCount>(b, 4, w);
 }
 
 // The Phong sum of every shade record (raytrace.rs:31-56), then either the
-// level push + reflection ray into Q_{k+1} (raytrace.rs:58-64) or the end of
-// the chain.
-__global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    const uint32_t n = b.cnt[kCntS + k];
+// level push + reflection ray into this workgroup's region of Q_{k+1}
+// (raytrace.rs:58-64) or the end of the chain.
+__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    __shared__ uint32_t s_scan[kMaxRegions + 1];
+    __shared__ uint32_t s_wave[kWfThreads / 64];
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    region_scan(b.rs + k * b.G, b.G, s_scan, s_wave);
+    const uint32_t n = s_scan[b.G];
     const int qn = (k + 1) & 1;
-    for (uint32_t base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
+    for (uint32_t base = blockIdx.x * kWfThreads; base < n; base += b.G * kWfThreads) {
         const uint32_t j = base + threadIdx.x;
         bool refl = false;
         Ray rr{};
         double nsig = 0.0;
         uint32_t p = 0;
         if (j < n) {
-            const double ptx = b.sr_pt[0][j], pty = b.sr_pt[1][j], ptz = b.sr_pt[2][j];
-            const double dx = b.sr_d[0][j], dy = b.sr_d[1][j], dz = b.sr_d[2][j];
-            const double sig = b.sr_sig[j];
-            const int32_t obj = b.sr_obj[j];
-            p = b.sr_pix[j];
+            const size_t at = region_entry(s_scan, b.G, b.R, j);
+            const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
+            const double dx = b.sr_d[0][at], dy = b.sr_d[1][at], dz = b.sr_d[2][at];
+            const double sig = b.sr_sig[at];
+            const int32_t obj = b.sr_obj[at];
+            p = b.sr_pix[at];
             const DevMaterial& m = sc.mats[obj];
             Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
             const bool diffuse = m.kd_sig * sig > kMinSignificance;
             const bool specular = m.ks_sig * sig > kMinSignificance;
             double nx, ny, nz;
-            hit_normal(sc, sc.spheres, b.sr_prim[j], ptx, pty, ptz, nx, ny, nz);
+            hit_normal(sc, sc.spheres, b.sr_prim[at], ptx, pty, ptz, nx, ny, nz);
             if (nx * dx + ny * dy + nz * dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
             if (sc.n_lights > 0) {
-                const uint32_t mask = b.occ[j];
+                const uint32_t mask = b.occ[at];
                 for (int l = 0; l < sc.n_lights; ++l) {
                     if ((mask >> l) & 1u) continue;                              // shadowed (raytrace.rs:42-49)
                     const DevLight& L = sc.lights[l];
@@ -360,9 +454,9 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
                 }
             }
             if (specular) {
-                const size_t at = static_cast<size_t>(k) * b.cap + p;
-                b.st[0][at] = res.r; b.st[1][at] = res.g; b.st[2][at] = res.b;
-                b.st_obj[at] = obj;
+                const size_t st = static_cast<size_t>(k) * b.cap + p;
+                b.st[0][st] = res.r; b.st[1][st] = res.g; b.st[2][st] = res.b;
+                b.st_obj[st] = obj;
                 rr = reflect_ray(Ray{0, 0, 0, dx, dy, dz}, ptx, pty, ptz, nx, ny, nz);
                 nsig = sig * m.ks_sig;
                 refl = true;
@@ -370,33 +464,29 @@ __global__ __launch_bounds__(kBlock) void wf_shade(DevScene sc, FrameParams fp, 
                 set_terminal(b, p, res, k);
             }
         }
-        const uint32_t slot = wave_append(&b.cnt[kCntQ + k + 1], refl);
+        const uint32_t slot = lds_append(&s_cnt, refl);
         if (refl) {
-            b.qo[qn][0][slot] = rr.ox; b.qo[qn][1][slot] = rr.oy; b.qo[qn][2][slot] = rr.oz;
-            b.qd[qn][0][slot] = rr.dx; b.qd[qn][1][slot] = rr.dy; b.qd[qn][2][slot] = rr.dz;
-            b.qsig[qn][slot] = nsig;
-            b.qpix[qn][slot] = p;
+            const size_t at = obase + slot;
+            b.qo[qn][0][at] = rr.ox; b.qo[qn][1][at] = rr.oy; b.qo[qn][2][at] = rr.oz;
+            b.qd[qn][0][at] = rr.dx; b.qd[qn][1][at] = rr.dy; b.qd[qn][2][at] = rr.dz;
+            b.qsig[qn][at] = nsig;
+            b.qpix[qn][at] = p;
         }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) b.rq[(k + 1) * b.G + blockIdx.x] = s_cnt;
 }
 
 // The fold factor of a level is the specular colour of its object
 // (raytrace.rs:63).
-__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, const double* ks_lds, uint32_t p) {
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p) {
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
     for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc
         const size_t at = static_cast<size_t>(k) * b.cap + p;
-        const int32_t obj = b.st_obj[at];
-        double k0, k1, k2;
-        if (ks_lds) {
-            k0 = ks_lds[3 * obj]; k1 = ks_lds[3 * obj + 1]; k2 = ks_lds[3 * obj + 2];
-        } else {
-            const DevMaterial& m = sc.mats[obj];
-            k0 = m.ks[0]; k1 = m.ks[1]; k2 = m.ks[2];
-        }
-        acc.r = b.st[0][at] + k0 * acc.r;
-        acc.g = b.st[1][at] + k1 * acc.g;
-        acc.b = b.st[2][at] + k2 * acc.b;
+        const DevMaterial& m = sc.mats[b.st_obj[at]];
+        acc.r = b.st[0][at] + m.ks[0] * acc.r;
+        acc.g = b.st[1][at] + m.ks[1] * acc.g;
+        acc.b = b.st[2][at] + m.ks[2] * acc.b;
     }
     return acc;
 }
@@ -405,23 +495,19 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, c
 // BGR rows unpadded and dword aligned): the block assembles its 3 KiB of RGB
 // and 768 B of BGR in LDS and stores them as whole dwords.
 template <bool kStaged>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, int n_objects) {
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
-    // (an LDS table of the fold factors was measured slower: 52 KB per block
-    // cut occupancy more than the gathers it saved)
-    const double* ks_lds = nullptr;
-    (void)n_objects;
     const uint32_t npix = fp.tile_w * fp.rows;
     for (uint32_t base = blockIdx.x * kBlock; base < npix; base += gridDim.x * kBlock) {
         const uint32_t p = base + threadIdx.x;
         if constexpr (!kStaged) {
             if (p < npix) {
-                const Col res = average_samples(fold_pixel(sc, b, ks_lds, p), fp.spp);
+                const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
                 write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res);
             }
         } else {
-            const Col res = average_samples(fold_pixel(sc, b, ks_lds, p), fp.spp);   // npix % 256 == 0 here
+            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
             s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
             s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
             s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
@@ -445,17 +531,35 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
 }
 
 // Scene::intersect calls of this chunk: every pixel's camera ray, every later
-// queue entry, and one shadow query per light per shaded hit.
-// (atomics: chunks on different streams finish concurrently)
-__global__ void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
-    const int t = threadIdx.x;                                  // kCntWords threads
-    atomicAdd(&b.gen_totals[t], static_cast<unsigned long long>(b.cnt[t]));
-    if (t == 0) {
+// queue entry, and one shadow query per light per shade record; plus the
+// per-generation queue sizes.  One workgroup; atomics because chunks on
+// different streams may finish together.
+__global__ __launch_bounds__(kBlock) void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
+    __shared__ unsigned long long s_sum[2 * kMaxGenerations];
+    for (int t = threadIdx.x; t < 2 * kMaxGenerations; t += kBlock) s_sum[t] = 0;
+    __syncthreads();
+    for (int g = 0; g < generations; ++g) {
+        unsigned long long q = 0, sh = 0;
+        for (uint32_t r = threadIdx.x; r < b.G; r += kBlock) {
+            if (g > 0) q += b.rq[g * b.G + r];
+            sh += b.rs[g * b.G + r];
+        }
+        atomicAdd(&s_sum[g], q);
+        atomicAdd(&s_sum[kMaxGenerations + g], sh);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
         unsigned long long nearest = static_cast<unsigned long long>(fp.tile_w) * fp.rows, shadow = 0;
-        for (int k = 1; k < generations; ++k) nearest += b.cnt[kCntQ + k];
-        for (int k = 0; k < generations; ++k) shadow += static_cast<unsigned long long>(b.cnt[kCntS + k]) * n_lights;
+        for (int g = 0; g < generations; ++g) {
+            nearest += s_sum[g];
+            shadow += s_sum[kMaxGenerations + g] * n_lights;
+        }
         atomicAdd(&b.totals[0], nearest * fp.spp);
         atomicAdd(&b.totals[1], shadow * fp.spp);
+    }
+    for (int g = threadIdx.x; g < generations; g += kBlock) {
+        atomicAdd(&b.gen_totals[kCntQ + g], s_sum[g]);
+        atomicAdd(&b.gen_totals[kCntS + g], s_sum[kMaxGenerations + g]);
     }
 }
 
@@ -481,40 +585,19 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
     return hipGetLastError();
 }
 
-// One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
-// must be zero on entry (the caller memsets them).
-template <int kSrc>
-size_t lds_bytes_of(const DevScene& sc, const WfBufs& b) {
-    size_t bytes = 0;
-    if constexpr (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
-    if constexpr (Src<kSrc>::nodes > 0) bytes = static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode);
-    if constexpr (Src<kSrc>::bvh && Src<kSrc>::sph_lds)
-        bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
-    return bytes;
-}
-
 template <int kSrc, bool kCount>
 void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s) {
-    constexpr int T = threads_of<kSrc>();
-    const size_t lds = lds_bytes_of<kSrc>(sc, b);
-    // Workgroups that stage LDS are kept resident-sized (the copy is per block);
-    // the others fill every SIMD.
-    const uint64_t cap = kSrc == kSrcLds ? 1024 : Src<kSrc>::nodes == 2 ? 512 : 16384;
-    const int gq = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((b.slots + T - 1) / T, cap)));
-    const int gs = blocks_for(b.slots, 8192);
-    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
-    else hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), dim3(gq), dim3(T), lds, s, sc, fp, b, k);
-    if (sc.n_lights > 0) {
-        const uint64_t items = static_cast<uint64_t>(b.slots) * sc.n_lights;
-        const int go = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((items + T - 1) / T, cap)));
-        hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), dim3(go), dim3(T), lds, s, sc, fp, b, k);
-    }
-    hipLaunchKernelGGL(wf_shade, dim3(gs), dim3(kBlock), 0, s, sc, fp, b, k);
+    const size_t lds = staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes) + queue_lds_bytes(b.G);
+    const dim3 grid(b.G), block(kWfThreads);
+    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), grid, block, lds, s, sc, fp, b, k);
+    else hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), grid, block, lds, s, sc, fp, b, k);
+    if (sc.n_lights > 0) hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), grid, block, lds, s, sc, fp, b, k);
+    hipLaunchKernelGGL(wf_shade, grid, block, 0, s, sc, fp, b, k);
 }
 
-// One chunk (fp.row0, fp.rows) through every generation.  Counters in b.cnt
-// must be zero on entry (the caller memsets them).  src: 0 brute/global,
-// 1 brute/LDS, 2 BVH.
+// One chunk (fp.row0, fp.rows) through every generation.  src: the sphere
+// source (kSrc*); count: instrumented kernels; mark is recorded on s after
+// generation mark_gen has been launched (chunk pipelining across streams).
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
                             hipStream_t s, hipEvent_t mark, int mark_gen) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
@@ -527,7 +610,8 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvhGS: RT_GEN(kSrcBvhGS); break;
         case kSrcBvhL: RT_GEN(kSrcBvhL); break;
         case kSrcBvhLS: RT_GEN(kSrcBvhLS); break;
-        default: RT_GEN(kSrcBvhP); break;
+        case kSrcBvhP: RT_GEN(kSrcBvhP); break;
+        default: RT_GEN(kSrcBvhL8); break;
         }
 #undef RT_GEN
         if (mark && k == mark_gen) {
@@ -538,10 +622,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
     const dim3 gf(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048));
-    const int n_objects = sc.n_spheres + sc.n_planes;
-    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
-    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b, n_objects);
-    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kCntWords), 0, s, fp, b, sc.n_lights, gens);
+    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kBlock), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }
 

@@ -395,13 +395,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         int32_t lds_nodes = 0;
         // sources: 2 BVH/L2 + scratch stack, 3 BVH/L2 + register stack, 4 BVH+spheres in LDS +
         // scratch stack, 5 the same + register stack, 6 top of BVH in LDS + register stack,
-        // 7 = 4 held to 64 VGPRs (two workgroups per CU)
+        // 7 = 4 held to 64 VGPRs (two workgroups per CU), 8 / 9 = 7 with 1 / 2 stack entries in registers
         const char* force = std::getenv("RT_WF_SRC");          // experiment override
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool all_fit = node_bytes + sph_bytes <= kLdsBudget;
-            src = force ? std::atoi(force) : (all_fit ? 4 : 2);
-            if (src < 2 || src > 7 || ((src == 4 || src == 5 || src == 7) && !all_fit)) src = 2;
-            if (src == 4 || src == 5 || src == 7) lds_nodes = c->dsc.n_bvh;
+            src = force ? std::atoi(force) : (all_fit ? 7 : 2);
+            const bool needs_all = src == 4 || src == 5 || src >= 7;
+            if (src < 2 || src > 9 || (needs_all && !all_fit)) src = 2;
+            if (src == 4 || src == 5 || src >= 7) lds_nodes = c->dsc.n_bvh;
             else if (src == 6)
                 lds_nodes = static_cast<int32_t>(std::min<size_t>(c->dsc.n_bvh, 32 * 1024 / sizeof(DevBvhNode)));
         } else {
@@ -418,10 +419,11 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
         const uint32_t cap = o->tile_w * chunk_rows;
-        // G regions: two resident 1024-thread workgroups per CU (the LDS-staged
-        // BVH allows no more), fewer for small chunks; R covers every slot.
+        // G regions = workgroups per queue launch: four per CU (two resident
+        // 1024-thread workgroups with the LDS-staged BVH, so two rounds),
+        // fewer for small chunks; R covers every slot.
         const int g_env = env_int("RT_WF_REGIONS", 0);
-        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
+        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 4u * static_cast<uint32_t>(c->n_cu);
         G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
         const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
         for (int l = 0; l < n_lanes; ++l) {

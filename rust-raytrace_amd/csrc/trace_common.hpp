@@ -41,18 +41,20 @@ struct Col {
 __device__ __forceinline__ double clamp_zero(double x) { return x < 0.0 ? 0.0 : x; }   // raytrace.rs:20-23
 
 // color.rs:593-600 as a binary search over the strictly increasing table.
-__device__ __forceinline__ uint8_t to_srgb(double v) {
-    if (!(v < c_srgb_avg[254])) return 255;      // also NaN
+__device__ __forceinline__ uint8_t to_srgb(double v, const double* table) {
+    if (!(v < table[254])) return 255;           // also NaN
     int lo = 0, hi = 254;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         int mid = (lo + hi) >> 1;
-        bool lt = v < c_srgb_avg[mid];
+        bool lt = v < table[mid];
         hi = lt ? mid : hi;
         lo = lt ? lo : mid + 1;
     }
     return static_cast<uint8_t>(lo);
 }
+
+__device__ __forceinline__ uint8_t to_srgb(double v) { return to_srgb(v, c_srgb_avg); }
 
 // shapes.rs:60-89: the exact quadratic; true + the t the reference returns, or
 // false for None.  `a2` = 2.0*a, `a4` = 4.0*a are hoisted per ray (the same
@@ -250,62 +252,49 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
 }
 
 // Traversal stacks, declared as plain locals so the compiler keeps the stack
-// pointer (and, for the short stack, the top entries) in registers.
-//  * memory stack: entries in a private array (scratch, cached in L1/L2);
-//  * short stack: the top kRegStack entries in registers, shifted with v_mov
-//    on push/pop (constant indices after unrolling); deeper entries spill to
-//    a private array.
+// pointer (and the register part) in registers.  The top kReg entries live in
+// registers, shifted with v_mov on push/pop (constant indices after
+// unrolling); deeper entries live in a private array (scratch, cached in
+// L1/L2).  A pop refills the register part from scratch, so the load's
+// latency overlaps the traversal work before the entry is needed; with
+// kReg = 0 every pop waits for its scratch load.  The nearest query packs
+// (node, entry t) into one 64-bit entry: one scratch access per push / pop.
 // The host bounds the tree depth, so kBvhStack entries always suffice.
-constexpr int kRegStack = 8;
-
-#define RT_STACK_DECL(kShort, kWithT)                                                  \
-    int32_t stk_p[kShort ? kRegStack : kBvhStack];                                     \
-    float stk_t[kShort ? kRegStack : kBvhStack];                                       \
-    int32_t ovf_p[kShort ? kBvhStack - kRegStack : 1];                                 \
-    float ovf_t[kShort ? kBvhStack - kRegStack : 1];                                   \
+#define RT_STACK_DECL(kReg, E)                                                         \
+    E stk_m[kBvhStack];                                                                \
+    E stk_r[(kReg) > 0 ? (kReg) : 1];                                                  \
     int stk_n = 0;                                                                     \
-    auto stk_push = [&](int32_t v, float tv) {                                         \
-        if constexpr (kShort) {                                                        \
-            if (stk_n >= kRegStack) {                                                  \
-                ovf_p[stk_n - kRegStack] = stk_p[kRegStack - 1];                       \
-                if constexpr (kWithT) ovf_t[stk_n - kRegStack] = stk_t[kRegStack - 1]; \
-            }                                                                          \
-            _Pragma("unroll") for (int q = kRegStack - 1; q > 0; --q) {                \
-                stk_p[q] = stk_p[q - 1];                                               \
-                if constexpr (kWithT) stk_t[q] = stk_t[q - 1];                         \
-            }                                                                          \
-            stk_p[0] = v;                                                              \
-            if constexpr (kWithT) stk_t[0] = tv;                                       \
+    auto stk_push = [&](E v) {                                                         \
+        if constexpr ((kReg) > 0) {                                                    \
+            if (stk_n >= (kReg)) stk_m[stk_n - (kReg)] = stk_r[(kReg) - 1];            \
+            _Pragma("unroll") for (int q = (kReg) - 1; q > 0; --q) stk_r[q] = stk_r[q - 1]; \
+            stk_r[0] = v;                                                              \
         } else {                                                                       \
-            stk_p[stk_n] = v;                                                          \
-            if constexpr (kWithT) stk_t[stk_n] = tv;                                   \
+            stk_m[stk_n] = v;                                                          \
         }                                                                              \
         ++stk_n;                                                                       \
     };                                                                                 \
-    auto stk_pop = [&](float& tv) -> int32_t {                                         \
+    auto stk_pop = [&]() -> E {                                                        \
         --stk_n;                                                                       \
-        int32_t v;                                                                     \
-        if constexpr (kShort) {                                                        \
-            v = stk_p[0];                                                              \
-            if constexpr (kWithT) tv = stk_t[0];                                       \
-            _Pragma("unroll") for (int q = 0; q < kRegStack - 1; ++q) {                \
-                stk_p[q] = stk_p[q + 1];                                               \
-                if constexpr (kWithT) stk_t[q] = stk_t[q + 1];                         \
-            }                                                                          \
-            if (stk_n >= kRegStack) {                                                  \
-                stk_p[kRegStack - 1] = ovf_p[stk_n - kRegStack];                       \
-                if constexpr (kWithT) stk_t[kRegStack - 1] = ovf_t[stk_n - kRegStack]; \
-            }                                                                          \
+        if constexpr ((kReg) > 0) {                                                    \
+            const E v = stk_r[0];                                                      \
+            _Pragma("unroll") for (int q = 0; q < (kReg) - 1; ++q) stk_r[q] = stk_r[q + 1]; \
+            if (stk_n >= (kReg)) stk_r[(kReg) - 1] = stk_m[stk_n - (kReg)];            \
+            return v;                                                                  \
         } else {                                                                       \
-            v = stk_p[stk_n];                                                          \
-            if constexpr (kWithT) tv = stk_t[stk_n];                                   \
+            return stk_m[stk_n];                                                       \
         }                                                                              \
-        return v;                                                                      \
     }
+
+__device__ __forceinline__ uint64_t stk_entry(int32_t node, float t) {
+    return (static_cast<uint64_t>(__float_as_uint(t)) << 32) | static_cast<uint32_t>(node);
+}
+__device__ __forceinline__ int32_t stk_node(uint64_t e) { return static_cast<int32_t>(static_cast<uint32_t>(e)); }
+__device__ __forceinline__ float stk_t(uint64_t e) { return __uint_as_float(static_cast<uint32_t>(e >> 32)); }
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
-template <bool kCount = false, int kNodes = 0, bool kShort = false>
+template <bool kCount = false, int kNodes = 0, int kReg = 0>
 __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
@@ -313,7 +302,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    RT_STACK_DECL(kShort, true);
+    RT_STACK_DECL(kReg, uint64_t);
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
@@ -324,7 +313,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                stk_push(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
+                stk_push(stk_entry(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0));
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -345,17 +334,17 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
             }
         }
         // pop, skipping entries that the current best already rules out
-        float tn = 0.0f;
         for (;;) {
             if (stk_n == 0) return h;
-            cur = stk_pop(tn);
-            if (tn <= tlim) break;
+            const uint64_t e = stk_pop();
+            cur = stk_node(e);
+            if (stk_t(e) <= tlim) break;
         }
     }
 }
 
 // The shadow query (see occluded_brute for the any-hit equivalence).
-template <bool kCount = false, int kNodes = 0, bool kShort = false>
+template <bool kCount = false, int kNodes = 0, int kReg = 0>
 __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w = nullptr) {
     bool plane_block = false;
@@ -373,7 +362,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
-    RT_STACK_DECL(kShort, false);
+    RT_STACK_DECL(kReg, int32_t);
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
@@ -384,7 +373,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
             if (h0 && h1) {
                 const bool first0 = t0 <= t1;
-                stk_push(first0 ? nd.c1 : nd.c0, 0.0f);
+                stk_push(first0 ? nd.c1 : nd.c0);
                 cur = first0 ? nd.c0 : nd.c1;
                 continue;
             }
@@ -399,8 +388,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
             }
         }
         if (stk_n == 0) return false;
-        float tn;
-        cur = stk_pop(tn);
+        cur = stk_pop();
     }
 }
 
@@ -490,7 +478,8 @@ __device__ __forceinline__ Col average_samples(Col c, uint32_t spp) {
     return Col{res.r / aa, res.g / aa, res.b / aa};
 }
 
-__device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, uint32_t out_row, Col res) {
+__device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, uint32_t out_row, Col res,
+                                            const double* srgb = c_srgb_avg) {
     const size_t p = static_cast<size_t>(out_row) * fp.tile_w + lx;
     if (fp.out_rgb) {
         fp.out_rgb[3 * p + 0] = static_cast<float>(res.r);
@@ -499,9 +488,9 @@ __device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, 
     }
     if (fp.out_bgr) {
         uint8_t* q = fp.out_bgr + static_cast<size_t>(out_row) * fp.bgr_pitch + 3u * lx;
-        q[0] = to_srgb(res.b);
-        q[1] = to_srgb(res.g);
-        q[2] = to_srgb(res.r);
+        q[0] = to_srgb(res.b, srgb);
+        q[1] = to_srgb(res.g, srgb);
+        q[2] = to_srgb(res.r, srgb);
         if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
             for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k)
                 fp.out_bgr[static_cast<size_t>(out_row) * fp.bgr_pitch + k] = 0;

@@ -213,14 +213,19 @@ constexpr int kSrcBvhL = 4;         // BVH + spheres in LDS, scratch stack
 constexpr int kSrcBvhLS = 5;        // BVH + spheres in LDS, register short stack
 constexpr int kSrcBvhP = 6;         // top of the BVH in LDS, spheres from HBM/L2, register short stack
 constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
+constexpr int kSrcBvhL8R1 = 8;      // kSrcBvhL8 with the top stack entry in registers
+constexpr int kSrcBvhL8R2 = 9;      // kSrcBvhL8 with the top two stack entries in registers
 
 template <int kSrc>
 struct Src {
     static constexpr bool bvh = kSrc >= kSrcBvhG;
-    static constexpr bool sph_lds = kSrc == kSrcLds || kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc == kSrcBvhL8;
-    static constexpr int nodes = (kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc == kSrcBvhL8) ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
-    static constexpr bool short_stack = kSrc == kSrcBvhGS || kSrc == kSrcBvhLS || kSrc == kSrcBvhP;
-    static constexpr int waves = kSrc == kSrcBvhL8 ? 8 : 4;      // min waves per SIMD (__launch_bounds__)
+    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc >= kSrcBvhL8;
+    static constexpr bool sph_lds = kSrc == kSrcLds || all_lds;
+    static constexpr int nodes = all_lds ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
+    // traversal stack entries held in registers
+    static constexpr int reg = (kSrc == kSrcBvhGS || kSrc == kSrcBvhLS || kSrc == kSrcBvhP) ? 8
+                             : kSrc == kSrcBvhL8R1 ? 1 : kSrc == kSrcBvhL8R2 ? 2 : 0;
+    static constexpr int waves = kSrc >= kSrcBvhL8 ? 8 : 4;      // min waves per SIMD (__launch_bounds__)
 };
 
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
@@ -260,7 +265,7 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
-    if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::short_stack>(sc, v, r, w);
+    if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::reg>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
 
@@ -268,7 +273,7 @@ template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w) {
     if constexpr (Src<kSrc>::bvh)
-        return occluded_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::short_stack>(sc, v, r, has_range, r2, w);
+        return occluded_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::reg>(sc, v, r, has_range, r2, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
@@ -478,54 +483,83 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 }
 
 // The fold factor of a level is the specular colour of its object
-// (raytrace.rs:63).
+// (raytrace.rs:63).  The chain is folded inner-first exactly as the
+// recursion returns (acc = res_k + ks_k * acc); the loads of four levels are
+// issued together so a pixel costs about two memory round trips per four
+// levels instead of two per level.
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p) {
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
-    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; --k) {       // res_k + ks_k * acc
-        const size_t at = static_cast<size_t>(k) * b.cap + p;
-        const DevMaterial& m = sc.mats[b.st_obj[at]];
-        acc.r = b.st[0][at] + m.ks[0] * acc.r;
-        acc.g = b.st[1][at] + m.ks[1] * acc.g;
-        acc.b = b.st[2][at] + m.ks[2] * acc.b;
+    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; k -= 4) {
+        double sr[4], sg[4], sb[4];
+        int32_t ob[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k - u >= 0) {
+                const size_t at = static_cast<size_t>(k - u) * b.cap + p;
+                ob[u] = b.st_obj[at];
+                sr[u] = b.st[0][at]; sg[u] = b.st[1][at]; sb[u] = b.st[2][at];
+            }
+        }
+        double kr[4], kg[4], kb[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k - u >= 0) {
+                const DevMaterial& m = sc.mats[ob[u]];
+                kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k - u >= 0) {
+                acc.r = sr[u] + kr[u] * acc.r;
+                acc.g = sg[u] + kg[u] * acc.g;
+                acc.b = sb[u] + kb[u] * acc.b;
+            }
+        }
     }
     return acc;
 }
 
-// kStaged: every group of 256 pixels lies in one output row (tile_w % 256 == 0,
-// BGR rows unpadded and dword aligned): the block assembles its 3 KiB of RGB
-// and 768 B of BGR in LDS and stores them as whole dwords.
+// One pixel per work-item.  The quantisation table is staged in LDS: the
+// binary search indexes it with a different entry per lane, which from
+// __constant__ memory costs nine dependent vector loads per channel.
+// kStaged: each workgroup's 256 pixels lie in one output row (tile_w % 256
+// == 0, BGR rows unpadded and dword aligned): the workgroup assembles its
+// 3 KiB of RGB and 768 B of BGR in LDS and stores them as whole dwords.
 template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
+    __shared__ double s_srgb[255];
+    for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
     const uint32_t npix = fp.tile_w * fp.rows;
-    for (uint32_t base = blockIdx.x * kBlock; base < npix; base += gridDim.x * kBlock) {
-        const uint32_t p = base + threadIdx.x;
-        if constexpr (!kStaged) {
-            if (p < npix) {
-                const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
-                write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res);
-            }
-        } else {
-            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
-            s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
-            s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
-            s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
-            uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr);
-            sb[3 * threadIdx.x + 0] = to_srgb(res.b);
-            sb[3 * threadIdx.x + 1] = to_srgb(res.g);
-            sb[3 * threadIdx.x + 2] = to_srgb(res.r);
-            __syncthreads();
-            const uint32_t row = fp.row0 + base / fp.tile_w, lx0 = base % fp.tile_w;
-            if (fp.out_rgb) {
-                float* dst = fp.out_rgb + (static_cast<size_t>(row) * fp.tile_w + lx0) * 3;
-                for (int q = threadIdx.x; q < 3 * kBlock; q += kBlock) dst[q] = s_rgb[q];
-            }
-            if (fp.out_bgr && threadIdx.x < 3 * kBlock / 4) {
-                uint32_t* dst = reinterpret_cast<uint32_t*>(fp.out_bgr + static_cast<size_t>(row) * fp.bgr_pitch + 3 * lx0);
-                dst[threadIdx.x] = s_bgr[threadIdx.x];
-            }
-            __syncthreads();
+    const uint32_t base = blockIdx.x * kBlock;
+    const uint32_t p = base + threadIdx.x;
+    if constexpr (!kStaged) {
+        __syncthreads();
+        if (p < npix) {
+            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
+            write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+        }
+    } else {
+        const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
+        s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
+        s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
+        s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
+        __syncthreads();                                   // also publishes s_srgb
+        uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr);
+        sb[3 * threadIdx.x + 0] = to_srgb(res.b, s_srgb);
+        sb[3 * threadIdx.x + 1] = to_srgb(res.g, s_srgb);
+        sb[3 * threadIdx.x + 2] = to_srgb(res.r, s_srgb);
+        const uint32_t row = fp.row0 + base / fp.tile_w, lx0 = base % fp.tile_w;
+        if (fp.out_rgb) {
+            float* dst = fp.out_rgb + (static_cast<size_t>(row) * fp.tile_w + lx0) * 3;
+            for (int q = threadIdx.x; q < 3 * kBlock; q += kBlock) dst[q] = s_rgb[q];
+        }
+        __syncthreads();
+        if (fp.out_bgr && threadIdx.x < 3 * kBlock / 4) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(fp.out_bgr + static_cast<size_t>(row) * fp.bgr_pitch + 3 * lx0);
+            dst[threadIdx.x] = s_bgr[threadIdx.x];
         }
     }
 }
@@ -534,18 +568,18 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
 // queue entry, and one shadow query per light per shade record; plus the
 // per-generation queue sizes.  One workgroup; atomics because chunks on
 // different streams may finish together.
-__global__ __launch_bounds__(kBlock) void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
+__global__ __launch_bounds__(kWfThreads) void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
     __shared__ unsigned long long s_sum[2 * kMaxGenerations];
-    for (int t = threadIdx.x; t < 2 * kMaxGenerations; t += kBlock) s_sum[t] = 0;
-    __syncthreads();
-    for (int g = 0; g < generations; ++g) {
-        unsigned long long q = 0, sh = 0;
-        for (uint32_t r = threadIdx.x; r < b.G; r += kBlock) {
-            if (g > 0) q += b.rq[g * b.G + r];
-            sh += b.rs[g * b.G + r];
-        }
-        atomicAdd(&s_sum[g], q);
-        atomicAdd(&s_sum[kMaxGenerations + g], sh);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // one wave per (generation, queue|records) pair, lanes striding the regions
+    for (int item = wave; item < 2 * generations; item += kWfThreads / 64) {
+        const int g = item >> 1;
+        const uint32_t* src = (item & 1) ? b.rs : b.rq;
+        unsigned long long v = 0;
+        if ((item & 1) || g > 0)
+            for (uint32_t r = lane; r < b.G; r += 64) v += src[g * b.G + r];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0) s_sum[(item & 1) ? kMaxGenerations + g : g] = v;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -557,16 +591,10 @@ __global__ __launch_bounds__(kBlock) void wf_tally(FrameParams fp, WfBufs b, int
         atomicAdd(&b.totals[0], nearest * fp.spp);
         atomicAdd(&b.totals[1], shadow * fp.spp);
     }
-    for (int g = threadIdx.x; g < generations; g += kBlock) {
+    for (int g = threadIdx.x; g < generations; g += kWfThreads) {
         atomicAdd(&b.gen_totals[kCntQ + g], s_sum[g]);
         atomicAdd(&b.gen_totals[kCntS + g], s_sum[kMaxGenerations + g]);
     }
-}
-
-inline int blocks_for(uint64_t items, int cap_blocks) {
-    uint64_t b = (items + kBlock - 1) / kBlock;
-    if (b < 1) b = 1;
-    return static_cast<int>(b < static_cast<uint64_t>(cap_blocks) ? b : cap_blocks);
 }
 
 }  // namespace
@@ -611,7 +639,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvhL: RT_GEN(kSrcBvhL); break;
         case kSrcBvhLS: RT_GEN(kSrcBvhLS); break;
         case kSrcBvhP: RT_GEN(kSrcBvhP); break;
-        default: RT_GEN(kSrcBvhL8); break;
+        case kSrcBvhL8: RT_GEN(kSrcBvhL8); break;
+        case kSrcBvhL8R1: RT_GEN(kSrcBvhL8R1); break;
+        default: RT_GEN(kSrcBvhL8R2); break;
         }
 #undef RT_GEN
         if (mark && k == mark_gen) {
@@ -621,10 +651,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
-    const dim3 gf(blocks_for(static_cast<uint64_t>(fp.tile_w) * fp.rows, 2048));
+    const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
     if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
     else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
-    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kBlock), 0, s, fp, b, sc.n_lights, gens);
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);
     return hipGetLastError();
 }
 

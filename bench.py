@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--algo", default="auto", choices=["auto", "wavefront", "lds", "global"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-kernel-times", action="store_true",
+                   help="do not record HIP events between the launches of the timed frames")
     return p.parse_args()
 
 
@@ -119,14 +121,21 @@ def main():
     # torch events below bracket the kernel (handle 0 would select the context's own stream)
     stream = torch.cuda.Stream(dev)
 
-    def step():
-        ctx.render_device(opts, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
+    # timed frames also record a HIP event after every launch (RT_TIME_KERNELS):
+    # per-kernel-family launch durations over exactly the timed region
+    timed_flags = opts.flags | (0 if args.no_kernel_times else lr.RT_TIME_KERNELS)
+    opts_timed = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+                                max_depth=args.depth, spp=1, algo=algo, flags=timed_flags)
+
+    def step(o=opts):
+        ctx.render_device(o, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     st = ctx.stats()                       # rays of one frame-slice (deterministic: same every step)
     local_rays = st.rays
+    ctx.kernel_times()                     # discard anything recorded before the timed region
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -135,7 +144,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        step()
+        step(opts_timed)
         evs[i][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -143,6 +152,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    ktimes = ctx.kernel_times()            # {family: (ms summed over the K timed frames, launches)}
 
     # one more, untimed frame with the instrumented kernels: exact box / sphere test counts
     work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
@@ -179,6 +189,14 @@ def main():
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
         key = f"c3_{W}x{H}_n{args.spheres}_d{args.depth}"
         traffic = pmc_traffic(key)
+        kernels = {}
+        for fam, (ms, n) in ktimes.items():
+            if n:
+                kernels["wf_" + fam] = {"avg_launch_us": round(ms / n * 1e3, 2),
+                                        "launches_per_frame": round(n / args.steps, 2),
+                                        "ms_per_frame": round(ms / args.steps, 4),
+                                        "share_of_frame": round(ms / args.steps / avg_kernel_ms, 4)}
+        dominant = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else None
         line = {
             "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -195,12 +213,13 @@ def main():
                          "kernel": "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
                                    "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernels": kernels or None, "dominant_kernel": dominant,
                          "note": "VALU-bound path (f64 exact tests, f32 BVH boxes); HBM fraction reported "
                                  "because the metric asks for it; see 'compute'"},
             "compute": {"bound": "valu", "sphere_tests_per_frame": sphere_tests, "box_tests_per_frame": box_tests,
                         "f64_flops_per_sphere_test": 19, "f32_flops_per_box_test": 20,
-                        "achieved_f64_tflops": round(sphere_tests * 19 / (avg_kernel_ms * 1e-3) / 1e12 * world, 3),
-                        "achieved_f32_box_tflops": round(box_tests * 20 / (avg_kernel_ms * 1e-3) / 1e12 * world, 3),
+                        "achieved_f64_tflops": round(sphere_tests * 19 / (avg_kernel_ms * 1e-3) / 1e12, 3),
+                        "achieved_f32_box_tflops": round(box_tests * 20 / (avg_kernel_ms * 1e-3) / 1e12, 3),
                         "peak_f64_tflops": FP64_VALU_PEAK_TFLOPS,
                         "tests_per_ray": round((sphere_tests + box_tests) / max(1, total_rays), 2),
                         "generation_queue_sizes": gen_q[:args.depth + 3] if world == 1 else None,

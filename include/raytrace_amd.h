@@ -140,7 +140,8 @@ enum rt_jitter { RT_JITTER_CENTER = 0 };   /* jx = jy = 0.5 (deterministic parit
 enum rt_out_flags {
     RT_OUT_RGB_F32 = 1,
     RT_OUT_BGR_U8 = 2,
-    RT_COUNT_WORK = 4          /* also count box / sphere tests (instrumented kernels; wavefront only) */
+    RT_COUNT_WORK = 4,         /* also count box / sphere tests (instrumented kernels; wavefront only) */
+    RT_TIME_KERNELS = 8        /* record a timing event after every launch (wavefront, one stream) */
 };
 enum rt_algo {
     RT_ALGO_AUTO = 0,
@@ -189,6 +190,14 @@ int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
  * (generation 0: 0, the camera rays are not queued), shaded[k] = hits that
  * issued shadow queries.  Diagnostic. */
 int rt_ctx_generation_counts(rt_ctx* ctx, uint32_t* queue, uint32_t* shaded, int n);
+/* Per kernel family, over every RT_TIME_KERNELS render since the previous
+ * call: summed launch time (ms, hipEvent pairs around each launch) and launch
+ * count; then resets.  Synchronises with the last timed launch.  Families:
+ * rt_kernel_family.  Renders split over several chunk streams are not timed. */
+enum rt_kernel_family {
+    RT_KF_NEAREST = 0, RT_KF_OCCLUSION = 1, RT_KF_SHADE = 2, RT_KF_FOLD = 3, RT_KF_TALLY = 4, RT_KF_COUNT = 5
+};
+int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 
 #ifdef __cplusplus
 }

@@ -16,8 +16,19 @@ struct BvhResult {
     int32_t root = 0;               // encoded pointer (node index, or ~leaf when the whole set is one leaf)
 };
 
-// Spheres (centre, radius); `pad` widens every box before f32 outward rounding.
+// Spheres (centre, radius); `pad` widens every box before f32 outward rounding;
+// leaves hold at most `leaf_max` (1..8) spheres.
 BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& cz,
-                           const std::vector<double>& radius, double pad);
+                           const std::vector<double>& radius, double pad, int leaf_max);
+
+// 4-wide BVH collapsed from a binary one (same leaves, same f32 boxes), in
+// the device's plane-major layout (device_layout.hpp, DevBvh4): plane k of
+// node i at planes[k * n_nodes + i].
+struct Bvh4Result {
+    std::vector<DevBvh4Plane> planes;   // kBvh4Planes * n_nodes
+    int32_t n_nodes = 0;
+    int32_t root = 0;                   // encoded pointer, as in DevBvhNode
+};
+Bvh4Result collapse_bvh4(const BvhResult& b2);
 
 }  // namespace rtamd

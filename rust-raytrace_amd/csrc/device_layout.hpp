@@ -48,6 +48,21 @@ struct alignas(16) DevBvhNode {
 };
 static_assert(sizeof(DevBvhNode) == 64, "BVH node is one 64-B line");
 
+// 4-wide BVH, plane-major: node i's child boxes and pointers are 7 16-byte
+// planes, plane k at index k * n_nodes + i (lo.x, hi.x, lo.y, hi.y, lo.z,
+// hi.z of the 4 children, then the 4 child pointers).  A wave's lanes reading
+// plane k of 16 different nodes hit 16 different LDS bank slots (an
+// array-of-nodes layout would put them on 2).  Child pointers as in
+// DevBvhNode; kBvh4Empty marks an unused slot.
+struct alignas(16) DevBvh4Plane {
+    union {
+        float f[4];
+        int32_t i[4];
+    };
+};
+constexpr int kBvh4Planes = 7;
+constexpr int32_t kBvh4Empty = INT32_MIN;
+
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -58,6 +73,8 @@ struct DevScene {
     const DevBvhNode* bvh;          // sphere BVH (spheres[] are in its leaf order)
     int32_t bvh_root;               // encoded child pointer of the root (see DevBvhNode)
     int32_t n_spheres, n_planes, n_lights, n_bvh;
+    const DevBvh4Plane* bvh4;       // the same tree collapsed 4-wide (DevBvh4Plane)
+    int32_t bvh4_root, n_bvh4;
     double cam_pos[3];
     double cam_m[9];                // row-major
     double bg[3];
@@ -107,7 +124,6 @@ struct WfBufs {
     uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
     uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
-    int32_t lds_nodes;              // BVH nodes (breadth-first prefix) staged in LDS by the BVH kernels
 };
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels

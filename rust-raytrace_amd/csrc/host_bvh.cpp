@@ -51,7 +51,6 @@ struct Prim {
     int32_t idx;
 };
 
-constexpr int kLeafMax = 4;
 constexpr int kBins = 16;
 constexpr int kSahDepth = 40;
 
@@ -59,6 +58,7 @@ struct Builder {
     std::vector<Prim>& prims;
     std::vector<BvhNodeHost>& nodes;
     double pad;
+    int leaf_max;
 
     Box bounds(int b, int e) const {
         Box r;
@@ -69,7 +69,7 @@ struct Builder {
     // Returns the encoded child pointer for prims[b, e).
     int32_t build(int b, int e, int depth) {
         const int n = e - b;
-        if (n <= kLeafMax) return ~((b << 3) | (n - 1));
+        if (n <= leaf_max) return ~((b << 3) | (n - 1));
         Box cb;                         // centroid bounds
         for (int i = b; i < e; ++i)
             for (int a = 0; a < 3; ++a) { cb.lo[a] = std::min(cb.lo[a], prims[i].c[a]); cb.hi[a] = std::max(cb.hi[a], prims[i].c[a]); }
@@ -145,7 +145,7 @@ struct Builder {
 }  // namespace
 
 BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<double>& cy, const std::vector<double>& cz,
-                           const std::vector<double>& radius, double pad) {
+                           const std::vector<double>& radius, double pad, int leaf_max) {
     BvhResult res;
     const size_t n = cx.size();
     if (n == 0) { res.root = 0; return res; }
@@ -163,8 +163,9 @@ BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<doub
         }
         p.idx = static_cast<int32_t>(i);
     }
-    res.nodes.reserve(2 * n / kLeafMax + 2);
-    Builder bld{prims, res.nodes, pad};
+    leaf_max = std::min(8, std::max(1, leaf_max));
+    res.nodes.reserve(2 * n / leaf_max + 2);
+    Builder bld{prims, res.nodes, pad, leaf_max};
     res.root = bld.build(0, static_cast<int>(n), 0);
     // Renumber breadth-first so the top levels are a prefix of the array: the
     // traversal kernels keep the first nodes that fit in LDS.
@@ -190,6 +191,74 @@ BvhResult build_sphere_bvh(const std::vector<double>& cx, const std::vector<doub
     res.order.resize(n);
     for (size_t i = 0; i < n; ++i) res.order[i] = prims[i].idx;
     return res;
+}
+
+// Collapse: each 4-wide node takes the two children of a binary node and
+// repeatedly opens the inner child with the largest box area until it has 4
+// children or only leaves.  Child boxes are the binary tree's f32 boxes
+// unchanged (so the culling stays conservative), numbered breadth-first.
+Bvh4Result collapse_bvh4(const BvhResult& b2) {
+    Bvh4Result out;
+    out.root = b2.root;
+    if (b2.nodes.empty() || b2.root < 0) return out;
+    struct Ref {
+        int32_t ptr;
+        float lo[3], hi[3];
+    };
+    auto area = [](const Ref& r) {
+        const double dx = r.hi[0] - r.lo[0], dy = r.hi[1] - r.lo[1], dz = r.hi[2] - r.lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    auto children = [&](int32_t node, Ref& a, Ref& b) {
+        const BvhNodeHost& nd = b2.nodes[node];
+        a.ptr = nd.c0; b.ptr = nd.c1;
+        for (int k = 0; k < 3; ++k) { a.lo[k] = nd.lo0[k]; a.hi[k] = nd.hi0[k]; b.lo[k] = nd.lo1[k]; b.hi[k] = nd.hi1[k]; }
+    };
+    struct Node4 {
+        Ref c[4];
+        int n;
+    };
+    std::vector<Node4> nodes;
+    std::vector<int32_t> queue{b2.root};       // binary node of each 4-wide node, breadth-first
+    for (size_t h = 0; h < queue.size(); ++h) {
+        Node4 nd{};
+        children(queue[h], nd.c[0], nd.c[1]);
+        nd.n = 2;
+        while (nd.n < 4) {
+            int best = -1;
+            double best_area = -1.0;
+            for (int k = 0; k < nd.n; ++k)
+                if (nd.c[k].ptr >= 0 && area(nd.c[k]) > best_area) { best = k; best_area = area(nd.c[k]); }
+            if (best < 0) break;
+            Ref a, b;
+            children(nd.c[best].ptr, a, b);
+            nd.c[best] = a;
+            nd.c[nd.n++] = b;
+        }
+        for (int k = 0; k < nd.n; ++k)
+            if (nd.c[k].ptr >= 0) {
+                const int32_t binary = nd.c[k].ptr;
+                nd.c[k].ptr = static_cast<int32_t>(queue.size());   // its 4-wide index
+                queue.push_back(binary);
+            }
+        nodes.push_back(nd);
+    }
+    const int32_t N = static_cast<int32_t>(nodes.size());
+    out.n_nodes = N;
+    out.root = 0;
+    out.planes.assign(static_cast<size_t>(kBvh4Planes) * N, DevBvh4Plane{});
+    for (int32_t i = 0; i < N; ++i) {
+        const Node4& nd = nodes[i];
+        for (int k = 0; k < 4; ++k) {
+            const bool used = k < nd.n;
+            for (int a = 0; a < 3; ++a) {
+                out.planes[static_cast<size_t>(2 * a) * N + i].f[k] = used ? nd.c[k].lo[a] : 0.0f;
+                out.planes[static_cast<size_t>(2 * a + 1) * N + i].f[k] = used ? nd.c[k].hi[a] : 0.0f;
+            }
+            out.planes[static_cast<size_t>(6) * N + i].i[k] = used ? nd.c[k].ptr : kBvh4Empty;
+        }
+    }
+    return out;
 }
 
 }  // namespace rtamd

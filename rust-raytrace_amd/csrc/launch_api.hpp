@@ -1,0 +1,64 @@
+// Host-side launchers of the kernels in trace_kernel.hip (called by rt_device.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "device_layout.hpp"
+
+namespace rtamd {
+
+// Kernel families of the wavefront schedule (rt_ctx_kernel_times indices).
+enum KernelFamily : int8_t { kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCount = 5 };
+
+// Per-launch timing (RT_TIME_KERNELS): begin() records a start event, mark()
+// an end event after each launch, noting (start, end, family); elapsed time
+// between the two = that launch's duration on an in-order stream.  Events
+// come from a pool owned by the context; intervals accumulate over renders
+// until harvested (rt_ctx_kernel_times).
+struct LaunchInterval {
+    int start, end;
+    KernelFamily fam;
+};
+
+struct LaunchMarks {
+    std::vector<hipEvent_t>* pool = nullptr;
+    int* used = nullptr;                   // events of the pool in use
+    std::vector<LaunchInterval>* out = nullptr;
+    int prev = -1;
+    static constexpr int kMaxEvents = 1 << 16;
+
+    hipError_t record(hipStream_t s, int& idx) {
+        idx = -1;
+        if (*used >= kMaxEvents) return hipSuccess;    // not harvested: stop recording
+        if (*used == static_cast<int>(pool->size())) {
+            hipEvent_t e;
+            const hipError_t err = hipEventCreate(&e);
+            if (err != hipSuccess) return err;
+            pool->push_back(e);
+        }
+        idx = (*used)++;
+        return hipEventRecord((*pool)[idx], s);
+    }
+    hipError_t begin(hipStream_t s) { return record(s, prev); }
+    hipError_t mark(hipStream_t s, KernelFamily f) {
+        int idx;
+        const hipError_t e = record(s, idx);
+        if (e == hipSuccess && idx >= 0 && prev >= 0) out->push_back(LaunchInterval{prev, idx, f});
+        prev = idx;
+        return e;
+    }
+};
+
+hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
+// Sphere sources (trace_kernel.hip, kSrc*): 0 brute force from HBM/L2, 1 brute
+// force staged in LDS, 2 binary BVH from HBM/L2, 4 binary BVH + spheres in
+// LDS, 7 = 4 held to 64 VGPRs, 10 4-wide BVH + spheres in LDS (64 VGPRs),
+// 11 4-wide BVH from HBM/L2, 12 = 10 with 128 VGPRs.  Supported (nearest,
+// occlusion) pairs: (s, s) for every s, (7, 10), (2, 11).
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
+                            bool count, hipStream_t s, hipEvent_t mark, int mark_gen, LaunchMarks* marks);
+hipError_t upload_srgb_table(const double* avg255);
+
+}  // namespace rtamd

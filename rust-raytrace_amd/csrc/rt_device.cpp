@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
@@ -14,13 +15,7 @@
 #include "bvh_build.hpp"
 #include "device_layout.hpp"
 #include "host_scene.hpp"
-
-namespace rtamd {
-hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
-                            hipStream_t s, hipEvent_t mark, int mark_gen);
-hipError_t upload_srgb_table(const double* avg255);
-}  // namespace rtamd
+#include "launch_api.hpp"
 
 using namespace rtamd;
 
@@ -53,6 +48,10 @@ struct rt_ctx {
         WfBufs b{};
     };
     std::vector<Lane> lanes;
+    // RT_TIME_KERNELS: launch intervals accumulated since the last harvest
+    std::vector<hipEvent_t> tev;
+    int t_used = 0;
+    std::vector<LaunchInterval> tint;
     hipEvent_t fork = nullptr;
     bool wf_used = false;
     std::string err;
@@ -84,6 +83,8 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 constexpr int kTotals = 2 * kCounterShards;
 constexpr int kGenTotals = kTotals + 8;
 constexpr int kCounterWords = kGenTotals + kCntWords;
+// LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
+constexpr size_t kLdsBudget = 72 * 1024;
 
 int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
@@ -205,6 +206,7 @@ void rt_ctx_destroy(rt_ctx* c) {
         if (L.done) (void)hipEventDestroy(L.done);
         if (L.s) (void)hipStreamDestroy(L.s);
     }
+    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -272,7 +274,14 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
         for (double v : {sx[k] - r, sx[k] + r, sy[k] - r, sy[k] + r, sz[k] - r, sz[k] + r})
             if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
     }
-    BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, 1e-5 * (1.0 + extent));
+    // Leaves of 2 spheres measured fastest at C3; 4 when that tree and the
+    // spheres would not fit the traversal kernels' LDS budget (RT_BVH_LEAF overrides).
+    const double pad = 1e-5 * (1.0 + extent);
+    const int leaf_env = env_int("RT_BVH_LEAF", 0);
+    BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf_env > 0 ? leaf_env : 2);
+    if (leaf_env <= 0 && bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
+        bvh = build_sphere_bvh(sx, sy, sz, srad, pad, 4);
+    const Bvh4Result bvh4 = collapse_bvh4(bvh);
     {
         std::vector<DevSphere> s2(spheres.size());
         std::vector<int32_t> o2(spheres.size());
@@ -290,6 +299,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_mat = place(mats.size() * sizeof(DevMaterial));
     const size_t o_li = place(lights.size() * sizeof(DevLight));
     const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
+    const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
     const size_t total = off ? off : 256;
     std::vector<uint8_t> host(total, 0);
     auto put = [&](size_t at, const void* p, size_t bytes) { if (bytes) std::memcpy(host.data() + at, p, bytes); };
@@ -300,6 +310,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_mat, mats.data(), mats.size() * sizeof(DevMaterial));
     put(o_li, lights.data(), lights.size() * sizeof(DevLight));
     put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
+    put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
     if (!c->d_blob) {
@@ -322,6 +333,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.n_planes = static_cast<int32_t>(planes.size());
     d.n_lights = static_cast<int32_t>(lights.size());
     d.n_bvh = static_cast<int32_t>(bvh.nodes.size());
+    d.bvh4 = reinterpret_cast<const DevBvh4Plane*>(base + o_bvh4);
+    d.bvh4_root = bvh4.root;
+    d.n_bvh4 = bvh4.n_nodes;
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
     for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
     d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;
@@ -388,25 +402,33 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     if (mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) {
         // LDS per traversal workgroup (1024 threads, two resident per CU): the
         // whole BVH + sphere list when they fit, else the top of the tree.
-        constexpr size_t kLdsBudget = 72 * 1024;
         const size_t node_bytes = static_cast<size_t>(c->dsc.n_bvh) * sizeof(DevBvhNode);
         const size_t sph_bytes = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
-        int src;
-        int32_t lds_nodes = 0;
-        // sources: 2 BVH/L2 + scratch stack, 3 BVH/L2 + register stack, 4 BVH+spheres in LDS +
-        // scratch stack, 5 the same + register stack, 6 top of BVH in LDS + register stack,
-        // 7 = 4 held to 64 VGPRs (two workgroups per CU), 8 / 9 = 7 with 1 / 2 stack entries in registers
-        const char* force = std::getenv("RT_WF_SRC");          // experiment override
+        const size_t node4_bytes = static_cast<size_t>(c->dsc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane);
+        // (nearest, occlusion) sphere sources, see launch_api.hpp.  Default: the
+        // binary tree for the nearest-hit query and the 4-wide tree for the
+        // shadow query, each staged whole in LDS with the spheres when it fits
+        // (measured best at C3); RT_WF_SRC = "n" or "n,o" overrides.
+        int src, src_occ;
         if (mode == RT_ALGO_WAVEFRONT) {
-            const bool all_fit = node_bytes + sph_bytes <= kLdsBudget;
-            src = force ? std::atoi(force) : (all_fit ? 7 : 2);
-            const bool needs_all = src == 4 || src == 5 || src >= 7;
-            if (src < 2 || src > 9 || (needs_all && !all_fit)) src = 2;
-            if (src == 4 || src == 5 || src >= 7) lds_nodes = c->dsc.n_bvh;
-            else if (src == 6)
-                lds_nodes = static_cast<int32_t>(std::min<size_t>(c->dsc.n_bvh, 32 * 1024 / sizeof(DevBvhNode)));
+            const bool fit2 = node_bytes + sph_bytes <= kLdsBudget;
+            const bool fit4 = node4_bytes + sph_bytes <= kLdsBudget;
+            src = fit2 ? 7 : 2;
+            src_occ = fit4 ? 10 : 11;
+            if (!fit2 || !fit4) { src = 2; src_occ = 11; }
+            if (const char* force = std::getenv("RT_WF_SRC")) {
+                int n = -1, oc = -1;
+                const int got = std::sscanf(force, "%d,%d", &n, &oc);
+                if (got >= 1) { src = n; src_occ = got == 2 ? oc : n; }
+            }
+            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 10 || v == 11 || v == 12; };
+            const bool pair_ok = ok(src) && ok(src_occ) &&
+                                 (src == src_occ || (src == 7 && src_occ == 10) || (src == 2 && src_occ == 11));
+            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
+                              !(src_occ == 10 && !fit4);
+            if (!pair_ok || !fits) { src = 2; src_occ = 11; }
         } else {
-            src = fits_lds ? 1 : 0;
+            src = src_occ = fits_lds ? 1 : 0;
         }
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
@@ -430,12 +452,18 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1);
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
-            c->lanes[l].b.lds_nodes = lds_nodes;
         }
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
+        // per-launch timing needs one in-order stream
+        const bool timed = (o->flags & RT_TIME_KERNELS) != 0 && n_lanes == 1;
+        LaunchMarks marks;
+        marks.pool = &c->tev;
+        marks.used = &c->t_used;
+        marks.out = &c->tint;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, hipEventRecord(c->fork, st));
         for (int l = 0; l < n_lanes; ++l) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
+        if (timed) HIP_TRY(c, marks.begin(c->lanes[0].s));
         for (uint32_t ci = 0; ci < n_chunks; ++ci) {
             rt_ctx::Lane& L = c->lanes[ci % n_lanes];
             if (ci > 0 && n_lanes > 1) HIP_TRY(c, hipStreamWaitEvent(L.s, c->lanes[(ci - 1) % n_lanes].mark, 0));
@@ -444,7 +472,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             f.rows = std::min(chunk_rows, o->tile_h - f.row0);
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, count, L.s, L.mark, mark_gen));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, L.s, L.mark, mark_gen, timed ? &marks : nullptr));
         }
         for (int l = 0; l < n_lanes; ++l) {
             HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));
@@ -498,6 +526,21 @@ int rt_ctx_generation_counts(rt_ctx* c, uint32_t* queue, uint32_t* shaded, int n
         queue[k] = static_cast<uint32_t>(h[kCntQ + k]);
         shaded[k] = static_cast<uint32_t>(h[kCntS + k]);
     }
+    return RT_OK;
+}
+
+int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
+    if (!c || n < 0 || (n && (!ms || !launches))) return RT_E_INVALID;
+    for (int i = 0; i < n; ++i) { ms[i] = 0.0; launches[i] = 0; }
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->t_used > 0) HIP_TRY(c, hipEventSynchronize(c->tev[c->t_used - 1]));
+    for (const LaunchInterval& iv : c->tint) {
+        float e = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&e, c->tev[iv.start], c->tev[iv.end]));
+        if (iv.fam < n) { ms[iv.fam] += e; ++launches[iv.fam]; }
+    }
+    c->tint.clear();
+    c->t_used = 0;
     return RT_OK;
 }
 

@@ -236,6 +236,8 @@ struct BvhView {
     const DevBvhNode* gnodes;
     const DevSphere* sph;
     const int32_t* obj;
+    const DevBvh4Plane* p4;      // 4-wide tree planes (LDS or HBM), stride n4
+    int32_t n4;
 };
 
 // kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS
@@ -379,6 +381,156 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
             }
             if (h0) { cur = nd.c0; continue; }
             if (h1) { cur = nd.c1; continue; }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += cnt;
+            for (int k = first; k < first + cnt; ++k) {
+                double t;
+                if (sphere_t(v.sph[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+            }
+        }
+        if (stk_n == 0) return false;
+        cur = stk_pop();
+    }
+}
+
+// ---- 4-wide BVH --------------------------------------------------------
+// One node visit tests the 4 child boxes (same conservative slab test).  The
+// nearest query continues with the nearest hit child and pushes the others
+// far-to-near with their entry t; the shadow query takes them in slot order.
+// Misses are marked by the child pointer (kBvh4Empty), never by t, so a box
+// hit at t = +inf is still visited.
+struct Node4Hits {
+    float t[4];
+    int32_t c[4];
+};
+
+__device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, const RayBox& rb, float tlim) {
+    // axis by axis (as box_hit, same operations), so only two planes are live at a time
+    const int32_t N = v.n4;
+    const DevBvh4Plane* P = v.p4 + node;
+    float tn[4], tf[4];
+    {
+        const DevBvh4Plane lo = P[0], hi = P[N];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float a = (lo.f[k] - rb.ox) * rb.ix, b = (hi.f[k] - rb.ox) * rb.ix;
+            tn[k] = fminf(a, b);
+            tf[k] = fmaxf(a, b);
+        }
+    }
+    {
+        const DevBvh4Plane lo = P[2 * N], hi = P[3 * N];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float a = (lo.f[k] - rb.oy) * rb.iy, b = (hi.f[k] - rb.oy) * rb.iy;
+            tn[k] = fmaxf(tn[k], fminf(a, b));
+            tf[k] = fminf(tf[k], fmaxf(a, b));
+        }
+    }
+    {
+        const DevBvh4Plane lo = P[4 * N], hi = P[5 * N];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float a = (lo.f[k] - rb.oz) * rb.iz, b = (hi.f[k] - rb.oz) * rb.iz;
+            tn[k] = fmaxf(tn[k], fminf(a, b));
+            tf[k] = fminf(tf[k], fmaxf(a, b));
+        }
+    }
+    const DevBvh4Plane ch = P[6 * N];
+    Node4Hits o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float n = tn[k] - kBoxTol * fabsf(tn[k]);
+        const float f = tf[k] + kBoxTol * fabsf(tf[k]);
+        const bool hit = n <= f && f >= 0.0f && n <= tlim && ch.i[k] != kBvh4Empty;
+        o.t[k] = hit ? n : __builtin_inff();
+        o.c[k] = hit ? ch.i[k] : kBvh4Empty;
+    }
+    return o;
+}
+
+__device__ __forceinline__ void cas4(Node4Hits& h, int i, int j) {
+    const bool sw = h.t[j] < h.t[i];
+    const float ti = h.t[i], tj = h.t[j];
+    const int32_t ci = h.c[i], cj = h.c[j];
+    h.t[i] = sw ? tj : ti; h.t[j] = sw ? ti : tj;
+    h.c[i] = sw ? cj : ci; h.c[j] = sw ? ci : cj;
+}
+
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    RT_STACK_DECL(0, uint64_t);
+    int32_t cur = sc.bvh4_root;
+    for (;;) {
+        if (cur >= 0) {
+            Node4Hits n = node4_test(v, cur, rb, tlim);
+            if constexpr (kCount) w->boxes += 4;
+            cas4(n, 0, 1); cas4(n, 2, 3); cas4(n, 0, 2); cas4(n, 1, 3); cas4(n, 1, 2);
+#pragma unroll
+            for (int k = 3; k >= 1; --k)
+                if (n.c[k] != kBvh4Empty) stk_push(stk_entry(n.c[k], n.t[k]));
+            if (n.c[0] != kBvh4Empty) { cur = n.c[0]; continue; }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += cnt;
+            for (int k = first; k < first + cnt; ++k) {
+                double t;
+                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                    const int32_t obj = v.obj[k];
+                    if (t < h.t || (t == h.t && obj < h.obj)) {
+                        h.t = t; h.obj = obj; h.prim = k;
+                        tlim = t_limit(t);
+                    }
+                }
+            }
+        }
+        for (;;) {                  // pop, skipping entries the current best rules out
+            if (stk_n == 0) return h;
+            const uint64_t e = stk_pop();
+            cur = stk_node(e);
+            if (stk_t(e) <= tlim) break;
+        }
+    }
+}
+
+template <bool kCount = false>
+__device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
+                                              double r2, Work* w = nullptr) {
+    bool plane_block = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        if (!has_range) return true;
+        if (t != t) return false;
+        plane_block |= t * t < r2;
+    }
+    if (plane_block) return true;
+    if (sc.n_spheres == 0) return false;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
+    RT_STACK_DECL(0, int32_t);
+    int32_t cur = sc.bvh4_root;
+    for (;;) {
+        if (cur >= 0) {
+            const Node4Hits n = node4_test(v, cur, rb, tlim);
+            if constexpr (kCount) w->boxes += 4;
+            int32_t next = kBvh4Empty;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (n.c[k] != kBvh4Empty) {
+                    if (next != kBvh4Empty) stk_push(next);
+                    next = n.c[k];
+                }
+            if (next != kBvh4Empty) { cur = next; continue; }
         } else {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
             if constexpr (kCount) w->spheres += cnt;

@@ -27,6 +27,7 @@
 #include <cstdint>
 
 #include "device_layout.hpp"
+#include "launch_api.hpp"
 #include "trace_common.hpp"
 
 namespace rtamd {
@@ -207,73 +208,82 @@ __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
 // Sphere sources of the wavefront intersection kernels.
 constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
-constexpr int kSrcBvhG = 2;         // BVH from HBM/L2, scratch stack
-constexpr int kSrcBvhGS = 3;        // BVH from HBM/L2, register short stack
-constexpr int kSrcBvhL = 4;         // BVH + spheres in LDS, scratch stack
-constexpr int kSrcBvhLS = 5;        // BVH + spheres in LDS, register short stack
-constexpr int kSrcBvhP = 6;         // top of the BVH in LDS, spheres from HBM/L2, register short stack
+constexpr int kSrcBvhG = 2;         // binary BVH from HBM/L2
+constexpr int kSrcBvhL = 4;         // binary BVH + spheres in LDS
 constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
-constexpr int kSrcBvhL8R1 = 8;      // kSrcBvhL8 with the top stack entry in registers
-constexpr int kSrcBvhL8R2 = 9;      // kSrcBvhL8 with the top two stack entries in registers
+constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
+constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
+constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
 
 template <int kSrc>
 struct Src {
     static constexpr bool bvh = kSrc >= kSrcBvhG;
-    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhLS || kSrc >= kSrcBvhL8;
+    static constexpr bool wide = kSrc >= kSrcBvh4L;
+    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds;
-    static constexpr int nodes = all_lds ? 2 : (kSrc == kSrcBvhP ? 1 : 0);
-    // traversal stack entries held in registers
-    static constexpr int reg = (kSrc == kSrcBvhGS || kSrc == kSrcBvhLS || kSrc == kSrcBvhP) ? 8
-                             : kSrc == kSrcBvhL8R1 ? 1 : kSrc == kSrcBvhL8R2 ? 2 : 0;
-    static constexpr int waves = kSrc >= kSrcBvhL8 ? 8 : 4;      // min waves per SIMD (__launch_bounds__)
+    static constexpr int nodes = all_lds ? 2 : 0;
+    static constexpr int waves = kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 ? 8 : 4;   // min waves per SIMD
 };
 
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
-__host__ __device__ inline size_t staged_bytes(int n_spheres, int lds_nodes) {
+__host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
-    if (kSrc == kSrcLds) bytes = static_cast<size_t>(n_spheres) * sizeof(DevSphere);
-    if (Src<kSrc>::nodes > 0) bytes = static_cast<size_t>(lds_nodes) * sizeof(DevBvhNode);
-    if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
+    if (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if (Src<kSrc>::nodes > 0)
+        bytes = Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
+                                : static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
+    if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     return (bytes + 15) / 16 * 16;
 }
 
-// Stage what the source keeps in LDS; returns the view the queries use.
+// Stage what the source keeps in LDS (the whole tree and the spheres); returns
+// the view the queries use.
 template <int kSrc>
-__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, const WfBufs& b, unsigned char* lds) {
+__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj};
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4};
+    size_t off = 0;
     if constexpr (kSrc == kSrcLds) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
+        return v;
+    } else if constexpr (Src<kSrc>::nodes > 0 && Src<kSrc>::wide) {
+        DevBvh4Plane* lp = reinterpret_cast<DevBvh4Plane*>(lds);
+        const int n = kBvh4Planes * sc.n_bvh4;
+        for (int i = threadIdx.x; i < n; i += T) lp[i] = sc.bvh4[i];
+        v.p4 = lp;
+        off = static_cast<size_t>(n) * sizeof(DevBvh4Plane);
     } else if constexpr (Src<kSrc>::nodes > 0) {
         DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
-        for (int i = threadIdx.x; i < b.lds_nodes; i += T) ln[i] = sc.bvh[i];
+        for (int i = threadIdx.x; i < sc.n_bvh; i += T) ln[i] = sc.bvh[i];
         v.lnodes = ln;
-        v.nl = b.lds_nodes;
-        if constexpr (Src<kSrc>::sph_lds) {
-            DevSphere* ls = reinterpret_cast<DevSphere*>(lds + static_cast<size_t>(b.lds_nodes) * sizeof(DevBvhNode));
-            int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
-            for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
-            v.sph = ls;
-            v.obj = lo;
-        }
+        v.nl = sc.n_bvh;
+        off = static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
+    }
+    if constexpr (Src<kSrc>::bvh && Src<kSrc>::sph_lds) {
+        DevSphere* ls = reinterpret_cast<DevSphere*>(lds + off);
+        int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
+        for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
+        v.sph = ls;
+        v.obj = lo;
     }
     return v;
 }
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
-    if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::reg>(sc, v, r, w);
+    if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, Work* w) {
-    if constexpr (Src<kSrc>::bvh)
-        return occluded_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::reg>(sc, v, r, has_range, r2, w);
+    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount>(sc, v, r, has_range, r2, w);
+    else if constexpr (Src<kSrc>::bvh) return occluded_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, has_range, r2, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
@@ -320,8 +330,8 @@ __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + 
 template <int kSrc, bool kCam, bool kCount>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const BvhView v = stage_lds<kSrc>(sc, b, lds);
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes), b.G);
+    const BvhView v = stage_lds<kSrc>(sc, lds);
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
     if (threadIdx.x == 0) *ql.count = 0;
     uint32_t n;
     if constexpr (kCam) {
@@ -398,8 +408,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
 template <int kSrc, bool kCount>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const BvhView v = stage_lds<kSrc>(sc, b, lds);
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes), b.G);
+    const BvhView v = stage_lds<kSrc>(sc, lds);
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
     region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
     const uint32_t n = ql.scan[b.G] * L;
@@ -613,39 +623,54 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
     return hipGetLastError();
 }
 
-template <int kSrc, bool kCount>
-void launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s) {
-    const size_t lds = staged_bytes<kSrc>(sc.n_spheres, b.lds_nodes) + queue_lds_bytes(b.G);
+template <int kSrcN, int kSrcO, bool kCount>
+hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s,
+                             LaunchMarks* m) {
     const dim3 grid(b.G), block(kWfThreads);
-    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrc, true, kCount>), grid, block, lds, s, sc, fp, b, k);
-    else hipLaunchKernelGGL((wf_nearest<kSrc, false, kCount>), grid, block, lds, s, sc, fp, b, k);
-    if (sc.n_lights > 0) hipLaunchKernelGGL((wf_occlusion<kSrc, kCount>), grid, block, lds, s, sc, fp, b, k);
+    const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
+    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrcN, true, kCount>), grid, block, lds_n, s, sc, fp, b, k);
+    else hipLaunchKernelGGL((wf_nearest<kSrcN, false, kCount>), grid, block, lds_n, s, sc, fp, b, k);
+    hipError_t e = m ? m->mark(s, kKfNearest) : hipSuccess;
+    if (e != hipSuccess) return e;
+    if (sc.n_lights > 0) {
+        const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
+        hipLaunchKernelGGL((wf_occlusion<kSrcO, kCount>), grid, block, lds_o, s, sc, fp, b, k);
+        e = m ? m->mark(s, kKfOcclusion) : hipSuccess;
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(wf_shade, grid, block, 0, s, sc, fp, b, k);
+    return m ? m->mark(s, kKfShade) : hipSuccess;
 }
 
 // One chunk (fp.row0, fp.rows) through every generation.  src: the sphere
-// source (kSrc*); count: instrumented kernels; mark is recorded on s after
-// generation mark_gen has been launched (chunk pipelining across streams).
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, bool count,
-                            hipStream_t s, hipEvent_t mark, int mark_gen) {
+// source of the nearest-hit kernel (kSrc*), src_occ: of the shadow kernel;
+// count: instrumented kernels; mark is recorded on s after generation
+// mark_gen has been launched (chunk pipelining across streams); marks (may
+// be null): per-launch timing events, started by the caller.
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
+                            bool count, hipStream_t s, hipEvent_t mark, int mark_gen, LaunchMarks* marks) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
-#define RT_GEN(S) (count ? launch_generation<S, true>(sc, fp, b, k, s) : launch_generation<S, false>(sc, fp, b, k, s))
-        switch (src) {
-        case kSrcGlobal: RT_GEN(kSrcGlobal); break;
-        case kSrcLds: RT_GEN(kSrcLds); break;
-        case kSrcBvhG: RT_GEN(kSrcBvhG); break;
-        case kSrcBvhGS: RT_GEN(kSrcBvhGS); break;
-        case kSrcBvhL: RT_GEN(kSrcBvhL); break;
-        case kSrcBvhLS: RT_GEN(kSrcBvhLS); break;
-        case kSrcBvhP: RT_GEN(kSrcBvhP); break;
-        case kSrcBvhL8: RT_GEN(kSrcBvhL8); break;
-        case kSrcBvhL8R1: RT_GEN(kSrcBvhL8R1); break;
-        default: RT_GEN(kSrcBvhL8R2); break;
+        hipError_t e;
+#define RT_GEN(N, O) e = (count ? launch_generation<N, O, true>(sc, fp, b, k, s, marks) \
+                                : launch_generation<N, O, false>(sc, fp, b, k, s, marks))
+        const int combo = src * 100 + src_occ;
+        switch (combo) {
+        case kSrcGlobal * 101: RT_GEN(kSrcGlobal, kSrcGlobal); break;
+        case kSrcLds * 101: RT_GEN(kSrcLds, kSrcLds); break;
+        case kSrcBvhG * 101: RT_GEN(kSrcBvhG, kSrcBvhG); break;
+        case kSrcBvhL * 101: RT_GEN(kSrcBvhL, kSrcBvhL); break;
+        case kSrcBvhL8 * 101: RT_GEN(kSrcBvhL8, kSrcBvhL8); break;
+        case kSrcBvh4L * 101: RT_GEN(kSrcBvh4L, kSrcBvh4L); break;
+        case kSrcBvh4L4 * 101: RT_GEN(kSrcBvh4L4, kSrcBvh4L4); break;
+        case kSrcBvhL8 * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8, kSrcBvh4L); break;
+        case kSrcBvhG * 100 + kSrcBvh4G: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
+        default: RT_GEN(kSrcBvh4G, kSrcBvh4G); break;
         }
 #undef RT_GEN
+        if (e != hipSuccess) return e;
         if (mark && k == mark_gen) {
-            const hipError_t e = hipEventRecord(mark, s);
+            e = hipEventRecord(mark, s);
             if (e != hipSuccess) return e;
         }
     }
@@ -654,7 +679,11 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
     if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
     else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    hipError_t e = marks ? marks->mark(s, kKfFold) : hipSuccess;
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);
+    e = marks ? marks->mark(s, kKfTally) : hipSuccess;
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -27,7 +27,8 @@ RT_MAT_PHONG, RT_MAT_INDIRECT_PHONG, RT_MAT_FRESNEL, RT_MAT_TRANSPARENT = 0, 1, 
 RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AREA = 0, 1, 2
 RT_CAMERA_SIMPLE, RT_CAMERA_DOF = 0, 1
 RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
-RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK = 1, 2, 4
+RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK, RT_TIME_KERNELS = 1, 2, 4, 8
+KERNEL_FAMILIES = ("nearest", "occlusion", "shade", "fold", "tally")
 RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL, RT_ALGO_WAVEFRONT, RT_ALGO_WAVEFRONT_BRUTE = 0, 1, 2, 3, 4
 RT_MAX_DEPTH_LIMIT = 30
 
@@ -105,6 +106,7 @@ def _load():
         "rt_render_device": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_void_p, C.c_void_p, C.c_void_p]),
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
         "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
+        "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -264,6 +266,15 @@ class Context:
         s = (C.c_uint32 * n)()
         _check(lib.rt_ctx_generation_counts(self._h, q, s, n), self._h)
         return list(q), list(s)
+
+    def kernel_times(self):
+        """{family: (summed ms, launches)} over the RT_TIME_KERNELS renders since
+        the previous call (then reset); synchronises with the last timed launch."""
+        n = len(KERNEL_FAMILIES)
+        ms = (C.c_double * n)()
+        cnt = (C.c_uint32 * n)()
+        _check(lib.rt_ctx_kernel_times(self._h, ms, cnt, n), self._h)
+        return {f: (ms[i], cnt[i]) for i, f in enumerate(KERNEL_FAMILIES)}
 
     def close(self):
         if self._h:

@@ -299,3 +299,24 @@ def test_work_counters(gpu_ctx):
     assert bvh.box_tests > 0
     q, s = gpu_ctx.generation_counts()
     assert sum(q[1:]) + 64 * 48 == nearest
+
+
+def test_kernel_times(gpu_ctx):
+    """RT_TIME_KERNELS: identical image; one interval per launch, accumulated
+    over renders until harvested."""
+    spec = scenes.config3(64, 48)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    base = dict(max_depth=8, spp=1, algo=lr.RT_ALGO_WAVEFRONT)
+    plain = gpu_ctx.render(lr.render_opts(64, 48, **base))
+    gpu_ctx.kernel_times()
+    timed = [gpu_ctx.render(lr.render_opts(64, 48, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS,
+                                           **base)) for _ in range(2)]
+    for t in timed:
+        assert np.array_equal(plain[1], t[1])
+    kt = gpu_ctx.kernel_times()
+    gens = 8 + 2
+    assert kt["nearest"][1] == 2 * gens and kt["shade"][1] == 2 * gens
+    assert kt["occlusion"][1] == 2 * gens            # config3 has lights
+    assert kt["fold"][1] == 2 and kt["tally"][1] == 2
+    assert all(ms > 0 for ms, n in kt.values())
+    assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested

@@ -1,0 +1,65 @@
+"""HBM bytes per render from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
+
+Each pass ran `bench.py --steps S --warmup W` (W + S uninstrumented renders,
+then one RT_COUNT_WORK render).  Frames are split at the generation-0
+wf_nearest launch; the last uninstrumented frame of each pass is used.
+MI355X_MICROARCH.md ("HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced read, so it is doubled.
+
+    python tools/pmc_traffic.py gpurun_out/pmc KEY [out.json]
+"""
+import collections
+import csv
+import glob
+import json
+import re
+import sys
+
+
+def frames(path, counter):
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    out, cur = [], None
+    for r in rows:
+        name = r["Kernel_Name"]
+        if re.search(r"wf_nearest<\d+, true, (true|false)>", name):
+            cur = {"instrumented": ", true, true>" in name, "kernels": collections.defaultdict(float)}
+            out.append(cur)
+        if cur is None or "wf_" not in name:
+            continue
+        fam = re.search(r"(wf_[a-z]+)", name).group(1)
+        cur["kernels"][fam] += float(r["Counter_Value"]) * 1024.0
+    return [f for f in out if not f["instrumented"]]
+
+
+def main():
+    root, key = sys.argv[1], sys.argv[2]
+    out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    per = {}
+    for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
+        for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+            fr = frames(f, counter)
+            if fr:
+                per[counter] = {k: v * scale for k, v in fr[-1]["kernels"].items()}
+                break
+    if len(per) != 2:
+        sys.exit("need one FETCH_SIZE and one WRITE_SIZE pass")
+    fams = sorted(set(per["FETCH_SIZE"]) | set(per["WRITE_SIZE"]))
+    kernels = {k: {"read_bytes": per["FETCH_SIZE"].get(k, 0.0), "write_bytes": per["WRITE_SIZE"].get(k, 0.0)}
+               for k in fams}
+    total = sum(v["read_bytes"] + v["write_bytes"] for v in kernels.values())
+    try:
+        doc = json.load(open(out_path))
+    except Exception:
+        doc = {}
+    doc[key] = {"hbm_bytes_per_launch": total, "launch": "one render (all wavefront launches of one frame)",
+                "per_kernel_family": kernels,
+                "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace only; "
+                          "KiB -> bytes; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section); "
+                          "last uninstrumented frame of each pass"}
+    json.dump(doc, open(out_path, "w"), indent=1)
+    print(json.dumps(doc[key], indent=1))
+
+
+if __name__ == "__main__":
+    main()

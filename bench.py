@@ -66,21 +66,19 @@ def cpu_baseline(spec, args):
     f64) on the host, on a deterministic row sample of the same frame."""
     from oracle import ref64
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    rows = 8
-    stride = max(1, spec.height // rows)
-    t0 = time.time()
-    r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads, want_rgb64=False)
-    dt = time.time() - t0
-    # scale the sample to ~cpu_seconds of work
-    want = max(rows, min(spec.height, int(rows * args.cpu_seconds / max(dt, 1e-3))))
-    if want > rows * 1.5:
-        rows = want
-        stride = max(1, spec.height // rows)
+    rows, stride = 8, max(1, spec.height // 8)
+    for _ in range(5):
+        # every stride-th row of the frame (a deterministic sample of the same workload),
+        # grown until the sample takes about cpu_seconds or covers the whole frame
         rows = spec.height // stride
         t0 = time.time()
         r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads,
                          want_rgb64=False)
         dt = time.time() - t0
+        if dt >= 0.6 * args.cpu_seconds or stride == 1:
+            break
+        want = rows * args.cpu_seconds / max(dt, 1e-3)
+        stride = max(1, min(stride - 1, int(spec.height / want)))
     return {"value": r["counts"]["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{rows} rows (every {stride}th) x {spec.width} px of the same frame; "
                       f"{r['counts']['rays']} rays in {dt:.2f} s; oracle/ref64.c, f64, {threads} threads"}

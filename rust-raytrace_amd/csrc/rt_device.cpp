@@ -441,11 +441,12 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
         const uint32_t cap = o->tile_w * chunk_rows;
-        // G regions = workgroups per queue launch: four per CU (two resident
-        // 1024-thread workgroups with the LDS-staged BVH, so two rounds),
-        // fewer for small chunks; R covers every slot.
+        // G regions = workgroups per queue launch: two per CU, i.e. every
+        // workgroup resident at once (1024 threads with the LDS-staged BVH),
+        // so the wave-chunk dealing spreads even a small tail queue over the
+        // whole chip in one round; fewer for small chunks; R covers every slot.
         const int g_env = env_int("RT_WF_REGIONS", 0);
-        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 4u * static_cast<uint32_t>(c->n_cu);
+        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
         G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
         const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
         for (int l = 0; l < n_lanes; ++l) {

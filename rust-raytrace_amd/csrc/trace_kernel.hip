@@ -150,6 +150,16 @@ __device__ __forceinline__ uint32_t lds_append(uint32_t* counter, bool want) {
     return want ? base + below : 0xFFFFFFFFu;
 }
 
+// Work dealing: a queue is consumed in 64-item chunks, chunk c by wave
+// c mod W (W = G * 16 waves), waves numbered workgroup-first, so a small tail
+// queue spreads over every workgroup (and CU) instead of filling the first
+// few; a workgroup still takes at most R items (16 chunks per round of W).
+// Loop condition and chunk are wave-uniform.
+#define RT_FOR_CHUNKS(b, n, j)                                                              \
+    for (uint32_t rt_c = (threadIdx.x >> 6) * (b).G + blockIdx.x, rt_w = (b).G * (kWfThreads / 64); \
+         static_cast<uint64_t>(rt_c) * 64u < static_cast<uint64_t>(n); rt_c += rt_w)        \
+        if (const uint32_t j = rt_c * 64u + (threadIdx.x & 63u); true)
+
 // Exclusive scan of the G region sizes `counts` into s_scan[0..G]
 // (s_scan[G] = queue size).  s_wave: 16 words.  Ends with a barrier.
 __device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan, uint32_t* s_wave) {
@@ -287,18 +297,27 @@ __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& 
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
-// One atomic per wave into totals[at], totals[at + 1] (instrumented builds only).
+// One global atomic per workgroup into totals[at], totals[at + 1]
+// (instrumented kernels only; every thread of the workgroup must call it).
 template <bool kCount>
 __device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
     if constexpr (kCount) {
+        __shared__ unsigned long long s_w[2];
+        if (threadIdx.x == 0) { s_w[0] = 0; s_w[1] = 0; }
+        __syncthreads();
         unsigned long long bx = w.boxes, sp = w.spheres;
         for (int off = 32; off > 0; off >>= 1) {
             bx += __shfl_xor(bx, off, 64);
             sp += __shfl_xor(sp, off, 64);
         }
         if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&b.totals[at], bx);
-            atomicAdd(&b.totals[at + 1], sp);
+            atomicAdd(&s_w[0], bx);
+            atomicAdd(&s_w[1], sp);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicAdd(&b.totals[at], s_w[0]);
+            atomicAdd(&b.totals[at + 1], s_w[1]);
         }
     }
 }
@@ -344,8 +363,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     Work w;
     const int q = k & 1;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
-    for (uint32_t base = blockIdx.x * kWfThreads; base < n; base += b.G * kWfThreads) {
-        const uint32_t j = base + threadIdx.x;
+    RT_FOR_CHUNKS(b, n, j) {
         bool shade = false;
         Ray r{};
         double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0;
@@ -414,7 +432,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
     const uint32_t n = ql.scan[b.G] * L;
     Work w;
-    for (uint32_t qi = blockIdx.x * kWfThreads + threadIdx.x; qi < n; qi += b.G * kWfThreads) {
+    RT_FOR_CHUNKS(b, n, qi) {
+        if (qi >= n) continue;
         const uint32_t j = qi / L, l = qi - j * L;
         const size_t at = region_entry(ql.scan, b.G, b.R, j);
         const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
@@ -438,8 +457,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     const uint32_t n = s_scan[b.G];
     const int qn = (k + 1) & 1;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
-    for (uint32_t base = blockIdx.x * kWfThreads; base < n; base += b.G * kWfThreads) {
-        const uint32_t j = base + threadIdx.x;
+    RT_FOR_CHUNKS(b, n, j) {
         bool refl = false;
         Ray rr{};
         double nsig = 0.0;

@@ -21,7 +21,11 @@ stop_if_fatal $? bench
 tail -1 gpurun_out/bench.log
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1
+      python3 bench.py ${BENCH_ARGS:-} --no-cpu > gpurun_out/prof.log 2>&1
   stop_if_fatal $? rocprof
   find gpurun_out/prof -name "*stats*" | head
+fi
+if [ "${PMC:-1}" = "1" ]; then
+  GROUPS_PMC="FETCH_SIZE;WRITE_SIZE" BENCH_ARGS="${BENCH_ARGS:-} --no-cpu" bash tools/gpu_pmc.sh
+  stop_if_fatal $? pmc
 fi

@@ -90,7 +90,11 @@ struct FrameParams {
     float* out_rgb;                 // tile_h * tile_w * 3, may be null
     uint8_t* out_bgr;               // tile_h * bgr_pitch, may be null
     unsigned long long* counters;   // [kCounterShards] rays, then [kCounterShards] shadow rays
+    float bg_rgb[3];                // output of a pixel whose camera ray misses: the background
+    uint8_t bg_bgr[3];              //   averaged over spp (main.rs:56), f32 and sRGB B,G,R (host-computed)
 };
+
+constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (camera ray missed)
 
 // Wavefront working set for one chunk of a tile (all in HBM; sized by the
 // host for `cap` pixels / `slots` generation-0 slots; 288 GB leaves room).

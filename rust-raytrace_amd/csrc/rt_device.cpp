@@ -385,6 +385,21 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     fp.out_rgb = (o->flags & RT_OUT_RGB_F32) ? static_cast<float*>(d_rgb) : nullptr;
     fp.out_bgr = (o->flags & RT_OUT_BGR_U8) ? static_cast<uint8_t*>(d_bgr) : nullptr;
     fp.counters = c->d_counters;
+    {
+        // The background pixel exactly as average_samples + to_srgb produce it on the
+        // device (same f64 operations): camera misses are written by wf_nearest directly.
+        double px[3];
+        for (int k = 0; k < 3; ++k) {
+            const double cam = (0.0 + c->dsc.bg[k]) / 1.0;        // raytrace.rs:270-276, one camera sample
+            double acc = 0.0;
+            for (uint32_t q = 0; q < spp; ++q) acc = acc + cam;    // main.rs:47-55
+            px[k] = acc / static_cast<double>(spp);
+            fp.bg_rgb[k] = static_cast<float>(px[k]);
+        }
+        fp.bg_bgr[0] = to_srgb(px[2]);                             // color.rs:628-632, B G R
+        fp.bg_bgr[1] = to_srgb(px[1]);
+        fp.bg_bgr[2] = to_srgb(px[0]);
+    }
     fp.row0 = 0;
     fp.rows = o->tile_h;
     const size_t lds_bytes = static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere);

@@ -172,8 +172,12 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
 constexpr float kBoxTol = 1e-5f;
 constexpr int kBvhStack = 64;      // host builder bounds the depth (median splits past depth 40)
 
+// f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
+// bound is one FMA, fma(lo, 1/d, -o/d).  The FMA's rounding terms are of the
+// same two kinds the tolerance argument covers: relative to t (rounding of
+// 1/d and of the result) and a spatial 2^-24 |o| from rounding o/d.
 struct RayBox {
-    float ox, oy, oz, ix, iy, iz;
+    float ix, iy, iz, nox, noy, noz;
 };
 
 __device__ __forceinline__ float inv_dir(double d) {
@@ -183,19 +187,27 @@ __device__ __forceinline__ float inv_dir(double d) {
 }
 
 __device__ __forceinline__ RayBox make_raybox(const Ray& r) {
-    return RayBox{static_cast<float>(r.ox), static_cast<float>(r.oy), static_cast<float>(r.oz),
-                  inv_dir(r.dx), inv_dir(r.dy), inv_dir(r.dz)};
+    const float ix = inv_dir(r.dx), iy = inv_dir(r.dy), iz = inv_dir(r.dz);
+    return RayBox{ix, iy, iz, -(static_cast<float>(r.ox) * ix), -(static_cast<float>(r.oy) * iy),
+                  -(static_cast<float>(r.oz) * iz)};
 }
+
+// Slab bound t at coordinate v along the axis with (1/d, -o/d) = (i, no).
+__device__ __forceinline__ float slab_t(float v, float i, float no) { return __builtin_fmaf(v, i, no); }
+
+// Interval widening by the relative kBoxTol (one FMA with an |x| modifier).
+__device__ __forceinline__ float widen_lo(float t) { return __builtin_fmaf(-kBoxTol, fabsf(t), t); }
+__device__ __forceinline__ float widen_hi(float t) { return __builtin_fmaf(kBoxTol, fabsf(t), t); }
 
 // Conservative slab test; tlim = largest t still of interest.
 __device__ __forceinline__ bool box_hit(const float* lo, const float* hi, const RayBox& rb, float tlim, float& tnear) {
-    const float ax = (lo[0] - rb.ox) * rb.ix, bx = (hi[0] - rb.ox) * rb.ix;
-    const float ay = (lo[1] - rb.oy) * rb.iy, by = (hi[1] - rb.oy) * rb.iy;
-    const float az = (lo[2] - rb.oz) * rb.iz, bz = (hi[2] - rb.oz) * rb.iz;
+    const float ax = slab_t(lo[0], rb.ix, rb.nox), bx = slab_t(hi[0], rb.ix, rb.nox);
+    const float ay = slab_t(lo[1], rb.iy, rb.noy), by = slab_t(hi[1], rb.iy, rb.noy);
+    const float az = slab_t(lo[2], rb.iz, rb.noz), bz = slab_t(hi[2], rb.iz, rb.noz);
     float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    tn = tn - kBoxTol * fabsf(tn);
-    tf = tf + kBoxTol * fabsf(tf);
+    tn = widen_lo(tn);
+    tf = widen_hi(tf);
     tnear = tn;
     return tn <= tf && tf >= 0.0f && tn <= tlim;
 }
@@ -414,7 +426,7 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
         const DevBvh4Plane lo = P[0], hi = P[N];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float a = (lo.f[k] - rb.ox) * rb.ix, b = (hi.f[k] - rb.ox) * rb.ix;
+            const float a = slab_t(lo.f[k], rb.ix, rb.nox), b = slab_t(hi.f[k], rb.ix, rb.nox);
             tn[k] = fminf(a, b);
             tf[k] = fmaxf(a, b);
         }
@@ -423,7 +435,7 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
         const DevBvh4Plane lo = P[2 * N], hi = P[3 * N];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float a = (lo.f[k] - rb.oy) * rb.iy, b = (hi.f[k] - rb.oy) * rb.iy;
+            const float a = slab_t(lo.f[k], rb.iy, rb.noy), b = slab_t(hi.f[k], rb.iy, rb.noy);
             tn[k] = fmaxf(tn[k], fminf(a, b));
             tf[k] = fminf(tf[k], fmaxf(a, b));
         }
@@ -432,7 +444,7 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
         const DevBvh4Plane lo = P[4 * N], hi = P[5 * N];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float a = (lo.f[k] - rb.oz) * rb.iz, b = (hi.f[k] - rb.oz) * rb.iz;
+            const float a = slab_t(lo.f[k], rb.iz, rb.noz), b = slab_t(hi.f[k], rb.iz, rb.noz);
             tn[k] = fmaxf(tn[k], fminf(a, b));
             tf[k] = fminf(tf[k], fmaxf(a, b));
         }
@@ -441,8 +453,8 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
     Node4Hits o;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float n = tn[k] - kBoxTol * fabsf(tn[k]);
-        const float f = tf[k] + kBoxTol * fabsf(tf[k]);
+        const float n = widen_lo(tn[k]);
+        const float f = widen_hi(tf[k]);
         const bool hit = n <= f && f >= 0.0f && n <= tlim && ch.i[k] != kBvh4Empty;
         o.t[k] = hit ? n : __builtin_inff();
         o.c[k] = hit ? ch.i[k] : kBvh4Empty;

@@ -322,6 +322,24 @@ __device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
     }
 }
 
+// A camera ray that misses everything: the pixel is the background averaged
+// over samples, precomputed on the host (FrameParams::bg_*); written here and
+// marked so wf_fold skips it.
+__device__ __forceinline__ void write_background_pixel(const FrameParams& fp, const WfBufs& b, uint32_t p) {
+    const uint32_t lx = p % fp.tile_w, row = fp.row0 + p / fp.tile_w;
+    if (fp.out_rgb) {
+        float* q = fp.out_rgb + (static_cast<size_t>(row) * fp.tile_w + lx) * 3;
+        q[0] = fp.bg_rgb[0]; q[1] = fp.bg_rgb[1]; q[2] = fp.bg_rgb[2];
+    }
+    if (fp.out_bgr) {
+        uint8_t* q = fp.out_bgr + static_cast<size_t>(row) * fp.bgr_pitch + 3u * lx;
+        q[0] = fp.bg_bgr[0]; q[1] = fp.bg_bgr[1]; q[2] = fp.bg_bgr[2];
+        if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
+            for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k) fp.out_bgr[static_cast<size_t>(row) * fp.bgr_pitch + k] = 0;
+    }
+    b.nlev[p] = kNlevDone;
+}
+
 __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
     b.term[0][p] = c.r; b.term[1][p] = c.g; b.term[2][p] = c.b;
     b.nlev[p] = static_cast<uint8_t>(k);
@@ -389,8 +407,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         }
         if (live) {
             h = nearest_any<kSrc, kCount>(sc, v, r, &w);
-            if (h.obj == INT32_MAX) {
-                set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);      // raytrace.rs:265, 228-232
+            if (h.obj == INT32_MAX) {                                           // raytrace.rs:265, 228-232
+                if constexpr (kCam) write_background_pixel(fp, b, p);          // no levels: final now
+                else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
             } else {
                 const DevMaterial& m = sc.mats[h.obj];
                 const bool lit = static_cast<uint32_t>(k) <= fp.max_depth &&   // raytrace.rs:33
@@ -515,9 +534,10 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 // recursion returns (acc = res_k + ks_k * acc); the loads of four levels are
 // issued together so a pixel costs about two memory round trips per four
 // levels instead of two per level.
-__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p) {
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
+    if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
-    for (int k = static_cast<int>(b.nlev[p]) - 1; k >= 0; k -= 4) {
+    for (int k = static_cast<int>(nlev) - 1; k >= 0; k -= 4) {
         double sr[4], sg[4], sb[4];
         int32_t ob[4];
 #pragma unroll
@@ -563,14 +583,18 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
     const uint32_t npix = fp.tile_w * fp.rows;
     const uint32_t base = blockIdx.x * kBlock;
     const uint32_t p = base + threadIdx.x;
+    const uint8_t nlev = p < npix ? b.nlev[p] : kNlevDone;
+    // pixels marked done were written by wf_nearest; a workgroup of them has nothing to do
+    if (__syncthreads_and(nlev == kNlevDone)) return;
     if constexpr (!kStaged) {
-        __syncthreads();
-        if (p < npix) {
-            const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);
+        if (p < npix && nlev != kNlevDone) {
+            const Col res = average_samples(fold_pixel(sc, b, p, nlev), fp.spp);
             write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
         }
     } else {
-        const Col res = average_samples(fold_pixel(sc, b, p), fp.spp);   // npix % 256 == 0 here
+        // the whole 256-pixel row segment is stored; done pixels re-derive the
+        // background (bit-identical to the host-computed value) without loads
+        const Col res = average_samples(fold_pixel(sc, b, p, nlev), fp.spp);   // npix % 256 == 0 here
         s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
         s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
         s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);

@@ -436,11 +436,11 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
                 const int got = std::sscanf(force, "%d,%d", &n, &oc);
                 if (got >= 1) { src = n; src_occ = got == 2 ? oc : n; }
             }
-            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 10 || v == 11 || v == 12; };
+            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || (v >= 10 && v <= 12); };
             const bool pair_ok = ok(src) && ok(src_occ) &&
                                  (src == src_occ || (src == 7 && src_occ == 10) || (src == 2 && src_occ == 11));
-            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
-                              !(src_occ == 10 && !fit4);
+            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src >= 12) && !fit4) &&
+                              !((src_occ == 10 || src_occ >= 12) && !fit4);
             if (!pair_ok || !fits) { src = 2; src_occ = 11; }
         } else {
             src = src_occ = fits_lds ? 1 : 0;
@@ -488,7 +488,8 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             f.rows = std::min(chunk_rows, o->tile_h - f.row0);
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, L.s, L.mark, mark_gen, timed ? &marks : nullptr));
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, L.s, L.mark, mark_gen,
+                                        timed ? &marks : nullptr));
         }
         for (int l = 0; l < n_lanes; ++l) {
             HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));

@@ -360,7 +360,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 // The shadow query (see occluded_brute for the any-hit equivalence).
 template <bool kCount = false, int kNodes = 0, int kReg = 0>
 __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
-                                             double r2, Work* w = nullptr) {
+                                             double r2, int32_t hint = -1, Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -373,6 +373,11 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     if (sc.n_spheres == 0) return false;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const double a2 = 2.0 * a, a4 = 4.0 * a;
+    if (hint >= 0) {                     // see occluded_bvh4
+        if constexpr (kCount) ++w->spheres;
+        double t;
+        if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+    }
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
@@ -470,6 +475,11 @@ __device__ __forceinline__ void cas4(Node4Hits& h, int i, int j) {
     h.c[i] = sw ? cj : ci; h.c[j] = sw ? ci : cj;
 }
 
+// 5-comparator sorting network on entry t (misses carry t = +inf).
+__device__ __forceinline__ void sort4(Node4Hits& n) {
+    cas4(n, 0, 1); cas4(n, 2, 3); cas4(n, 0, 2); cas4(n, 1, 3); cas4(n, 1, 2);
+}
+
 template <bool kCount = false>
 __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
@@ -484,7 +494,10 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
         if (cur >= 0) {
             Node4Hits n = node4_test(v, cur, rb, tlim);
             if constexpr (kCount) w->boxes += 4;
-            cas4(n, 0, 1); cas4(n, 2, 3); cas4(n, 0, 2); cas4(n, 1, 3); cas4(n, 1, 2);
+            // near-to-far: continue with the nearest hit child, push the others
+            // far-first so they pop in order (the order decides how soon the
+            // best hit starts culling)
+            sort4(n);
 #pragma unroll
             for (int k = 3; k >= 1; --k)
                 if (n.c[k] != kBvh4Empty) stk_push(stk_entry(n.c[k], n.t[k]));
@@ -512,9 +525,13 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
     }
 }
 
+// `hint`: a sphere (leaf-order index, or -1) tested before the traversal: the
+// sphere the shadow ray starts on, which occludes it whenever the light is
+// behind that surface.  Any-hit: testing one sphere early cannot change the
+// answer (and the planes, with the NaN rule, are decided before it).
 template <bool kCount = false>
 __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
-                                              double r2, Work* w = nullptr) {
+                                              double r2, int32_t hint, Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -527,12 +544,18 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
     if (sc.n_spheres == 0) return false;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const double a2 = 2.0 * a, a4 = 4.0 * a;
+    if (hint >= 0) {
+        if constexpr (kCount) ++w->spheres;
+        double t;
+        if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+    }
     const RayBox rb = make_raybox(r);
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
     RT_STACK_DECL(0, int32_t);
     int32_t cur = sc.bvh4_root;
     for (;;) {
         if (cur >= 0) {
+            // slot order (measured: near-to-far sorting costs more than it saves here)
             const Node4Hits n = node4_test(v, cur, rb, tlim);
             if constexpr (kCount) w->boxes += 4;
             int32_t next = kBvh4Empty;

@@ -291,9 +291,9 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
-                                             double r2, Work* w) {
-    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount>(sc, v, r, has_range, r2, w);
-    else if constexpr (Src<kSrc>::bvh) return occluded_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, has_range, r2, w);
+                                             double r2, int32_t hint, Work* w) {
+    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount>(sc, v, r, has_range, r2, hint, w);
+    else if constexpr (Src<kSrc>::bvh) return occluded_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, has_range, r2, hint, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
 
@@ -449,17 +449,20 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
     region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-    const uint32_t n = ql.scan[b.G] * L;
+    const uint32_t nrec = ql.scan[b.G], n = nrec * L;
     Work w;
+    // light-major: a wave traces 64 consecutive records toward ONE light (coherent)
     RT_FOR_CHUNKS(b, n, qi) {
         if (qi >= n) continue;
-        const uint32_t j = qi / L, l = qi - j * L;
+        const uint32_t l = qi / nrec, j = qi - l * nrec;
         const size_t at = region_entry(ql.scan, b.G, b.R, j);
         const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, &w)) atomicOr(&b.occ[at], 1u << l);
+        // the sphere the point lies on is tested first (it shadows every light behind its surface)
+        const int32_t hint = b.sr_prim[at];
+        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w)) atomicOr(&b.occ[at], 1u << l);
     }
     flush_work<kCount>(b, 4, w);
 }

@@ -21,13 +21,20 @@ struct DevPlane {
 };
 
 // Per OBJECT (indexed by file-order object id), only what shading reads.
-struct DevMaterial {
-    double kd[3], ks[3], amb[3];
-    double exponent;
-    double kd_sig, ks_sig;          // Color::significance, color.rs:637-639
-    double ior;
+constexpr int32_t kMatPhong = 0;      // DevMaterial::kind (= rt_material_kind)
+constexpr int32_t kMatFresnel = 2;
+
+// What the fold and the significance tests read (ks, ks_sig, kind) shares the
+// first 64-B line.
+struct alignas(64) DevMaterial {
+    double ks[3];
+    double ks_sig;                  // Color::significance, color.rs:637-639
     int32_t kind;                   // rt_material_kind
     int32_t _pad;
+    double kd_sig;
+    double ior;
+    double kd[3], amb[3];
+    double exponent;
 };
 
 struct DevLight {
@@ -75,6 +82,7 @@ struct DevScene {
     int32_t n_spheres, n_planes, n_lights, n_bvh;
     const DevBvh4Plane* bvh4;       // the same tree collapsed 4-wide (DevBvh4Plane)
     int32_t bvh4_root, n_bvh4;
+    int32_t has_fresnel;            // some object uses FresnelMaterial
     double cam_pos[3];
     double cam_m[9];                // row-major
     double bg[3];
@@ -116,6 +124,7 @@ struct WfBufs {
     uint32_t* occ;                  // per shade record: bit l set = light l shadowed
     double* st[3];                  // per-level local colour, [level * cap + p]
     int32_t* st_obj;                // per-level object id (its specular colour is the fold factor)
+    double* st_f;                   // per-level Schlick factor, written for FresnelMaterial levels only
     double* term[3];                // terminal colour of each pixel's chain
     uint8_t* nlev;                  // levels pushed per pixel
     uint32_t* rq;                   // [k * G + r]: entries in region r of Q_k (written by its producer)

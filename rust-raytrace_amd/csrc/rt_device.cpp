@@ -83,6 +83,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 constexpr int kTotals = 2 * kCounterShards;
 constexpr int kGenTotals = kTotals + 8;
 constexpr int kCounterWords = kGenTotals + kCntWords;
+static_assert(kMatPhong == RT_MAT_PHONG && kMatFresnel == RT_MAT_FRESNEL, "DevMaterial::kind mirrors rt_material_kind");
 // LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
 constexpr size_t kLdsBudget = 72 * 1024;
 
@@ -131,6 +132,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     add(reinterpret_cast<void**>(&b.occ), q * 4);
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.st[a]), static_cast<size_t>(levels) * cap * 8);
     add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
+    add(reinterpret_cast<void**>(&b.st_f), static_cast<size_t>(levels) * cap * 8);
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.term[a]), static_cast<size_t>(cap) * 8);
     add(reinterpret_cast<void**>(&b.nlev), cap);
     add(reinterpret_cast<void**>(&b.rq), static_cast<size_t>(kMaxGenerations) * G * 4);
@@ -233,8 +235,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     std::vector<DevLight> lights;
     for (size_t i = 0; i < s->objects.size(); ++i) {
         const rt_object& o = s->objects[i];
-        if (o.material != RT_MAT_PHONG)
-            return fail(c, RT_E_UNSUPPORTED, "object " + std::to_string(i) + ": only PhongMaterial is implemented on the device path");
+        if (o.material != RT_MAT_PHONG && o.material != RT_MAT_FRESNEL)
+            return fail(c, RT_E_UNSUPPORTED, "object " + std::to_string(i) +
+                                                 ": only PhongMaterial and FresnelMaterial are implemented on the device path");
         if (o.shape == RT_SHAPE_SPHERE) {
             spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
             sphere_obj.push_back(static_cast<int32_t>(i));
@@ -336,6 +339,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.bvh4 = reinterpret_cast<const DevBvh4Plane*>(base + o_bvh4);
     d.bvh4_root = bvh4.root;
     d.n_bvh4 = bvh4.n_nodes;
+    d.has_fresnel = 0;
+    for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
     for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
     d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;

@@ -610,9 +610,40 @@ __device__ __forceinline__ bool light_dir(const DevLight& L, double ptx, double 
     return false;
 }
 
-// The diffuse and Blinn-Phong terms of one unshadowed light (raytrace.rs:51-56).
+// FresnelMaterial's Schlick factor from the UNflipped n.d (raytrace.rs:128-136),
+// in the reference's operation order.
+__device__ __forceinline__ double fresnel_factor(const DevMaterial& m, double nd) {
+    double r0 = (m.ior - 1.0) / (m.ior + 1.0);
+    r0 = r0 * r0;
+    const double omcos = 1.0 - fabs(nd);
+    const double omcos2 = omcos * omcos;
+    const double f = r0 + (((1.0 - r0) * omcos2) * omcos2) * omcos;
+    return f > 1.0 ? 1.0 : f;                                       // clamp_one, raytrace.rs:26-28
+}
+
+// The per-hit flags of PhongMaterial / FresnelMaterial::color.  `f` is the
+// Fresnel factor (1.0 for Phong): every Fresnel expression multiplies the
+// Phong one by f in a position where x * 1.0 == x exactly, so one code path
+// reproduces both materials bit for bit.
+struct Shading {
+    bool diffuse, specular;
+    double f;
+};
+
+// kFresnel = false: the scene has no FresnelMaterial (f is the constant 1.0).
+template <bool kFresnel = true>
+__device__ __forceinline__ Shading shading_flags(const DevMaterial& m, double sig, double nd) {
+    Shading s;
+    s.f = kFresnel && m.kind == kMatFresnel ? fresnel_factor(m, nd) : 1.0;
+    s.diffuse = m.kd_sig * sig > kMinSignificance;                  // raytrace.rs:35 / 137
+    s.specular = (m.ks_sig * s.f) * sig > kMinSignificance;         // raytrace.rs:36 / 138
+    return s;
+}
+
+// The diffuse and specular terms of one unshadowed light (raytrace.rs:51-56,
+// Fresnel: 151-156, where the specular term is ((ks * lc) * f) * pow).
 __device__ __forceinline__ void add_light(Col& res, const DevMaterial& m, const DevLight& L, bool diffuse, bool specular,
-                                          double lx, double ly, double lz, double nx, double ny, double nz,
+                                          double f, double lx, double ly, double lz, double nx, double ny, double nz,
                                           double dx, double dy, double dz) {
     if (diffuse) {
         const double s = clamp_zero(lx * nx + ly * ny + lz * nz);
@@ -625,9 +656,9 @@ __device__ __forceinline__ void add_light(Col& res, const DevMaterial& m, const 
         const double hl = sqrt(hx * hx + hy * hy + hz * hz);
         const double c = clamp_zero(nx * (hx / hl) + ny * (hy / hl) + nz * (hz / hl));
         const double p = pow(c, m.exponent);
-        res.r = res.r + (m.ks[0] * L.color[0]) * p;
-        res.g = res.g + (m.ks[1] * L.color[1]) * p;
-        res.b = res.b + (m.ks[2] * L.color[2]) * p;
+        res.r = res.r + ((m.ks[0] * L.color[0]) * f) * p;
+        res.g = res.g + ((m.ks[1] * L.color[1]) * f) * p;
+        res.b = res.b + ((m.ks[2] * L.color[2]) * f) * p;
     }
 }
 

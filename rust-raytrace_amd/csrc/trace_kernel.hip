@@ -43,7 +43,7 @@ constexpr int kBlock = 256;                 // 4 waves
 template <class SpherePtr>
 __device__ Col trace_chain(const DevScene& sc, SpherePtr S, Ray ray, uint32_t max_depth, uint32_t& rays,
                            uint32_t& shadows) {
-    double st_r[kMaxLevels], st_g[kMaxLevels], st_b[kMaxLevels];
+    double st_r[kMaxLevels], st_g[kMaxLevels], st_b[kMaxLevels], st_f[kMaxLevels];
     int32_t st_obj[kMaxLevels];
     int lvl = 0;
     double sig = 1.0;
@@ -59,9 +59,10 @@ __device__ Col trace_chain(const DevScene& sc, SpherePtr S, Ray ray, uint32_t ma
         const double ptx = ray.ox + ray.dx * h.t, pty = ray.oy + ray.dy * h.t, ptz = ray.oz + ray.dz * h.t;
         double nx, ny, nz;
         hit_normal(sc, sc.spheres, h.prim, ptx, pty, ptz, nx, ny, nz);
-        const bool diffuse = m.kd_sig * sig > kMinSignificance;
-        const bool specular = m.ks_sig * sig > kMinSignificance;
-        if (nx * ray.dx + ny * ray.dy + nz * ray.dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+        const double nd = nx * ray.dx + ny * ray.dy + nz * ray.dz;
+        const Shading sh = shading_flags(m, sig, nd);
+        const bool diffuse = sh.diffuse, specular = sh.specular;
+        if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
         if (diffuse || specular) {
             for (int li = 0; li < sc.n_lights; ++li) {
                 const DevLight& L = sc.lights[li];
@@ -71,22 +72,22 @@ __device__ Col trace_chain(const DevScene& sc, SpherePtr S, Ray ray, uint32_t ma
                 ++rays;
                 ++shadows;
                 if (occluded_brute(sc, S, sray, has_range, r2)) continue;
-                add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, ray.dx, ray.dy, ray.dz);
+                add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, ray.dx, ray.dy, ray.dz);
             }
         }
         if (!specular) { term = res; break; }
-        st_r[lvl] = res.r; st_g[lvl] = res.g; st_b[lvl] = res.b; st_obj[lvl] = h.obj;
+        st_r[lvl] = res.r; st_g[lvl] = res.g; st_b[lvl] = res.b; st_obj[lvl] = h.obj; st_f[lvl] = sh.f;
         ++lvl;
         ray = reflect_ray(ray, ptx, pty, ptz, nx, ny, nz);
-        sig = sig * m.ks_sig;
+        sig = (sh.f * sig) * m.ks_sig;                             // raytrace.rs:63 / 163
         ++depth;
     }
-    Col acc = term;                                                // fold inner-first (raytrace.rs:63)
+    Col acc = term;                                                // fold inner-first (raytrace.rs:63 / 163)
     for (int k = lvl - 1; k >= 0; --k) {
         const DevMaterial& m = sc.mats[st_obj[k]];
-        acc.r = st_r[k] + m.ks[0] * acc.r;
-        acc.g = st_g[k] + m.ks[1] * acc.g;
-        acc.b = st_b[k] + m.ks[2] * acc.b;
+        acc.r = st_r[k] + (m.ks[0] * acc.r) * st_f[k];
+        acc.g = st_g[k] + (m.ks[1] * acc.g) * st_f[k];
+        acc.b = st_b[k] + (m.ks[2] * acc.b) * st_f[k];
     }
     return acc;
 }
@@ -412,8 +413,19 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
                 else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
             } else {
                 const DevMaterial& m = sc.mats[h.obj];
-                const bool lit = static_cast<uint32_t>(k) <= fp.max_depth &&   // raytrace.rs:33
-                                 (m.kd_sig * sig > kMinSignificance || m.ks_sig * sig > kMinSignificance);
+                bool lit = static_cast<uint32_t>(k) <= fp.max_depth;            // raytrace.rs:33 / 126
+                if (lit) {
+                    // FresnelMaterial's specular flag needs the Schlick factor (n.d of the hit)
+                    double nd = 0.0;
+                    if (m.kind == kMatFresnel) {
+                        double nx, ny, nz;
+                        hit_normal(sc, v.sph, h.prim, r.ox + r.dx * h.t, r.oy + r.dy * h.t, r.oz + r.dz * h.t,
+                                   nx, ny, nz);
+                        nd = nx * r.dx + ny * r.dy + nz * r.dz;
+                    }
+                    const Shading shf = shading_flags(m, sig, nd);
+                    lit = shf.diffuse || shf.specular;
+                }
                 if (!lit) {
                     set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
                 } else {
@@ -470,6 +482,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
 // The Phong sum of every shade record (raytrace.rs:31-56), then either the
 // level push + reflection ray into this workgroup's region of Q_{k+1}
 // (raytrace.rs:58-64) or the end of the chain.
+template <bool kFresnel>
 __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
     __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
@@ -493,11 +506,12 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
             p = b.sr_pix[at];
             const DevMaterial& m = sc.mats[obj];
             Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
-            const bool diffuse = m.kd_sig * sig > kMinSignificance;
-            const bool specular = m.ks_sig * sig > kMinSignificance;
             double nx, ny, nz;
             hit_normal(sc, sc.spheres, b.sr_prim[at], ptx, pty, ptz, nx, ny, nz);
-            if (nx * dx + ny * dy + nz * dz > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+            const double nd = nx * dx + ny * dy + nz * dz;
+            const Shading sh = shading_flags<kFresnel>(m, sig, nd);
+            const bool diffuse = sh.diffuse, specular = sh.specular;
+            if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
             if (sc.n_lights > 0) {
                 const uint32_t mask = b.occ[at];
                 for (int l = 0; l < sc.n_lights; ++l) {
@@ -505,15 +519,16 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
                     const DevLight& L = sc.lights[l];
                     double lx, ly, lz, r2;
                     light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
-                    add_light(res, m, L, diffuse, specular, lx, ly, lz, nx, ny, nz, dx, dy, dz);
+                    add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
                 }
             }
             if (specular) {
                 const size_t st = static_cast<size_t>(k) * b.cap + p;
                 b.st[0][st] = res.r; b.st[1][st] = res.g; b.st[2][st] = res.b;
                 b.st_obj[st] = obj;
+                if (kFresnel && m.kind == kMatFresnel) b.st_f[st] = sh.f;
                 rr = reflect_ray(Ray{0, 0, 0, dx, dy, dz}, ptx, pty, ptz, nx, ny, nz);
-                nsig = sig * m.ks_sig;
+                nsig = (sh.f * sig) * m.ks_sig;                                  // raytrace.rs:63 / 163
                 refl = true;
             } else {
                 set_terminal(b, p, res, k);
@@ -532,11 +547,12 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     if (threadIdx.x == 0) b.rq[(k + 1) * b.G + blockIdx.x] = s_cnt;
 }
 
-// The fold factor of a level is the specular colour of its object
-// (raytrace.rs:63).  The chain is folded inner-first exactly as the
+// The fold factor of a level is the specular colour of its object times, for
+// FresnelMaterial, the level's Schlick factor (raytrace.rs:63 / 163).  The chain is folded inner-first exactly as the
 // recursion returns (acc = res_k + ks_k * acc); the loads of four levels are
 // issued together so a pixel costs about two memory round trips per four
 // levels instead of two per level.
+template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
     if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
     Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
@@ -551,20 +567,21 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
                 sr[u] = b.st[0][at]; sg[u] = b.st[1][at]; sb[u] = b.st[2][at];
             }
         }
-        double kr[4], kg[4], kb[4];
+        double kr[4], kg[4], kb[4], kf[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (k - u >= 0) {
                 const DevMaterial& m = sc.mats[ob[u]];
                 kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
+                kf[u] = kFresnel && m.kind == kMatFresnel ? b.st_f[static_cast<size_t>(k - u) * b.cap + p] : 1.0;
             }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (k - u >= 0) {
-                acc.r = sr[u] + kr[u] * acc.r;
-                acc.g = sg[u] + kg[u] * acc.g;
-                acc.b = sb[u] + kb[u] * acc.b;
+            if (k - u >= 0) {                  // res + (ks * child) * f, f = 1 for Phong (raytrace.rs:63 / 163)
+                acc.r = sr[u] + (kr[u] * acc.r) * kf[u];
+                acc.g = sg[u] + (kg[u] * acc.g) * kf[u];
+                acc.b = sb[u] + (kb[u] * acc.b) * kf[u];
             }
         }
     }
@@ -577,7 +594,7 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
 // kStaged: each workgroup's 256 pixels lie in one output row (tile_w % 256
 // == 0, BGR rows unpadded and dword aligned): the workgroup assembles its
 // 3 KiB of RGB and 768 B of BGR in LDS and stores them as whole dwords.
-template <bool kStaged>
+template <bool kStaged, bool kFresnel>
 __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
@@ -591,13 +608,13 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
     if (__syncthreads_and(nlev == kNlevDone)) return;
     if constexpr (!kStaged) {
         if (p < npix && nlev != kNlevDone) {
-            const Col res = average_samples(fold_pixel(sc, b, p, nlev), fp.spp);
+            const Col res = average_samples(fold_pixel<kFresnel>(sc, b, p, nlev), fp.spp);
             write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
         }
     } else {
         // the whole 256-pixel row segment is stored; done pixels re-derive the
         // background (bit-identical to the host-computed value) without loads
-        const Col res = average_samples(fold_pixel(sc, b, p, nlev), fp.spp);   // npix % 256 == 0 here
+        const Col res = average_samples(fold_pixel<kFresnel>(sc, b, p, nlev), fp.spp);   // npix % 256 == 0 here
         s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
         s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
         s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
@@ -683,7 +700,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         e = m ? m->mark(s, kKfOcclusion) : hipSuccess;
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(wf_shade, grid, block, 0, s, sc, fp, b, k);
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, s, sc, fp, b, k);
+    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, s, sc, fp, b, k);
     return m ? m->mark(s, kKfShade) : hipSuccess;
 }
 
@@ -722,8 +740,14 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
     const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
-    if (staged) hipLaunchKernelGGL(wf_fold<true>, gf, dim3(kBlock), 0, s, sc, fp, b);
-    else hipLaunchKernelGGL(wf_fold<false>, gf, dim3(kBlock), 0, s, sc, fp, b);
+    // the Fresnel-capable fold costs registers; scenes without FresnelMaterial use the plain one
+    if (sc.has_fresnel) {
+        if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
+        else hipLaunchKernelGGL((wf_fold<false, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
+    } else {
+        if (staged) hipLaunchKernelGGL((wf_fold<true, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
+        else hipLaunchKernelGGL((wf_fold<false, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
+    }
     hipError_t e = marks ? marks->mark(s, kKfFold) : hipSuccess;
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);

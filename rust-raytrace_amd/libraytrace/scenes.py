@@ -111,6 +111,12 @@ def phong(diffuse, specular, exponent, ambient):
             "exponent": float(exponent), "ambient": tuple(ambient)}
 
 
+def fresnel(diffuse, specular, exponent, ambient, ior):
+    """FresnelMaterial (raytrace.rs:123-167): Phong with a Schlick-weighted specular."""
+    return {"kind": "fresnel", "diffuse": tuple(diffuse), "specular": tuple(specular),
+            "exponent": float(exponent), "ambient": tuple(ambient), "ior": float(ior)}
+
+
 def _material_text(m):
     k = m["kind"]
     if k == "phong":
@@ -163,6 +169,27 @@ def config2(width=1920, height=1080):
                  phong(kd, (0.3, 0.3, 0.3), 32.0, tuple(0.02 * c for c in kd)))
     s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), phong((0.6, 0.6, 0.6), (0.1, 0.1, 0.1), 16.0, (0.01, 0.01, 0.01)))
     _lights(s)
+    return s
+
+
+def config2_fresnel(width=1920, height=1080, max_depth=6):
+    """C2 with FresnelMaterial on every other sphere (ior 1.3 .. 2.0) and on a
+    mirror-like ground plane, plus a directional light."""
+    s = SceneSpec(width=width, height=height, antialias=1, max_depth=max_depth, name="c2f",
+                  camera=dict(DEFAULT_CAMERA), background=(0.05, 0.05, 0.05))
+    for i in range(8):
+        a = 2.0 * math.pi * i / 8.0
+        kd = colorsys.hsv_to_rgb(i / 8.0, 0.7, 0.9)
+        amb = tuple(0.02 * c for c in kd)
+        if i % 2:
+            m = fresnel(kd, (0.9, 0.9, 0.9), 64.0, amb, 1.3 + 0.1 * i)
+        else:
+            m = phong(kd, (0.3, 0.3, 0.3), 32.0, amb)
+        s.sphere((4.0 * math.cos(a), 1.0, -6.0 + 4.0 * math.sin(a)), 1.0, m)
+    s.sphere((0.0, 1.5, -6.0), 1.5, fresnel((0.1, 0.1, 0.1), (1.0, 1.0, 1.0), 128.0, (0.0, 0.0, 0.0), 1.5))
+    s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), fresnel((0.6, 0.6, 0.6), (0.8, 0.8, 0.8), 16.0, (0.01, 0.01, 0.01), 1.33))
+    _lights(s)
+    s.directional_light((0.3, -1.0, -0.2), (0.3, 0.3, 0.35))
     return s
 
 

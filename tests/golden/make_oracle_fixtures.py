@@ -32,7 +32,8 @@ def fixture_specs():
     mirror = scenes.random_spheres(40, 48, 40, 16, seed=11, plane=True, name="mirror16")
     for o in mirror.objects:   # strong mirrors: significance never falls below 1/512 -> full depth
         o["material"] = dict(o["material"], specular=(0.9, 0.8, 0.95))
-    return {"c2_96x54": c2, "c3_64x64": c3, "mirror16_48x40": mirror}
+    c2f = scenes.config2_fresnel(80, 45)      # FresnelMaterial + directional light
+    return {"c2_96x54": c2, "c3_64x64": c3, "mirror16_48x40": mirror, "c2fresnel_80x45": c2f}
 
 
 def bmp_bytes(w, h, bgr_rows):

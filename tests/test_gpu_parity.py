@@ -66,6 +66,29 @@ def test_config3_downscaled(gpu_ctx, algo):
     print(f"C3 256x256 algo={algo}: f32 bit-identical fraction {frac:.6f}, rays {st.rays}")
 
 
+@pytest.mark.parametrize("algo", ALGOS)
+def test_fresnel_material(gpu_ctx, algo):
+    """FresnelMaterial (raytrace.rs:123-167) on spheres and the ground plane,
+    with point and directional lights: Schlick factor from the unflipped n.d,
+    Fresnel-weighted specular, fresnel*sig*ks.sig significance and the
+    (ks * child) * fresnel fold."""
+    frac, st = check_parity(gpu_ctx, scenes.config2_fresnel(320, 180), algo)
+    print(f"C2-Fresnel 320x180 algo={algo}: f32 bit-identical fraction {frac:.6f}, rays {st.rays}")
+
+
+def test_fresnel_random_spheres_deep(gpu_ctx):
+    """A third of C3's spheres turned Fresnel, depth 16: mixed Phong / Fresnel
+    chains through the BVH paths."""
+    spec = scenes.config3(192, 128)
+    spec.max_depth = 16
+    for i, o in enumerate(spec.objects):
+        if i % 3 == 0:
+            m = o["material"]
+            o["material"] = scenes.fresnel(m["diffuse"], (0.95, 0.95, 0.95), m["exponent"], m["ambient"],
+                                           1.2 + 0.05 * (i % 16))
+    check_parity(gpu_ctx, spec)
+
+
 def test_config3_full_size_sampled_rows(gpu_ctx):
     """The headline config at full size: every 256th row (16 rows x 4096 px)
     checked against the oracle, plus frame-level properties."""
@@ -81,7 +104,7 @@ def test_config3_full_size_sampled_rows(gpu_ctx):
     assert np.isfinite(rgb).all()
 
 
-@pytest.mark.parametrize("name", ["c2_96x54", "c3_64x64", "mirror16_48x40"])
+@pytest.mark.parametrize("name", ["c2_96x54", "c3_64x64", "mirror16_48x40", "c2fresnel_80x45"])
 def test_golden_fixtures(gpu_ctx, name):
     z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     sc = lr.Scene.deserialize(str(z["scene_text"]))

@@ -113,8 +113,11 @@ struct WfBufs {
     double* qd[2][3];               // ray direction
     double* qsig[2];                // significance passed down (raytrace.rs:63)
     uint32_t* qpix[2];              // owning pixel (chunk-local index)
-    // Shade records of the current generation: the hits that go on to light
-    // evaluation and/or reflection, in the same block-partitioned layout as the queues.
+    // Shade records: the hits that go on to light evaluation and/or
+    // reflection, in the same block-partitioned layout as the queues, one
+    // record buffer PER GENERATION (generation k at offset k * rstride), so
+    // the nearest-hit kernels never wait for the shadow / shading kernels of
+    // earlier generations (which run on a second stream).
     double* sr_pt[3];               // hit point ray.cast(t)
     double* sr_d[3];                // incoming direction
     double* sr_sig;                 // significance
@@ -132,11 +135,14 @@ struct WfBufs {
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
+    size_t rstride;                 // entries per generation of the shade-record arrays (= G * R)
     uint32_t cap;                   // pixel capacity (stack stride)
     uint32_t G;                     // regions per queue
     uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
     uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
+    uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
+                                    // workgroup (idle workgroups exit at once), 0 = workgroup-first
 };
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels

@@ -12,9 +12,10 @@ namespace rtamd {
 // Kernel families of the wavefront schedule (rt_ctx_kernel_times indices).
 enum KernelFamily : int8_t { kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCount = 5 };
 
-// Per-launch timing (RT_TIME_KERNELS): begin() records a start event, mark()
-// an end event after each launch, noting (start, end, family); elapsed time
-// between the two = that launch's duration on an in-order stream.  Events
+// Per-launch timing (RT_TIME_KERNELS): begin() records a start event before a
+// launch (after any cross-stream wait), mark() an end event after it, noting
+// (start, end, family): the elapsed time between the two is that launch's
+// duration (one LaunchMarks per stream).  Events
 // come from a pool owned by the context; intervals accumulate over renders
 // until harvested (rt_ctx_kernel_times).
 struct LaunchInterval {
@@ -57,8 +58,23 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 // LDS, 7 = 4 held to 64 VGPRs, 10 4-wide BVH + spheres in LDS (64 VGPRs),
 // 11 4-wide BVH from HBM/L2, 12 = 10 with 128 VGPRs.  Supported (nearest,
 // occlusion) pairs: (s, s) for every s, (7, 10), (2, 11).
+// The streams of one wavefront lane: a runs the nearest-hit chain and the
+// fold; the shadow + shading kernels of generation k run on b[k % nb] (b[i] ==
+// a: one in-order stream).  near_done: kMaxGenerations events; b_done: one
+// per b stream; marks may be null.  fuse: shading inside the shadow kernel.
+constexpr int kMaxBStreams = 4;
+struct WfStreams {
+    hipStream_t a;
+    hipStream_t b[kMaxBStreams];
+    int nb;
+    hipEvent_t* near_done;
+    hipEvent_t b_done[kMaxBStreams];
+    LaunchMarks* ma;
+    LaunchMarks* mb[kMaxBStreams];
+    bool fuse;
+};
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
-                            bool count, hipStream_t s, hipEvent_t mark, int mark_gen, LaunchMarks* marks);
+                            bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
 
 }  // namespace rtamd

@@ -42,7 +42,10 @@ struct rt_ctx {
     // so its big launches overlap chunk c's latency-bound tail.
     struct Lane {
         hipStream_t s = nullptr;
+        std::vector<hipStream_t> sb;       // shadow + shading kernels of the generations
         hipEvent_t mark = nullptr, done = nullptr;
+        std::vector<hipEvent_t> b_done;    // one per sb stream
+        std::vector<hipEvent_t> near_done; // per generation: nearest-hit kernel finished (s -> sb)
         void* mem = nullptr;
         size_t bytes = 0;
         WfBufs b{};
@@ -98,19 +101,46 @@ uint32_t wf_chunk_pixels() {
     return v > 0 ? static_cast<uint32_t>(v) : (1u << 24);
 }
 
+// The b streams need hardware queues of their own: HIP deals streams over a
+// few shared queues (GPU_MAX_HW_QUEUES), and two streams on one queue run
+// strictly in submission order.  A CU-masked stream (mask = every CU) gets a
+// dedicated queue.  Created on demand: every extra hardware queue costs the
+// firmware scheduler, measurably slowing the others.
+int ensure_bstreams(rt_ctx* c, rt_ctx::Lane& M, int nb) {
+    std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
+    for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    while (static_cast<int>(M.sb.size()) < nb) {
+        hipStream_t s = nullptr;
+        if (env_int("RT_WF_CUMASK", 1) == 0 ||
+            hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        }
+        M.sb.push_back(s);
+        hipEvent_t e = nullptr;
+        HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        M.b_done.push_back(e);
+    }
+    return RT_OK;
+}
+
 int ensure_lanes(rt_ctx* c, int n) {
     while (static_cast<int>(c->lanes.size()) < n) {
         rt_ctx::Lane L;
-        HIP_TRY(c, hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
-        HIP_TRY(c, hipEventCreateWithFlags(&L.mark, hipEventDisableTiming));
-        HIP_TRY(c, hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
         c->lanes.push_back(L);
+        rt_ctx::Lane& M = c->lanes.back();
+        HIP_TRY(c, hipStreamCreateWithFlags(&M.s, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&M.mark, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&M.done, hipEventDisableTiming));
+        M.near_done.assign(kMaxGenerations, nullptr);
+        for (hipEvent_t& e : M.near_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return RT_OK;
 }
 
 // Carve a lane's wavefront working set for chunks of up to `cap` pixels: every
-// queue and shade-record array is G regions of R entries.
+// queue and shade-record array is G regions of R entries; the shade records
+// have one such array per lit generation (`levels` = max_depth + 1).
 int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels) {
     WfBufs& b = L.b;
     size_t off = 0;
@@ -123,13 +153,14 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         add(reinterpret_cast<void**>(&b.qsig[g]), q * 8);
         add(reinterpret_cast<void**>(&b.qpix[g]), q * 4);
     }
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_pt[a]), q * 8);
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_d[a]), q * 8);
-    add(reinterpret_cast<void**>(&b.sr_sig), q * 8);
-    add(reinterpret_cast<void**>(&b.sr_obj), q * 4);
-    add(reinterpret_cast<void**>(&b.sr_prim), q * 4);
-    add(reinterpret_cast<void**>(&b.sr_pix), q * 4);
-    add(reinterpret_cast<void**>(&b.occ), q * 4);
+    const size_t qr = q * levels;                  // shade records: one region array per generation
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_pt[a]), qr * 8);
+    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_d[a]), qr * 8);
+    add(reinterpret_cast<void**>(&b.sr_sig), qr * 8);
+    add(reinterpret_cast<void**>(&b.sr_obj), qr * 4);
+    add(reinterpret_cast<void**>(&b.sr_prim), qr * 4);
+    add(reinterpret_cast<void**>(&b.sr_pix), qr * 4);
+    add(reinterpret_cast<void**>(&b.occ), qr * 4);
     for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.st[a]), static_cast<size_t>(levels) * cap * 8);
     add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
     add(reinterpret_cast<void**>(&b.st_f), static_cast<size_t>(levels) * cap * 8);
@@ -138,7 +169,11 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     add(reinterpret_cast<void**>(&b.rq), static_cast<size_t>(kMaxGenerations) * G * 4);
     add(reinterpret_cast<void**>(&b.rs), static_cast<size_t>(kMaxGenerations) * G * 4);
     if (off > L.bytes) {
-        if (L.mem) { (void)hipStreamSynchronize(L.s); (void)hipFree(L.mem); }
+        if (L.mem) {
+            (void)hipStreamSynchronize(L.s);
+            for (hipStream_t x : L.sb) (void)hipStreamSynchronize(x);
+            (void)hipFree(L.mem);
+        }
         L.mem = nullptr;
         L.bytes = 0;
         HIP_TRY(c, hipMalloc(&L.mem, off));
@@ -148,6 +183,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     for (auto& pr : parts) *pr.first = base + pr.second;
     b.totals = c->d_counters + kTotals;
     b.gen_totals = c->d_counters + kGenTotals;
+    b.rstride = q;
     b.cap = cap;
     b.G = G;
     b.R = R;
@@ -203,10 +239,14 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->d_bgr) (void)hipFree(c->d_bgr);
     for (auto& L : c->lanes) {
         if (L.s) (void)hipStreamSynchronize(L.s);
+        for (hipStream_t x : L.sb) if (x) (void)hipStreamSynchronize(x);
         if (L.mem) (void)hipFree(L.mem);
         if (L.mark) (void)hipEventDestroy(L.mark);
         if (L.done) (void)hipEventDestroy(L.done);
+        for (hipEvent_t e : L.b_done) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
         if (L.s) (void)hipStreamDestroy(L.s);
+        for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
     }
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     if (c->fork) (void)hipEventDestroy(c->fork);
@@ -469,22 +509,38 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
         G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
         const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
+        // RT_WF_SPLIT=0: every kernel on one in-order stream (A/B measurement);
+        // RT_WF_DEAL: 1 workgroup-major chunk dealing (default), 0 workgroup-first
+        // RT_WF_BSTREAMS: streams for the shadow + shading kernels (default 1;
+        // generations alternate over them); RT_WF_FUSE=0: separate shading kernel
+        const bool split = env_int("RT_WF_SPLIT", 1) != 0;
+        const int n_b = std::max(1, std::min(kMaxBStreams, env_int("RT_WF_BSTREAMS", 1)));
+        const bool fuse = env_int("RT_WF_FUSE", 1) != 0;
+        const uint32_t wg_major = env_int("RT_WF_DEAL", 1) != 0 ? 1u : 0u;
         for (int l = 0; l < n_lanes; ++l) {
+            if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
             rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1);
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
+            c->lanes[l].b.wg_major = wg_major;
         }
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
         // per-launch timing needs one in-order stream
         const bool timed = (o->flags & RT_TIME_KERNELS) != 0 && n_lanes == 1;
-        LaunchMarks marks;
-        marks.pool = &c->tev;
-        marks.used = &c->t_used;
-        marks.out = &c->tint;
+        LaunchMarks marks, marks_b[kMaxBStreams];
+        for (int i = -1; i < kMaxBStreams; ++i) {
+            LaunchMarks* m = i < 0 ? &marks : &marks_b[i];
+            m->pool = &c->tev;
+            m->used = &c->t_used;
+            m->out = &c->tint;
+        }
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, hipEventRecord(c->fork, st));
-        for (int l = 0; l < n_lanes; ++l) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
-        if (timed) HIP_TRY(c, marks.begin(c->lanes[0].s));
+        for (int l = 0; l < n_lanes; ++l) {
+            HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
+            if (split)
+                for (int i = 0; i < n_b; ++i) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].sb[i], c->fork, 0));
+        }
         for (uint32_t ci = 0; ci < n_chunks; ++ci) {
             rt_ctx::Lane& L = c->lanes[ci % n_lanes];
             if (ci > 0 && n_lanes > 1) HIP_TRY(c, hipStreamWaitEvent(L.s, c->lanes[(ci - 1) % n_lanes].mark, 0));
@@ -493,8 +549,18 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             f.rows = std::min(chunk_rows, o->tile_h - f.row0);
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
-            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, L.s, L.mark, mark_gen,
-                                        timed ? &marks : nullptr));
+            WfStreams ws{};
+            ws.a = L.s;
+            ws.nb = split ? n_b : 1;
+            for (int i = 0; i < ws.nb; ++i) {
+                ws.b[i] = split ? L.sb[i] : L.s;
+                ws.b_done[i] = split ? L.b_done[i] : nullptr;
+                ws.mb[i] = timed ? (split ? &marks_b[i] : &marks) : nullptr;
+            }
+            ws.near_done = L.near_done.data();
+            ws.ma = timed ? &marks : nullptr;
+            ws.fuse = fuse;
+            HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, ws, L.mark, mark_gen));
         }
         for (int l = 0; l < n_lanes; ++l) {
             HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));

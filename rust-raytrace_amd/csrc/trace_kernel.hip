@@ -151,13 +151,27 @@ __device__ __forceinline__ uint32_t lds_append(uint32_t* counter, bool want) {
     return want ? base + below : 0xFFFFFFFFu;
 }
 
-// Work dealing: a queue is consumed in 64-item chunks, chunk c by wave
-// c mod W (W = G * 16 waves), waves numbered workgroup-first, so a small tail
-// queue spreads over every workgroup (and CU) instead of filling the first
-// few; a workgroup still takes at most R items (16 chunks per round of W).
-// Loop condition and chunk are wave-uniform.
+// Work dealing: a queue is consumed in 64-item chunks; chunk c goes to wave
+// slot c mod W (W = G * 16 waves).  Slots are numbered workgroup-first
+// (b.wg_major = 0: a small tail queue spreads over every workgroup) or
+// workgroup-major (b.wg_major = 1: consecutive chunks fill one workgroup's
+// waves, so the workgroups past the queue's end exit at once and free their
+// CU for the kernels of the other stream).  Either way a workgroup takes at
+// most 16 chunks per round of W, i.e. at most R items.  Loop condition and
+// chunk are wave-uniform.
+__device__ __forceinline__ uint32_t wave_slot(const WfBufs& b) {
+    const uint32_t wave = threadIdx.x >> 6;
+    return b.wg_major ? blockIdx.x * (kWfThreads / 64) + wave : wave * b.G + blockIdx.x;
+}
+
+// Whether this workgroup's first chunk is below n (workgroup-uniform).
+__device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n) {
+    const uint64_t first = b.wg_major ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
+    return first * 64u < n;
+}
+
 #define RT_FOR_CHUNKS(b, n, j)                                                              \
-    for (uint32_t rt_c = (threadIdx.x >> 6) * (b).G + blockIdx.x, rt_w = (b).G * (kWfThreads / 64); \
+    for (uint32_t rt_c = wave_slot(b), rt_w = (b).G * (kWfThreads / 64);                     \
          static_cast<uint64_t>(rt_c) * 64u < static_cast<uint64_t>(n); rt_c += rt_w)        \
         if (const uint32_t j = rt_c * 64u + (threadIdx.x & 63u); true)
 
@@ -350,7 +364,7 @@ __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c,
 struct QueueLds {
     uint32_t* scan;     // G + 1
     uint32_t* wave;     // 16
-    uint32_t* count;    // 1
+    uint32_t* count;    // 2: shade records, reflection rays appended by this workgroup
 };
 
 __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
@@ -358,34 +372,43 @@ __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
     return QueueLds{p, p + G + 1, p + G + 1 + kWfThreads / 64};
 }
 
-__host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + 1) * 4u; }
+__host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + 2) * 4u; }
 
 // Scene::intersect for every ray of Q_k (generation 0: the camera rays of the
 // chunk, computed here).  Outcomes that end the chain without lighting are
 // resolved on the spot (miss -> background; depth cut-off or insignificant
-// surface -> ambient, raytrace.rs:32-35); the rest become shade records in
-// this workgroup's region.
-template <int kSrc, bool kCam, bool kCount>
+// surface -> ambient, raytrace.rs:32-35); the rest become shade records of
+// generation k in this workgroup's region, and a specular hit also appends
+// its reflection ray (raytrace.rs:58-64) to Q_{k+1} right here: the next
+// generation depends only on the hit, never on the shadow rays or the Phong
+// sum, so those run on the other stream, off the critical path.
+template <int kSrc, bool kCam, bool kCount, bool kFresnel>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const BvhView v = stage_lds<kSrc>(sc, lds);
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
-    if (threadIdx.x == 0) *ql.count = 0;
+    if (threadIdx.x < 2) ql.count[threadIdx.x] = 0;
     uint32_t n;
     if constexpr (kCam) {
         n = b.slots;
-        __syncthreads();                                   // publishes the LDS staging
     } else {
         region_scan(b.rq + k * b.G, b.G, ql.scan, ql.wave);
         n = ql.scan[b.G];
     }
+    if (!wg_has_work(b, n)) {                  // nothing dealt here: publish empty regions, free the CU
+        if (threadIdx.x == 0) { b.rs[k * b.G + blockIdx.x] = 0; b.rq[(k + 1) * b.G + blockIdx.x] = 0; }
+        return;
+    }
+    const BvhView v = stage_lds<kSrc>(sc, lds);
+    __syncthreads();                                       // publishes the LDS staging and counters
     Work w;
-    const int q = k & 1;
+    const int qn = (k + 1) & 1;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
+    const size_t rbase = static_cast<size_t>(k) * b.rstride + obase;
     RT_FOR_CHUNKS(b, n, j) {
-        bool shade = false;
+        bool shade = false, refl = false;
         Ray r{};
-        double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0;
+        double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0, nsig = 0.0;
+        Ray rr{};
         uint32_t p = 0;
         Hit h{};
         bool live = false;
@@ -400,9 +423,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
                 }
             } else {
                 const size_t at = region_entry(ql.scan, b.G, b.R, j);
-                r = load_ray(b, q, at);
-                sig = b.qsig[q][at];
-                p = b.qpix[q][at];
+                r = load_ray(b, k & 1, at);
+                sig = b.qsig[k & 1][at];
+                p = b.qpix[k & 1][at];
                 live = true;
             }
         }
@@ -413,30 +436,31 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
                 else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
             } else {
                 const DevMaterial& m = sc.mats[h.obj];
-                bool lit = static_cast<uint32_t>(k) <= fp.max_depth;            // raytrace.rs:33 / 126
-                if (lit) {
-                    // FresnelMaterial's specular flag needs the Schlick factor (n.d of the hit)
-                    double nd = 0.0;
-                    if (m.kind == kMatFresnel) {
-                        double nx, ny, nz;
-                        hit_normal(sc, v.sph, h.prim, r.ox + r.dx * h.t, r.oy + r.dy * h.t, r.oz + r.dz * h.t,
-                                   nx, ny, nz);
-                        nd = nx * r.dx + ny * r.dy + nz * r.dz;
-                    }
-                    const Shading shf = shading_flags(m, sig, nd);
-                    lit = shf.diffuse || shf.specular;
-                }
-                if (!lit) {
+                if (static_cast<uint32_t>(k) > fp.max_depth) {                  // raytrace.rs:33 / 126
                     set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
                 } else {
-                    shade = true;
                     ptx = r.ox + r.dx * h.t; pty = r.oy + r.dy * h.t; ptz = r.oz + r.dz * h.t;   // ray.cast(t)
+                    double nx, ny, nz;
+                    hit_normal(sc, v.sph, h.prim, ptx, pty, ptz, nx, ny, nz);
+                    const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
+                    const Shading sh = shading_flags<kFresnel>(m, sig, nd);
+                    if (!sh.diffuse && !sh.specular) {
+                        set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+                    } else {
+                        shade = true;
+                        if (sh.specular) {                                      // raytrace.rs:58-64 / 159-164
+                            if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+                            rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
+                            nsig = (sh.f * sig) * m.ks_sig;
+                            refl = true;
+                        }
+                    }
                 }
             }
         }
-        const uint32_t slot = lds_append(ql.count, shade);
+        const uint32_t slot = lds_append(&ql.count[0], shade);
         if (shade) {
-            const size_t at = obase + slot;
+            const size_t at = rbase + slot;
             b.sr_pt[0][at] = ptx; b.sr_pt[1][at] = pty; b.sr_pt[2][at] = ptz;
             b.sr_d[0][at] = r.dx; b.sr_d[1][at] = r.dy; b.sr_d[2][at] = r.dz;
             b.sr_sig[at] = sig;
@@ -445,98 +469,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             b.sr_pix[at] = p;
             b.occ[at] = 0u;
         }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) b.rs[k * b.G + blockIdx.x] = *ql.count;
-    flush_work<kCount>(b, 2, w);
-}
-
-// The shadow queries of every shade record (raytrace.rs:39-49): one work-item
-// per (record, light) pair -- the lights of one hit are independent queries --
-// setting bit l of the record's occlusion mask.
-template <int kSrc, bool kCount>
-__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const BvhView v = stage_lds<kSrc>(sc, lds);
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
-    region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
-    const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-    const uint32_t nrec = ql.scan[b.G], n = nrec * L;
-    Work w;
-    // light-major: a wave traces 64 consecutive records toward ONE light (coherent)
-    RT_FOR_CHUNKS(b, n, qi) {
-        if (qi >= n) continue;
-        const uint32_t l = qi / nrec, j = qi - l * nrec;
-        const size_t at = region_entry(ql.scan, b.G, b.R, j);
-        const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
-        double lx, ly, lz, r2;
-        const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
-        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        // the sphere the point lies on is tested first (it shadows every light behind its surface)
-        const int32_t hint = b.sr_prim[at];
-        if (occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w)) atomicOr(&b.occ[at], 1u << l);
-    }
-    flush_work<kCount>(b, 4, w);
-}
-
-// The Phong sum of every shade record (raytrace.rs:31-56), then either the
-// level push + reflection ray into this workgroup's region of Q_{k+1}
-// (raytrace.rs:58-64) or the end of the chain.
-template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    __shared__ uint32_t s_scan[kMaxRegions + 1];
-    __shared__ uint32_t s_wave[kWfThreads / 64];
-    __shared__ uint32_t s_cnt;
-    if (threadIdx.x == 0) s_cnt = 0;
-    region_scan(b.rs + k * b.G, b.G, s_scan, s_wave);
-    const uint32_t n = s_scan[b.G];
-    const int qn = (k + 1) & 1;
-    const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
-    RT_FOR_CHUNKS(b, n, j) {
-        bool refl = false;
-        Ray rr{};
-        double nsig = 0.0;
-        uint32_t p = 0;
-        if (j < n) {
-            const size_t at = region_entry(s_scan, b.G, b.R, j);
-            const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
-            const double dx = b.sr_d[0][at], dy = b.sr_d[1][at], dz = b.sr_d[2][at];
-            const double sig = b.sr_sig[at];
-            const int32_t obj = b.sr_obj[at];
-            p = b.sr_pix[at];
-            const DevMaterial& m = sc.mats[obj];
-            Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
-            double nx, ny, nz;
-            hit_normal(sc, sc.spheres, b.sr_prim[at], ptx, pty, ptz, nx, ny, nz);
-            const double nd = nx * dx + ny * dy + nz * dz;
-            const Shading sh = shading_flags<kFresnel>(m, sig, nd);
-            const bool diffuse = sh.diffuse, specular = sh.specular;
-            if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
-            if (sc.n_lights > 0) {
-                const uint32_t mask = b.occ[at];
-                for (int l = 0; l < sc.n_lights; ++l) {
-                    if ((mask >> l) & 1u) continue;                              // shadowed (raytrace.rs:42-49)
-                    const DevLight& L = sc.lights[l];
-                    double lx, ly, lz, r2;
-                    light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
-                    add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
-                }
-            }
-            if (specular) {
-                const size_t st = static_cast<size_t>(k) * b.cap + p;
-                b.st[0][st] = res.r; b.st[1][st] = res.g; b.st[2][st] = res.b;
-                b.st_obj[st] = obj;
-                if (kFresnel && m.kind == kMatFresnel) b.st_f[st] = sh.f;
-                rr = reflect_ray(Ray{0, 0, 0, dx, dy, dz}, ptx, pty, ptz, nx, ny, nz);
-                nsig = (sh.f * sig) * m.ks_sig;                                  // raytrace.rs:63 / 163
-                refl = true;
-            } else {
-                set_terminal(b, p, res, k);
-            }
-        }
-        const uint32_t slot = lds_append(&s_cnt, refl);
+        const uint32_t rslot = lds_append(&ql.count[1], refl);
         if (refl) {
-            const size_t at = obase + slot;
+            const size_t at = obase + rslot;
             b.qo[qn][0][at] = rr.ox; b.qo[qn][1][at] = rr.oy; b.qo[qn][2][at] = rr.oz;
             b.qd[qn][0][at] = rr.dx; b.qd[qn][1][at] = rr.dy; b.qd[qn][2][at] = rr.dz;
             b.qsig[qn][at] = nsig;
@@ -544,7 +479,109 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) b.rq[(k + 1) * b.G + blockIdx.x] = s_cnt;
+    if (threadIdx.x == 0) {
+        b.rs[k * b.G + blockIdx.x] = ql.count[0];
+        b.rq[(k + 1) * b.G + blockIdx.x] = ql.count[1];
+    }
+    flush_work<kCount>(b, 2, w);
+}
+
+// The Phong sum of shade record `at` of generation k (raytrace.rs:31-56) with
+// the shadow mask of its lights: a specular hit pushes the level's local
+// colour (its reflection ray was already queued by wf_nearest); any other hit
+// ends the chain with it.
+template <bool kFresnel>
+__device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
+    const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
+    const double dx = b.sr_d[0][at], dy = b.sr_d[1][at], dz = b.sr_d[2][at];
+    const double sig = b.sr_sig[at];
+    const int32_t obj = b.sr_obj[at];
+    const uint32_t p = b.sr_pix[at];
+    const DevMaterial& m = sc.mats[obj];
+    Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
+    double nx, ny, nz;
+    hit_normal(sc, sc.spheres, b.sr_prim[at], ptx, pty, ptz, nx, ny, nz);
+    const double nd = nx * dx + ny * dy + nz * dz;
+    const Shading sh = shading_flags<kFresnel>(m, sig, nd);
+    const bool diffuse = sh.diffuse, specular = sh.specular;
+    if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+    for (int l = 0; l < sc.n_lights; ++l) {
+        if ((mask >> l) & 1u) continue;                                  // shadowed (raytrace.rs:42-49)
+        const DevLight& L = sc.lights[l];
+        double lx, ly, lz, r2;
+        light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
+        add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
+    }
+    if (specular) {
+        const size_t st = static_cast<size_t>(k) * b.cap + p;
+        b.st[0][st] = res.r; b.st[1][st] = res.g; b.st[2][st] = res.b;
+        b.st_obj[st] = obj;
+        if (kFresnel && m.kind == kMatFresnel) b.st_f[st] = sh.f;
+    } else {
+        set_terminal(b, p, res, k);
+    }
+}
+
+// Fused shadow + shading: each (record, light) item adds its shadow bit and
+// one to the record's finished-light count (bits kOccCount..) in a single
+// atomic; the item that completes the count shades the record with the
+// final mask.  Needs n_lights < 2^kOccCount.
+constexpr int kOccCount = 24;
+constexpr int kMaxFusedLights = 24;
+
+// The shadow queries of every shade record of generation k (raytrace.rs:39-49):
+// one work-item per (record, light) pair -- the lights of one hit are
+// independent queries -- setting bit l of the record's occlusion mask
+// (kShade: and shading the record once its last light is done).
+template <int kSrc, bool kCount, bool kShade, bool kFresnel>
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
+    region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
+    const uint32_t L = static_cast<uint32_t>(sc.n_lights);
+    const uint32_t nrec = ql.scan[b.G], n = nrec * L;
+    if (!wg_has_work(b, n)) return;
+    const BvhView v = stage_lds<kSrc>(sc, lds);
+    __syncthreads();
+    Work w;
+    const size_t rk = static_cast<size_t>(k) * b.rstride;
+    // light-major: a wave traces 64 consecutive records toward ONE light (coherent)
+    RT_FOR_CHUNKS(b, n, qi) {
+        if (qi >= n) continue;
+        const uint32_t l = qi / nrec, j = qi - l * nrec;
+        const size_t at = rk + region_entry(ql.scan, b.G, b.R, j);
+        const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
+        double lx, ly, lz, r2;
+        const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+        // the sphere the point lies on is tested first (it shadows every light behind its surface)
+        const int32_t hint = b.sr_prim[at];
+        const bool occluded = occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
+        if constexpr (kShade) {
+            const uint32_t inc = (occluded ? 1u << l : 0u) + (1u << kOccCount);
+            const uint32_t now = atomicAdd(&b.occ[at], inc) + inc;
+            if ((now >> kOccCount) == L) shade_record<kFresnel>(sc, b, k, at, now & ((1u << kOccCount) - 1u));
+        } else {
+            if (occluded) atomicOr(&b.occ[at], 1u << l);
+        }
+    }
+    flush_work<kCount>(b, 4, w);
+}
+
+// The Phong sum of every shade record of generation k (scenes without lights,
+// or with more lights than the fused kernel's count field holds).
+template <bool kFresnel>
+__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    __shared__ uint32_t s_scan[kMaxRegions + 1];
+    __shared__ uint32_t s_wave[kWfThreads / 64];
+    region_scan(b.rs + k * b.G, b.G, s_scan, s_wave);
+    const uint32_t n = s_scan[b.G];
+    const size_t rk = static_cast<size_t>(k) * b.rstride;
+    RT_FOR_CHUNKS(b, n, j) {
+        if (j >= n) continue;
+        const size_t at = rk + region_entry(s_scan, b.G, b.R, j);
+        shade_record<kFresnel>(sc, b, k, at, sc.n_lights > 0 ? b.occ[at] : 0u);
+    }
 }
 
 // The fold factor of a level is the specular colour of its object times, for
@@ -686,37 +723,62 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 }
 
 template <int kSrcN, int kSrcO, bool kCount>
-hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, hipStream_t s,
-                             LaunchMarks* m) {
+hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws) {
     const dim3 grid(b.G), block(kWfThreads);
     const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
-    if (k == 0) hipLaunchKernelGGL((wf_nearest<kSrcN, true, kCount>), grid, block, lds_n, s, sc, fp, b, k);
-    else hipLaunchKernelGGL((wf_nearest<kSrcN, false, kCount>), grid, block, lds_n, s, sc, fp, b, k);
-    hipError_t e = m ? m->mark(s, kKfNearest) : hipSuccess;
+    hipError_t e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
+#define RT_NEAR(CAM, FR) hipLaunchKernelGGL((wf_nearest<kSrcN, CAM, kCount, FR>), grid, block, lds_n, ws.a, sc, fp, b, k)
+    if (sc.has_fresnel) {
+        if (k == 0) RT_NEAR(true, true); else RT_NEAR(false, true);
+    } else {
+        if (k == 0) RT_NEAR(true, false); else RT_NEAR(false, false);
+    }
+#undef RT_NEAR
+    e = ws.ma ? ws.ma->mark(ws.a, kKfNearest) : hipSuccess;
+    if (e != hipSuccess) return e;
+    if (static_cast<uint32_t>(k) > fp.max_depth) return hipSuccess;     // no shade records past the cut-off
+    // shadows and shading of generation k: on a b stream once nearest_k is done
+    // (generations alternate over the b streams, so consecutive ones overlap too)
+    const int bi = k % ws.nb;
+    const hipStream_t sb = ws.b[bi];
+    LaunchMarks* mb = ws.mb[bi];
+    if (sb != ws.a) {
+        if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(sb, ws.near_done[k], 0)) != hipSuccess) return e;
+    }
+    const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && ws.fuse;
     if (sc.n_lights > 0) {
         const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
-        hipLaunchKernelGGL((wf_occlusion<kSrcO, kCount>), grid, block, lds_o, s, sc, fp, b, k);
-        e = m ? m->mark(s, kKfOcclusion) : hipSuccess;
-        if (e != hipSuccess) return e;
+        if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+#define RT_OCC(SH, FR) hipLaunchKernelGGL((wf_occlusion<kSrcO, kCount, SH, FR>), grid, block, lds_o, sb, sc, fp, b, k)
+        if (!fused) RT_OCC(false, false);
+        else if (sc.has_fresnel) RT_OCC(true, true);
+        else RT_OCC(true, false);
+#undef RT_OCC
+        if (mb && (e = mb->mark(sb, kKfOcclusion)) != hipSuccess) return e;
     }
-    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, s, sc, fp, b, k);
-    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, s, sc, fp, b, k);
-    return m ? m->mark(s, kKfShade) : hipSuccess;
+    if (fused) return hipSuccess;
+    if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, sb, sc, fp, b, k);
+    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, sb, sc, fp, b, k);
+    return mb ? mb->mark(sb, kKfShade) : hipSuccess;
 }
 
 // One chunk (fp.row0, fp.rows) through every generation.  src: the sphere
 // source of the nearest-hit kernel (kSrc*), src_occ: of the shadow kernel;
-// count: instrumented kernels; mark is recorded on s after generation
-// mark_gen has been launched (chunk pipelining across streams); marks (may
-// be null): per-launch timing events, started by the caller.
+// count: instrumented kernels; mark is recorded on stream a after generation
+// mark_gen has been launched (chunk pipelining across lanes).  The nearest-hit
+// chain runs on ws.a, the shadow + shading kernels of each generation on ws.b
+// streams (each waiting for its generation's nearest-hit kernel); the fold
+// waits for all of them.
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
-                            bool count, hipStream_t s, hipEvent_t mark, int mark_gen, LaunchMarks* marks) {
+                            bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
     for (int k = 0; k < gens; ++k) {
         hipError_t e;
-#define RT_GEN(N, O) e = (count ? launch_generation<N, O, true>(sc, fp, b, k, s, marks) \
-                                : launch_generation<N, O, false>(sc, fp, b, k, s, marks))
+#define RT_GEN(N, O) e = (count ? launch_generation<N, O, true>(sc, fp, b, k, ws) \
+                                : launch_generation<N, O, false>(sc, fp, b, k, ws))
         const int combo = src * 100 + src_occ;
         switch (combo) {
         case kSrcGlobal * 101: RT_GEN(kSrcGlobal, kSrcGlobal); break;
@@ -733,13 +795,21 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
 #undef RT_GEN
         if (e != hipSuccess) return e;
         if (mark && k == mark_gen) {
-            e = hipEventRecord(mark, s);
+            e = hipEventRecord(mark, ws.a);
             if (e != hipSuccess) return e;
         }
     }
+    hipError_t e;
+    for (int i = 0; i < ws.nb; ++i) {
+        if (ws.b[i] == ws.a) continue;
+        if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
+    }
+    const hipStream_t s = ws.a;
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
     const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
+    if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
     // the Fresnel-capable fold costs registers; scenes without FresnelMaterial use the plain one
     if (sc.has_fresnel) {
         if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
@@ -748,11 +818,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         if (staged) hipLaunchKernelGGL((wf_fold<true, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
         else hipLaunchKernelGGL((wf_fold<false, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
     }
-    hipError_t e = marks ? marks->mark(s, kKfFold) : hipSuccess;
-    if (e != hipSuccess) return e;
+    if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
+    if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);
-    e = marks ? marks->mark(s, kKfTally) : hipSuccess;
-    if (e != hipSuccess) return e;
+    if (ws.ma && (e = ws.ma->mark(s, kKfTally)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -1,18 +1,27 @@
 """Per-launch timeline of the last uninstrumented wavefront frame of a
-rocprofv3 --kernel-trace run (directory argument)."""
+rocprofv3 --kernel-trace run (directory argument): start (us from the frame's
+first launch), duration (us), stream, kernel."""
 import csv
 import sys
 
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
 tr = list(csv.DictReader(open(f"{d}/run_kernel_trace.csv")))
 tr.sort(key=lambda t: int(t["Start_Timestamp"]))
-starts = [i for i, t in enumerate(tr) if "wf_nearest" in t["Kernel_Name"] and ", true, false>" in t["Kernel_Name"]]
+
+
+def targs(name):
+    return [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")] if "<" in name else []
+
+
+# generation 0 of an uninstrumented frame: wf_nearest<src, kCam = true, kCount = false, ...>
+starts = [i for i, t in enumerate(tr) if "wf_nearest<" in t["Kernel_Name"] and targs(t["Kernel_Name"])[1:3] == ["true", "false"]]
 i0 = starts[-1]
 t0 = int(tr[i0]["Start_Timestamp"])
 for t in tr[i0:]:
     s = (int(t["Start_Timestamp"]) - t0) / 1e3
     dur = (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3
     name = t["Kernel_Name"].replace("rtamd::(anonymous namespace)::", "").split("(")[0].replace("void ", "")
-    print(f"{s:8.1f} {dur:8.1f}  {name}")
+    q = t.get("Stream_Id") or t.get("Queue_Id") or ""
+    print(f"{s:8.1f} {dur:8.1f}  {q:>3}  {name}")
     if "wf_tally" in name:
         break

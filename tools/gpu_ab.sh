@@ -15,7 +15,7 @@ for v in ${VARIANTS:-default:X=1}; do
         -k "config3 or axis_aligned or extreme or ten_thousand or bit_for_bit or golden" > gpurun_out/vtest_$name.log 2>&1
     rc=$?; echo "vtests $name rc=$rc: $(tail -1 gpurun_out/vtest_$name.log)"; if [ $rc -gt 1 ]; then exit $rc; fi
   fi
-  env $envs timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu > gpurun_out/bench_$name.log 2>&1
+  env $envs timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu ${BENCH_EXTRA:-} > gpurun_out/bench_$name.log 2>&1
   rc=$?; echo "bench $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/bench_$name.log; exit $rc; fi
   python -c "import json,sys; d=json.loads(open('gpurun_out/bench_$name.log').read().strip().splitlines()[-1]); print('$name', d['value'], 'Mrays/s', d['ms_per_step'], 'ms')"

@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-kernel-times", action="store_true",
-                   help="do not record HIP events between the launches of the timed frames")
+                   help="skip the instrumented frames that time every launch with HIP events")
     return p.parse_args()
 
 
@@ -119,9 +119,10 @@ def main():
     # torch events below bracket the kernel (handle 0 would select the context's own stream)
     stream = torch.cuda.Stream(dev)
 
-    # timed frames also record a HIP event after every launch (RT_TIME_KERNELS):
-    # per-kernel-family launch durations over exactly the timed region
-    timed_flags = opts.flags | (0 if args.no_kernel_times else lr.RT_TIME_KERNELS)
+    # per-kernel-family launch durations come from K more frames that record HIP
+    # events around every launch (RT_TIME_KERNELS), after the timed region: the
+    # events sit between launches on both streams and would perturb the timing
+    timed_flags = opts.flags | lr.RT_TIME_KERNELS
     opts_timed = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
                                 max_depth=args.depth, spp=1, algo=algo, flags=timed_flags)
 
@@ -142,7 +143,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        step(opts_timed)
+        step()
         evs[i][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -150,7 +151,12 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    ktimes = ctx.kernel_times()            # {family: (ms summed over the K timed frames, launches)}
+    ktimes = {}
+    if not args.no_kernel_times:
+        for _ in range(args.steps):
+            step(opts_timed)
+        torch.cuda.synchronize(dev)
+        ktimes = ctx.kernel_times()        # {family: (ms summed over K instrumented frames, launches)}
 
     # one more, untimed frame with the instrumented kernels: exact box / sphere test counts
     work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
@@ -201,8 +207,7 @@ def main():
             if n:
                 kernels["wf_" + fam] = {"avg_launch_us": round(ms / n * 1e3, 2),
                                         "launches_per_frame": round(n / args.steps, 2),
-                                        "ms_per_frame": round(ms / args.steps, 4),
-                                        "share_of_frame": round(ms / args.steps / avg_kernel_ms, 4)}
+                                        "ms_per_frame": round(ms / args.steps, 4)}
         dominant = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else None
         line = {
             "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",

@@ -31,4 +31,8 @@ struct Bvh4Result {
 };
 Bvh4Result collapse_bvh4(const BvhResult& b2);
 
+// Camera view of every node of a binary BVH (DevCamNode) for a camera at
+// `pos` with direction matrix `m` (row-major, camera.rs:57-61).
+std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]);
+
 }  // namespace rtamd

@@ -55,6 +55,21 @@ struct alignas(16) DevBvhNode {
 };
 static_assert(sizeof(DevBvhNode) == 64, "BVH node is one 64-B line");
 
+// Camera view of one binary BVH node, for the generation-0 tile traversal:
+// every camera ray starts at the camera position, so a child box maps to a
+// conservative rectangle of image-plane coordinates (px, py) -- the (px, py)
+// of main.rs:50-53 / camera.rs:78 -- outside which no camera ray can report a
+// hit inside the box, and to a lower bound on the t of any such hit.  Rects
+// are rounded outward to f32 (+-inf when the box reaches behind the camera
+// plane); tmin is rounded down.  Same index and child pointers as DevBvhNode.
+struct alignas(16) DevCamNode {
+    float r0[4];                    // child 0: px_lo, py_lo, px_hi, py_hi
+    float r1[4];                    // child 1
+    float tmin0, tmin1;
+    int32_t c0, c1;
+};
+static_assert(sizeof(DevCamNode) == 48, "camera node is 48 B");
+
 // 4-wide BVH, plane-major: node i's child boxes and pointers are 7 16-byte
 // planes, plane k at index k * n_nodes + i (lo.x, hi.x, lo.y, hi.y, lo.z,
 // hi.z of the 4 children, then the 4 child pointers).  A wave's lanes reading
@@ -82,6 +97,7 @@ struct DevScene {
     int32_t n_spheres, n_planes, n_lights, n_bvh;
     const DevBvh4Plane* bvh4;       // the same tree collapsed 4-wide (DevBvh4Plane)
     int32_t bvh4_root, n_bvh4;
+    const DevCamNode* cam_nodes;    // camera view of the binary BVH (null: generation 0 traverses per ray)
     int32_t has_fresnel;            // some object uses FresnelMaterial
     double cam_pos[3];
     double cam_m[9];                // row-major

@@ -261,4 +261,73 @@ Bvh4Result collapse_bvh4(const BvhResult& b2) {
     return out;
 }
 
+// Image-plane rectangle of a box seen from the camera.  A camera ray is
+// dir = normalize(M (px, py, 1)) (camera.rs:78), so a world point X it passes
+// through has M^-1 (X - pos) = s (px, py, 1) with s > 0.  When every corner of
+// the box lies strictly in front of the camera plane (third coordinate > 0),
+// the box's image is the convex hull of the corner images (the perspective map
+// keeps segments straight on that side), so their bounding rectangle holds
+// every (px, py) whose ray meets the box.  A relative 1e-5 margin absorbs the
+// rounding of the ray direction and of this projection (far below a pixel).
+namespace {
+void project_box(const float lo[3], const float hi[3], const double pos[3], const double inv[9], float rect[4],
+                 float& tmin) {
+    double r[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    bool front = true;
+    for (int c = 0; c < 8 && front; ++c) {
+        const double X[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+        const double d[3] = {X[0] - pos[0], X[1] - pos[1], X[2] - pos[2]};
+        double q[3];
+        for (int i = 0; i < 3; ++i) q[i] = inv[3 * i] * d[0] + inv[3 * i + 1] * d[1] + inv[3 * i + 2] * d[2];
+        const double dn = std::fabs(d[0]) + std::fabs(d[1]) + std::fabs(d[2]);
+        if (!(q[2] > 1e-9 * dn) || !std::isfinite(q[0]) || !std::isfinite(q[1])) { front = false; break; }
+        const double px = q[0] / q[2], py = q[1] / q[2];
+        r[0] = std::min(r[0], px); r[1] = std::min(r[1], py);
+        r[2] = std::max(r[2], px); r[3] = std::max(r[3], py);
+    }
+    if (!front) {
+        rect[0] = rect[1] = -HUGE_VALF;
+        rect[2] = rect[3] = HUGE_VALF;
+    } else {
+        for (int i = 0; i < 2; ++i) rect[i] = down(r[i] - 1e-5 * (1.0 + std::fabs(r[i])));
+        for (int i = 2; i < 4; ++i) rect[i] = up(r[i] + 1e-5 * (1.0 + std::fabs(r[i])));
+    }
+    // distance from the camera to the box: a hit inside it is at t >= this
+    // (unit direction up to rounding; the 1e-6 relative cut covers that)
+    double dd = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double v = pos[a] < lo[a] ? lo[a] - pos[a] : (pos[a] > hi[a] ? pos[a] - hi[a] : 0.0);
+        dd += v * v;
+    }
+    const double dist = std::sqrt(dd) * (1.0 - 1e-6);
+    tmin = std::isfinite(dist) ? down(dist) : 0.0f;
+}
+}  // namespace
+
+std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]) {
+    std::vector<DevCamNode> out(b2.nodes.size());
+    // M^-1 by the adjugate
+    const double a = m[0], b = m[1], c = m[2], d = m[3], e = m[4], f = m[5], g = m[6], h = m[7], i = m[8];
+    const double det = a * (e * i - f * h) - b * (d * i - f * g) + c * (d * h - e * g);
+    const double inv[9] = {(e * i - f * h) / det, (c * h - b * i) / det, (b * f - c * e) / det,
+                           (f * g - d * i) / det, (a * i - c * g) / det, (c * d - a * f) / det,
+                           (d * h - e * g) / det, (b * g - a * h) / det, (a * e - b * d) / det};
+    bool ok = std::isfinite(det) && det != 0.0;
+    for (double v : inv) ok = ok && std::isfinite(v);
+    for (size_t k = 0; k < b2.nodes.size(); ++k) {
+        const DevBvhNode& n = b2.nodes[k];
+        DevCamNode& o = out[k];
+        if (ok) {
+            project_box(n.lo0, n.hi0, pos, inv, o.r0, o.tmin0);
+            project_box(n.lo1, n.hi1, pos, inv, o.r1, o.tmin1);
+        } else {                                  // degenerate camera: every box everywhere
+            for (float* r : {o.r0, o.r1}) { r[0] = r[1] = -HUGE_VALF; r[2] = r[3] = HUGE_VALF; }
+            o.tmin0 = o.tmin1 = 0.0f;
+        }
+        o.c0 = n.c0;
+        o.c1 = n.c1;
+    }
+    return out;
+}
+
 }  // namespace rtamd

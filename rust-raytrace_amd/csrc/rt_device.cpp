@@ -325,6 +325,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (leaf_env <= 0 && bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
         bvh = build_sphere_bvh(sx, sy, sz, srad, pad, 4);
     const Bvh4Result bvh4 = collapse_bvh4(bvh);
+    const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
     {
         std::vector<DevSphere> s2(spheres.size());
         std::vector<int32_t> o2(spheres.size());
@@ -343,6 +344,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_li = place(lights.size() * sizeof(DevLight));
     const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
     const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
+    const size_t o_cam = place(camn.size() * sizeof(DevCamNode));
     const size_t total = off ? off : 256;
     std::vector<uint8_t> host(total, 0);
     auto put = [&](size_t at, const void* p, size_t bytes) { if (bytes) std::memcpy(host.data() + at, p, bytes); };
@@ -354,6 +356,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_li, lights.data(), lights.size() * sizeof(DevLight));
     put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
     put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
+    put(o_cam, camn.data(), camn.size() * sizeof(DevCamNode));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
     if (!c->d_blob) {
@@ -379,6 +382,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.bvh4 = reinterpret_cast<const DevBvh4Plane*>(base + o_bvh4);
     d.bvh4_root = bvh4.root;
     d.n_bvh4 = bvh4.n_nodes;
+    d.cam_nodes = reinterpret_cast<const DevCamNode*>(base + o_cam);
     d.has_fresnel = 0;
     for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
@@ -516,6 +520,16 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const bool split = env_int("RT_WF_SPLIT", 1) != 0;
         const int n_b = std::max(1, std::min(kMaxBStreams, env_int("RT_WF_BSTREAMS", 1)));
         const bool fuse = env_int("RT_WF_FUSE", 1) != 0;
+        // generation 0 by camera tile (RT_WF_CAM=0: per-ray like the other generations);
+        // only with the binary-tree sources, whose node order the camera view shares
+        int cam = 0;
+        if (src == 2 || src == 4 || src == 7) {
+            const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
+            cam = cam_lds <= kLdsBudget ? 1 : 2;
+            const int ce = env_int("RT_WF_CAM", -1);
+            if (ce == 0) cam = 0;
+            else if (ce == 2) cam = 2;
+        }
         const uint32_t wg_major = env_int("RT_WF_DEAL", 1) != 0 ? 1u : 0u;
         for (int l = 0; l < n_lanes; ++l) {
             if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
@@ -560,6 +574,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             ws.near_done = L.near_done.data();
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
+            ws.cam = cam;
             HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, ws, L.mark, mark_gen));
         }
         for (int l = 0; l < n_lanes; ++l) {

@@ -250,6 +250,8 @@ struct BvhView {
     const int32_t* obj;
     const DevBvh4Plane* p4;      // 4-wide tree planes (LDS or HBM), stride n4
     int32_t n4;
+    const DevCamNode* cn;        // camera view of the binary tree (LDS or HBM)
+    int32_t* stk;                // this wave's LDS traversal stack (camera sources)
 };
 
 // kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS
@@ -576,6 +578,65 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
         }
         if (stk_n == 0) return false;
         cur = stk_pop();
+    }
+}
+
+// ---- generation 0: camera rays by 8x8 tile -----------------------------
+// Every camera ray starts at the camera, so the wave's 64 rays of one pixel
+// tile share a rectangle of image-plane coordinates [tx0, tx1] x [ty0, ty1]
+// (the px, py of main.rs:50-53).  The wave walks the camera view of the binary
+// BVH (DevCamNode) with ONE wave-uniform stack in LDS: a child is entered when
+// its image rectangle overlaps the tile's and some lane's current best t is
+// not below the child's distance bound.  The tree is only a filter; every
+// lane tests every sphere of an entered leaf with the exact f64 quadratic and
+// keeps the (t, object id) minimum, so the result is the linear scan's
+// ("BVH exactness": a reported hit point lies in its padded box,
+// hence its image in the box's rectangle, hence its pixel's (px, py) within
+// the tile's rectangle).  Lanes with `act` = false (no pixel, or a NaN plane
+// hit, which wins outright) only ride along.
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_camera(const DevScene& sc, const BvhView& v, const Ray& r, bool act, float tx0,
+                                              float ty0, float tx1, float ty1, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    const bool go = act && !h.nan_t;
+    if (sc.n_spheres == 0 || __ballot(go) == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    int32_t* stk = v.stk;
+    int sp = 0;
+    int32_t cur = sc.bvh_root;
+    for (;;) {
+        if (cur >= 0) {
+            const DevCamNode n = v.cn[cur];
+            if constexpr (kCount) w->boxes += go ? 2 : 0;
+            const bool o0 = !(n.r0[2] < tx0 || n.r0[0] > tx1 || n.r0[3] < ty0 || n.r0[1] > ty1);
+            const bool o1 = !(n.r1[2] < tx0 || n.r1[0] > tx1 || n.r1[3] < ty0 || n.r1[1] > ty1);
+            // a lane can still gain from a child unless its best t is below the child's bound
+            const bool e0 = __ballot(go && o0 && !(static_cast<double>(n.tmin0) > h.t)) != 0;
+            const bool e1 = __ballot(go && o1 && !(static_cast<double>(n.tmin1) > h.t)) != 0;
+            const int32_t c0 = __builtin_amdgcn_readfirstlane(n.c0), c1 = __builtin_amdgcn_readfirstlane(n.c1);
+            if (e0 && e1) {
+                const bool first0 = __builtin_amdgcn_readfirstlane(n.tmin0 <= n.tmin1);   // nearer child first
+                stk[sp++] = first0 ? c1 : c0;
+                cur = first0 ? c0 : c1;
+                continue;
+            }
+            if (e0) { cur = c0; continue; }
+            if (e1) { cur = c1; continue; }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += go ? cnt : 0;
+            for (int k = first; k < first + cnt; ++k) {
+                const DevSphere s = v.sph[k];
+                double t;
+                if (go && sphere_t(s, r, a2, a4, t)) {
+                    const int32_t obj = v.obj[k];
+                    if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = k; }
+                }
+            }
+        }
+        if (sp == 0) return h;
+        cur = __builtin_amdgcn_readfirstlane(stk[--sp]);
     }
 }
 

@@ -226,6 +226,25 @@ __device__ __forceinline__ bool slot_pixel(const WfBufs& b, const FrameParams& f
     return lx < fp.tile_w && ly < fp.rows;
 }
 
+// Image-plane rectangle (f32, rounded outward) of the live pixels of
+// generation-0 tile `tile`: px grows with x and py with the frame row, which
+// grows with the local row for any band layout (camera_ray's mapping).
+__device__ __forceinline__ void tile_rect(const FrameParams& fp, const WfBufs& b, uint32_t tile, float& tx0, float& ty0,
+                                          float& tx1, float& ty1) {
+    const uint32_t xa = (tile % b.tiles_x) * 8u, la = (tile / b.tiles_x) * 8u;
+    const uint32_t xb = min(xa + 7u, fp.tile_w - 1u), lb = min(la + 7u, fp.rows - 1u);
+    auto row = [&](uint32_t l) {
+        const uint32_t lr = fp.row0 + l;
+        return fp.y0 + ((lr / fp.band) * fp.band_stride + fp.band_phase) * fp.band + lr % fp.band;
+    };
+    const double px0 = ((static_cast<double>(fp.x0 + xa) + 0.5) - fp.hw) * fp.scale;
+    const double px1 = ((static_cast<double>(fp.x0 + xb) + 0.5) - fp.hw) * fp.scale;
+    const double py0 = ((static_cast<double>(row(la)) + 0.5) - fp.hh) * fp.scale;
+    const double py1 = ((static_cast<double>(row(lb)) + 0.5) - fp.hh) * fp.scale;
+    tx0 = __double2float_rd(px0); tx1 = __double2float_ru(px1);
+    ty0 = __double2float_rd(py0); ty1 = __double2float_ru(py1);
+}
+
 __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
     return Ray{b.qo[q][0][i], b.qo[q][1][i], b.qo[q][2][i], b.qd[q][0][i], b.qd[q][1][i], b.qd[q][2][i]};
 }
@@ -239,25 +258,36 @@ constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-threa
 constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
 constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
 constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
+// Generation 0 only: camera rays by 8x8 tile, a wave-uniform traversal of the
+// binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
+constexpr int kSrcCamL = 20;        // camera nodes + spheres in LDS
+constexpr int kSrcCamG = 21;        // camera nodes + spheres from HBM/L2
 
 template <int kSrc>
 struct Src {
+    static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
     static constexpr bool bvh = kSrc >= kSrcBvhG;
-    static constexpr bool wide = kSrc >= kSrcBvh4L;
-    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4;
+    static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4L4;
+    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
+                                    kSrc == kSrcCamL;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds;
     static constexpr int nodes = all_lds ? 2 : 0;
     static constexpr int waves = kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 ? 8 : 4;   // min waves per SIMD
 };
+
+// Per-wave traversal stack of the camera sources (wave-uniform entries).
+constexpr int kCamStack = 64;
 
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
     if (Src<kSrc>::nodes > 0)
-        bytes = Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
-                                : static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
+        bytes += Src<kSrc>::cam    ? static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode)
+                 : Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
+                                   : static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     return (bytes + 15) / 16 * 16;
 }
@@ -267,9 +297,18 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
 template <int kSrc>
 __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4};
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, sc.cam_nodes, nullptr};
     size_t off = 0;
-    if constexpr (kSrc == kSrcLds) {
+    if constexpr (Src<kSrc>::cam) {
+        v.stk = reinterpret_cast<int32_t*>(lds) + (threadIdx.x >> 6) * kCamStack;
+        off = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
+        if constexpr (Src<kSrc>::nodes > 0) {
+            DevCamNode* lc = reinterpret_cast<DevCamNode*>(lds + off);
+            for (int i = threadIdx.x; i < sc.n_bvh; i += T) lc[i] = sc.cam_nodes[i];
+            v.cn = lc;
+            off += static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode);
+        }
+    } else if constexpr (kSrc == kSrcLds) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
@@ -374,6 +413,68 @@ __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
 
 __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + 2) * 4u; }
 
+// What follows a nearest hit (all 64 lanes call it; `live` lanes carry a
+// query): a miss or a cut-off ends the chain at once (terminal colour; a
+// camera miss writes its final pixel); a lit hit becomes a shade record of
+// generation k, and a specular one also queues its reflection ray in Q_{k+1}.
+// counts[0..1]: this workgroup's LDS append counters (records, rays).
+template <bool kCam, bool kFresnel>
+__device__ __forceinline__ void finish_nearest(const DevScene& sc, const FrameParams& fp, const WfBufs& b,
+                                               const DevSphere* sph, int k, bool live, const Ray& r, double sig,
+                                               uint32_t p, const Hit& h, uint32_t* counts, size_t obase, size_t rbase) {
+    bool shade = false, refl = false;
+    double ptx = 0.0, pty = 0.0, ptz = 0.0, nsig = 0.0;
+    Ray rr{};
+    if (live) {
+        if (h.obj == INT32_MAX) {                                           // raytrace.rs:265, 228-232
+            if constexpr (kCam) write_background_pixel(fp, b, p);          // no levels: final now
+            else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
+        } else {
+            const DevMaterial& m = sc.mats[h.obj];
+            if (static_cast<uint32_t>(k) > fp.max_depth) {                  // raytrace.rs:33 / 126
+                set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+            } else {
+                ptx = r.ox + r.dx * h.t; pty = r.oy + r.dy * h.t; ptz = r.oz + r.dz * h.t;   // ray.cast(t)
+                double nx, ny, nz;
+                hit_normal(sc, sph, h.prim, ptx, pty, ptz, nx, ny, nz);
+                const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
+                const Shading sh = shading_flags<kFresnel>(m, sig, nd);
+                if (!sh.diffuse && !sh.specular) {
+                    set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+                } else {
+                    shade = true;
+                    if (sh.specular) {                                      // raytrace.rs:58-64 / 159-164
+                        if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
+                        rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
+                        nsig = (sh.f * sig) * m.ks_sig;
+                        refl = true;
+                    }
+                }
+            }
+        }
+    }
+    const uint32_t slot = lds_append(&counts[0], shade);
+    if (shade) {
+        const size_t at = rbase + slot;
+        b.sr_pt[0][at] = ptx; b.sr_pt[1][at] = pty; b.sr_pt[2][at] = ptz;
+        b.sr_d[0][at] = r.dx; b.sr_d[1][at] = r.dy; b.sr_d[2][at] = r.dz;
+        b.sr_sig[at] = sig;
+        b.sr_obj[at] = h.obj;
+        b.sr_prim[at] = h.prim;
+        b.sr_pix[at] = p;
+        b.occ[at] = 0u;
+    }
+    const uint32_t rslot = lds_append(&counts[1], refl);
+    if (refl) {
+        const int qn = (k + 1) & 1;
+        const size_t at = obase + rslot;
+        b.qo[qn][0][at] = rr.ox; b.qo[qn][1][at] = rr.oy; b.qo[qn][2][at] = rr.oz;
+        b.qd[qn][0][at] = rr.dx; b.qd[qn][1][at] = rr.dy; b.qd[qn][2][at] = rr.dz;
+        b.qsig[qn][at] = nsig;
+        b.qpix[qn][at] = p;
+    }
+}
+
 // Scene::intersect for every ray of Q_k (generation 0: the camera rays of the
 // chunk, computed here).  Outcomes that end the chain without lighting are
 // resolved on the spot (miss -> background; depth cut-off or insignificant
@@ -401,14 +502,11 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();                                       // publishes the LDS staging and counters
     Work w;
-    const int qn = (k + 1) & 1;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
     const size_t rbase = static_cast<size_t>(k) * b.rstride + obase;
     RT_FOR_CHUNKS(b, n, j) {
-        bool shade = false, refl = false;
         Ray r{};
-        double sig = 0.0, ptx = 0.0, pty = 0.0, ptz = 0.0, nsig = 0.0;
-        Ray rr{};
+        double sig = 0.0;
         uint32_t p = 0;
         Hit h{};
         bool live = false;
@@ -429,54 +527,15 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
                 live = true;
             }
         }
+        if constexpr (Src<kSrc>::cam) {                 // whole wave: one pixel tile
+            float tx0, ty0, tx1, ty1;
+            tile_rect(fp, b, j >> 6, tx0, ty0, tx1, ty1);
+            h = nearest_camera<kCount>(sc, v, r, live, tx0, ty0, tx1, ty1, &w);
+        }
         if (live) {
-            h = nearest_any<kSrc, kCount>(sc, v, r, &w);
-            if (h.obj == INT32_MAX) {                                           // raytrace.rs:265, 228-232
-                if constexpr (kCam) write_background_pixel(fp, b, p);          // no levels: final now
-                else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
-            } else {
-                const DevMaterial& m = sc.mats[h.obj];
-                if (static_cast<uint32_t>(k) > fp.max_depth) {                  // raytrace.rs:33 / 126
-                    set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
-                } else {
-                    ptx = r.ox + r.dx * h.t; pty = r.oy + r.dy * h.t; ptz = r.oz + r.dz * h.t;   // ray.cast(t)
-                    double nx, ny, nz;
-                    hit_normal(sc, v.sph, h.prim, ptx, pty, ptz, nx, ny, nz);
-                    const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
-                    const Shading sh = shading_flags<kFresnel>(m, sig, nd);
-                    if (!sh.diffuse && !sh.specular) {
-                        set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
-                    } else {
-                        shade = true;
-                        if (sh.specular) {                                      // raytrace.rs:58-64 / 159-164
-                            if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }
-                            rr = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
-                            nsig = (sh.f * sig) * m.ks_sig;
-                            refl = true;
-                        }
-                    }
-                }
-            }
+            if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         }
-        const uint32_t slot = lds_append(&ql.count[0], shade);
-        if (shade) {
-            const size_t at = rbase + slot;
-            b.sr_pt[0][at] = ptx; b.sr_pt[1][at] = pty; b.sr_pt[2][at] = ptz;
-            b.sr_d[0][at] = r.dx; b.sr_d[1][at] = r.dy; b.sr_d[2][at] = r.dz;
-            b.sr_sig[at] = sig;
-            b.sr_obj[at] = h.obj;
-            b.sr_prim[at] = h.prim;
-            b.sr_pix[at] = p;
-            b.occ[at] = 0u;
-        }
-        const uint32_t rslot = lds_append(&ql.count[1], refl);
-        if (refl) {
-            const size_t at = obase + rslot;
-            b.qo[qn][0][at] = rr.ox; b.qo[qn][1][at] = rr.oy; b.qo[qn][2][at] = rr.oz;
-            b.qd[qn][0][at] = rr.dx; b.qd[qn][1][at] = rr.dy; b.qd[qn][2][at] = rr.dz;
-            b.qsig[qn][at] = nsig;
-            b.qpix[qn][at] = p;
-        }
+        finish_nearest<kCam, kFresnel>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -529,6 +588,20 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
 constexpr int kOccCount = 24;
 constexpr int kMaxFusedLights = 24;
 
+// Record the answer of shadow query (record at, light l); kShade: the query
+// that completes the record's light count shades it.
+template <bool kShade, bool kFresnel>
+__device__ __forceinline__ void occlusion_done(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t l,
+                                               uint32_t L, bool occluded) {
+    if constexpr (kShade) {
+        const uint32_t inc = (occluded ? 1u << l : 0u) + (1u << kOccCount);
+        const uint32_t now = atomicAdd(&b.occ[at], inc) + inc;
+        if ((now >> kOccCount) == L) shade_record<kFresnel>(sc, b, k, at, now & ((1u << kOccCount) - 1u));
+    } else {
+        if (occluded) atomicOr(&b.occ[at], 1u << l);
+    }
+}
+
 // The shadow queries of every shade record of generation k (raytrace.rs:39-49):
 // one work-item per (record, light) pair -- the lights of one hit are
 // independent queries -- setting bit l of the record's occlusion mask
@@ -557,13 +630,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
         const int32_t hint = b.sr_prim[at];
         const bool occluded = occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
-        if constexpr (kShade) {
-            const uint32_t inc = (occluded ? 1u << l : 0u) + (1u << kOccCount);
-            const uint32_t now = atomicAdd(&b.occ[at], inc) + inc;
-            if ((now >> kOccCount) == L) shade_record<kFresnel>(sc, b, k, at, now & ((1u << kOccCount) - 1u));
-        } else {
-            if (occluded) atomicOr(&b.occ[at], 1u << l);
-        }
+        occlusion_done<kShade, kFresnel>(sc, b, k, at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
 }
@@ -728,13 +795,19 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
     hipError_t e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
-#define RT_NEAR(CAM, FR) hipLaunchKernelGGL((wf_nearest<kSrcN, CAM, kCount, FR>), grid, block, lds_n, ws.a, sc, fp, b, k)
-    if (sc.has_fresnel) {
-        if (k == 0) RT_NEAR(true, true); else RT_NEAR(false, true);
+#define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR>), grid, block, \
+                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+    if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
+        if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
+    } else if (k == 0 && ws.cam == 2) {
+        if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
+    } else if (sc.has_fresnel) {
+        if (k == 0) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, false, true);
     } else {
-        if (k == 0) RT_NEAR(true, false); else RT_NEAR(false, false);
+        if (k == 0) RT_NEAR(kSrcN, true, false); else RT_NEAR(kSrcN, false, false);
     }
 #undef RT_NEAR
+    (void)lds_n;
     e = ws.ma ? ws.ma->mark(ws.a, kKfNearest) : hipSuccess;
     if (e != hipSuccess) return e;
     if (static_cast<uint32_t>(k) > fp.max_depth) return hipSuccess;     // no shade records past the cut-off
@@ -751,11 +824,13 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (sc.n_lights > 0) {
         const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
         if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-#define RT_OCC(SH, FR) hipLaunchKernelGGL((wf_occlusion<kSrcO, kCount, SH, FR>), grid, block, lds_o, sb, sc, fp, b, k)
-        if (!fused) RT_OCC(false, false);
-        else if (sc.has_fresnel) RT_OCC(true, true);
-        else RT_OCC(true, false);
+#define RT_OCC(S, SH, FR) hipLaunchKernelGGL((wf_occlusion<S, kCount, SH, FR>), grid, block, \
+                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), sb, sc, fp, b, k)
+        if (!fused) RT_OCC(kSrcO, false, false);
+        else if (sc.has_fresnel) RT_OCC(kSrcO, true, true);
+        else RT_OCC(kSrcO, true, false);
 #undef RT_OCC
+        (void)lds_o;
         if (mb && (e = mb->mark(sb, kKfOcclusion)) != hipSuccess) return e;
     }
     if (fused) return hipSuccess;

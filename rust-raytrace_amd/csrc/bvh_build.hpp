@@ -31,6 +31,12 @@ struct Bvh4Result {
 };
 Bvh4Result collapse_bvh4(const BvhResult& b2);
 
+// Worst-case traversal stack depth of a 4-wide tree: the largest sum, over
+// the nodes of a root-to-leaf path, of (children - 1) pending siblings, + 1.
+int bvh4_stack_need(const Bvh4Result& b4);
+// Depth of a binary tree (its traversal pushes at most one entry per level).
+int bvh_depth(const BvhResult& b2);
+
 // Camera view of every node of a binary BVH (DevCamNode) for a camera at
 // `pos` with direction matrix `m` (row-major, camera.rs:57-61).
 std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]);

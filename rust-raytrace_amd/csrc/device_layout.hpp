@@ -120,45 +120,83 @@ struct FrameParams {
 
 constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (camera ray missed)
 
-// Wavefront working set for one chunk of a tile (all in HBM; sized by the
-// host for `cap` pixels / `slots` generation-0 slots; 288 GB leaves room).
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__
+#else
+#define RT_HD
+#endif
+
+// Wavefront working set for one chunk of a tile (HBM; sized by the host for
+// `cap` pixels / `slots` generation-0 slots; 288 GB leaves room).
 // Generation k = recursion depth k (raytrace.rs:33,63): queue Q_k holds the
 // rays ray_color is called with at depth k.
+//
+// ONE allocation, addressed by offsets: a kernel keeps one base pointer and a
+// few sizes live instead of ~40 array pointers (which the compiler holds in
+// SGPRs and spills into the traversal loop's VGPRs).  Sections, each an SoA
+// of arrays:
+//   queues   [parity 2][field 8][qcap]: origin x,y,z, direction x,y,z,
+//            significance (f64), owning pixel (u32 in an 8-B slot); queues
+//            ping-pong by generation parity;
+//   records  shade records, f64 fields [7][levels*qcap] (hit point x,y,z,
+//            incoming direction x,y,z, significance) then u32 fields
+//            [4][levels*qcap] (object id, primitive: sphere >= 0 / ~plane,
+//            pixel, occlusion mask: bit l = light l shadowed, bits 24.. = lights
+//            decided).  One region array per generation (generation k at
+//            k*qcap), so the nearest-hit kernels never wait for the shadow /
+//            shading kernels of earlier generations (the other stream);
+//   levels   per-level local colour r,g,b and Schlick factor (f64)
+//            [4][levels*capa], then object id (i32) [levels*capa]; [k*capa + p];
+//   term     terminal colour of each pixel's chain [3][capa] (f64), then nlev
+//            (u8, levels pushed, kNlevDone = written by wf_nearest) [capa];
+//   rq / rs  [k*G + r]: entries of region r of Q_k / of generation k's records;
+//   oq / ro  shadow item lists (nlists > 0): for generation k and light l the
+//            records whose query toward l needs the sphere traversal; list
+//            n_lights = records with nothing left to trace.  Entry = record
+//            index within generation k; [(k*nlists + list)*qcap + entry] and
+//            region sizes [(k*nlists + list)*G + r].
+// Queue, record and list arrays are G regions of R entries (qcap = G*R); region
+// r is written only by workgroup r of the producing kernel.
 struct WfBufs {
-    double* qo[2][3];               // ray origin x,y,z  (queues ping-pong by generation parity)
-    double* qd[2][3];               // ray direction
-    double* qsig[2];                // significance passed down (raytrace.rs:63)
-    uint32_t* qpix[2];              // owning pixel (chunk-local index)
-    // Shade records: the hits that go on to light evaluation and/or
-    // reflection, in the same block-partitioned layout as the queues, one
-    // record buffer PER GENERATION (generation k at offset k * rstride), so
-    // the nearest-hit kernels never wait for the shadow / shading kernels of
-    // earlier generations (which run on a second stream).
-    double* sr_pt[3];               // hit point ray.cast(t)
-    double* sr_d[3];                // incoming direction
-    double* sr_sig;                 // significance
-    int32_t* sr_obj;                // object id
-    int32_t* sr_prim;               // sphere index >= 0, ~plane index < 0
-    uint32_t* sr_pix;               // owning pixel
-    uint32_t* occ;                  // per shade record: bit l set = light l shadowed
-    double* st[3];                  // per-level local colour, [level * cap + p]
-    int32_t* st_obj;                // per-level object id (its specular colour is the fold factor)
-    double* st_f;                   // per-level Schlick factor, written for FresnelMaterial levels only
-    double* term[3];                // terminal colour of each pixel's chain
-    uint8_t* nlev;                  // levels pushed per pixel
-    uint32_t* rq;                   // [k * G + r]: entries in region r of Q_k (written by its producer)
-    uint32_t* rs;                   // [k * G + r]: shade records in region r of generation k
+    unsigned char* mem;
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
-    size_t rstride;                 // entries per generation of the shade-record arrays (= G * R)
-    uint32_t cap;                   // pixel capacity (stack stride)
+    uint64_t qcap;                  // G * R
+    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_oq, o_ro;   // byte offsets of the sections
+    uint32_t cap;                   // pixel capacity
+    uint32_t capa;                  // cap rounded up to 64 (stride of the per-pixel arrays)
+    uint32_t levels;                // record generations / stack levels (max_depth + 1)
+    uint32_t nlists;                // n_lights + 1, or 0 (no lists: the plain shadow kernel)
     uint32_t G;                     // regions per queue
     uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
     uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
+
+    // queues: f = 0..5 origin / direction, 6 significance
+    RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
+    RT_HD uint32_t* qpix(int q) const {
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + 7) * qcap);
+    }
+    // records (index = k * qcap + entry): f = 0..2 point, 3..5 direction, 6 significance
+    RT_HD uint64_t rn() const { return static_cast<uint64_t>(levels) * qcap; }
+    RT_HD double* rf(int f) const { return reinterpret_cast<double*>(mem + o_rec) + f * rn(); }
+    RT_HD uint32_t* ru(int f) const {             // 0 object, 1 primitive, 2 pixel, 3 occlusion
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<double*>(mem + o_rec) + 7 * rn()) + f * rn();
+    }
+    // levels (index = k * capa + p): f = 0..2 colour, 3 Schlick factor
+    RT_HD double* lf(int f) const { return reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(f) * levels * capa; }
+    RT_HD int32_t* lobj() const {
+        return reinterpret_cast<int32_t*>(reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(4) * levels * capa);
+    }
+    RT_HD double* term(int f) const { return reinterpret_cast<double*>(mem + o_term) + static_cast<uint64_t>(f) * capa; }
+    RT_HD uint8_t* nlev() const { return reinterpret_cast<uint8_t*>(reinterpret_cast<double*>(mem + o_term) + 3ull * capa); }
+    RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
+    RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
+    RT_HD uint32_t* oq() const { return reinterpret_cast<uint32_t*>(mem + o_oq); }
+    RT_HD uint32_t* ro() const { return reinterpret_cast<uint32_t*>(mem + o_ro); }
 };
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels

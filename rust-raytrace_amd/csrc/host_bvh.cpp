@@ -330,4 +330,37 @@ std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], c
     return out;
 }
 
+int bvh4_stack_need(const Bvh4Result& b4) {
+    if (b4.root < 0 || b4.n_nodes == 0) return 1;
+    const int N = b4.n_nodes;
+    int worst = 0;
+    std::vector<std::pair<int32_t, int>> todo{{b4.root, 0}};      // (node, pending siblings above it)
+    while (!todo.empty()) {
+        const auto [node, pend] = todo.back();
+        todo.pop_back();
+        const DevBvh4Plane& ch = b4.planes[static_cast<size_t>(6) * N + node];
+        int kids = 0;
+        for (int k = 0; k < 4; ++k) kids += ch.i[k] != kBvh4Empty ? 1 : 0;
+        const int here = pend + std::max(0, kids - 1);
+        worst = std::max(worst, here);
+        for (int k = 0; k < 4; ++k)
+            if (ch.i[k] != kBvh4Empty && ch.i[k] >= 0) todo.push_back({ch.i[k], here});
+    }
+    return worst + 1;
+}
+
+int bvh_depth(const BvhResult& b2) {
+    if (b2.root < 0 || b2.nodes.empty()) return 0;
+    int worst = 0;
+    std::vector<std::pair<int32_t, int>> todo{{b2.root, 1}};
+    while (!todo.empty()) {
+        const auto [node, d] = todo.back();
+        todo.pop_back();
+        worst = std::max(worst, d);
+        for (int32_t c : {b2.nodes[node].c0, b2.nodes[node].c1})
+            if (c >= 0) todo.push_back({c, d + 1});
+    }
+    return worst;
+}
+
 }  // namespace rtamd

@@ -28,6 +28,7 @@ struct rt_ctx {
     size_t blob_bytes = 0;
     DevScene dsc{};
     bool has_scene = false;
+    bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
     unsigned long long* d_counters = nullptr;
     float* d_rgb = nullptr;
     size_t rgb_cap = 0;
@@ -141,33 +142,27 @@ int ensure_lanes(rt_ctx* c, int n) {
 // Carve a lane's wavefront working set for chunks of up to `cap` pixels: every
 // queue and shade-record array is G regions of R entries; the shade records
 // have one such array per lit generation (`levels` = max_depth + 1).
-int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels) {
+int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels, uint32_t nlists) {
     WfBufs& b = L.b;
-    size_t off = 0;
-    std::vector<std::pair<void**, size_t>> parts;
-    auto add = [&](void** p, size_t bytes) { parts.emplace_back(p, off); off = align_up(off + bytes, 256); };
-    const size_t q = static_cast<size_t>(G) * R;   // queue capacity (>= generation-0 slots)
-    for (int g = 0; g < 2; ++g) {
-        for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qo[g][a]), q * 8);
-        for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.qd[g][a]), q * 8);
-        add(reinterpret_cast<void**>(&b.qsig[g]), q * 8);
-        add(reinterpret_cast<void**>(&b.qpix[g]), q * 4);
-    }
-    const size_t qr = q * levels;                  // shade records: one region array per generation
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_pt[a]), qr * 8);
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.sr_d[a]), qr * 8);
-    add(reinterpret_cast<void**>(&b.sr_sig), qr * 8);
-    add(reinterpret_cast<void**>(&b.sr_obj), qr * 4);
-    add(reinterpret_cast<void**>(&b.sr_prim), qr * 4);
-    add(reinterpret_cast<void**>(&b.sr_pix), qr * 4);
-    add(reinterpret_cast<void**>(&b.occ), qr * 4);
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.st[a]), static_cast<size_t>(levels) * cap * 8);
-    add(reinterpret_cast<void**>(&b.st_obj), static_cast<size_t>(levels) * cap * 4);
-    add(reinterpret_cast<void**>(&b.st_f), static_cast<size_t>(levels) * cap * 8);
-    for (int a = 0; a < 3; ++a) add(reinterpret_cast<void**>(&b.term[a]), static_cast<size_t>(cap) * 8);
-    add(reinterpret_cast<void**>(&b.nlev), cap);
-    add(reinterpret_cast<void**>(&b.rq), static_cast<size_t>(kMaxGenerations) * G * 4);
-    add(reinterpret_cast<void**>(&b.rs), static_cast<size_t>(kMaxGenerations) * G * 4);
+    const uint64_t q = static_cast<uint64_t>(G) * R;   // queue capacity (>= generation-0 slots)
+    const uint64_t capa = align_up(cap, 64);
+    const uint64_t nl = std::max(1u, nlists);
+    // section sizes (device_layout.hpp, WfBufs)
+    const uint64_t s_queue = 2ull * 8 * q * 8;
+    const uint64_t s_rec = static_cast<uint64_t>(levels) * q * (7 * 8 + 4 * 4);
+    const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (4 * 8 + 4);
+    const uint64_t s_term = capa * (3 * 8 + 1);
+    const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
+    const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;
+    const uint64_t s_ro = static_cast<uint64_t>(kMaxGenerations) * nl * G * 4;
+    uint64_t off = align_up(s_queue, 256);
+    b.o_rec = off; off = align_up(off + s_rec, 256);
+    b.o_lev = off; off = align_up(off + s_lev, 256);
+    b.o_term = off; off = align_up(off + s_term, 256);
+    b.o_rq = off; off = align_up(off + s_reg, 256);
+    b.o_rs = off; off = align_up(off + s_reg, 256);
+    b.o_oq = off; off = align_up(off + s_oq, 256);
+    b.o_ro = off; off = align_up(off + s_ro, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -179,12 +174,14 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         HIP_TRY(c, hipMalloc(&L.mem, off));
         L.bytes = off;
     }
-    auto* base = static_cast<uint8_t*>(L.mem);
-    for (auto& pr : parts) *pr.first = base + pr.second;
+    b.mem = static_cast<unsigned char*>(L.mem);
     b.totals = c->d_counters + kTotals;
     b.gen_totals = c->d_counters + kGenTotals;
-    b.rstride = q;
+    b.qcap = q;
     b.cap = cap;
+    b.capa = static_cast<uint32_t>(capa);
+    b.levels = levels;
+    b.nlists = nlists;
     b.G = G;
     b.R = R;
     return RT_OK;
@@ -325,6 +322,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (leaf_env <= 0 && bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
         bvh = build_sphere_bvh(sx, sy, sz, srad, pad, 4);
     const Bvh4Result bvh4 = collapse_bvh4(bvh);
+    // traversal stacks hold 64 entries (trace_common.hpp kBvhStack / kBvh4Stack)
+    if (bvh_depth(bvh) > 64) return fail(c, RT_E_UNSUPPORTED, "sphere BVH deeper than the traversal stack");
+    c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
     const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
     {
         std::vector<DevSphere> s2(spheres.size());
@@ -480,6 +480,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             src = fit2 ? 7 : 2;
             src_occ = fit4 ? 10 : 11;
             if (!fit2 || !fit4) { src = 2; src_occ = 11; }
+            if (c->deep_bvh4) src_occ = src;                 // the 4-wide stack could overflow
             if (const char* force = std::getenv("RT_WF_SRC")) {
                 int n = -1, oc = -1;
                 const int got = std::sscanf(force, "%d,%d", &n, &oc);
@@ -491,6 +492,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src >= 12) && !fit4) &&
                               !((src_occ == 10 || src_occ >= 12) && !fit4);
             if (!pair_ok || !fits) { src = 2; src_occ = 11; }
+            if (c->deep_bvh4 && src_occ >= 10) src_occ = src = 2;
         } else {
             src = src_occ = fits_lds ? 1 : 0;
         }
@@ -520,6 +522,9 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const bool split = env_int("RT_WF_SPLIT", 1) != 0;
         const int n_b = std::max(1, std::min(kMaxBStreams, env_int("RT_WF_BSTREAMS", 1)));
         const bool fuse = env_int("RT_WF_FUSE", 1) != 0;
+        // shadow item lists (RT_WF_LISTS=0: every (record, light) pair goes to the shadow kernel)
+        const uint32_t nlists = (split && fuse && env_int("RT_WF_LISTS", 1) != 0 && c->dsc.n_lights > 0 &&
+                                 c->dsc.n_lights <= 24) ? static_cast<uint32_t>(c->dsc.n_lights) + 1u : 0u;
         // generation 0 by camera tile (RT_WF_CAM=0: per-ray like the other generations);
         // only with the binary-tree sources, whose node order the camera view shares
         int cam = 0;
@@ -533,7 +538,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         const uint32_t wg_major = env_int("RT_WF_DEAL", 1) != 0 ? 1u : 0u;
         for (int l = 0; l < n_lanes; ++l) {
             if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
-            rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1);
+            rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1, nlists);
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;

@@ -171,6 +171,13 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
 // exactness" has the argument in full.
 constexpr float kBoxTol = 1e-5f;
 constexpr int kBvhStack = 64;      // host builder bounds the depth (median splits past depth 40)
+#ifndef RT_SEL4
+#define RT_SEL4 0
+#endif
+#ifndef RT_PUSH_BRANCHLESS
+#define RT_PUSH_BRANCHLESS 0
+#endif
+constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst case (bvh4_stack_need) against it
 
 // f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
 // bound is one FMA, fma(lo, 1/d, -o/d).  The FMA's rounding terms are of the
@@ -179,6 +186,20 @@ constexpr int kBvhStack = 64;      // host builder bounds the depth (median spli
 struct RayBox {
     float ix, iy, iz, nox, noy, noz;
 };
+
+// The near-plane selectors of a ray for the plane-major 4-wide nodes: the
+// near slab bound of axis a is plane 2a (lo) when the ray's 1/d_a >= 0, else
+// plane 2a + 1 (hi), and the far bound the other one.  fma with a fixed 1/d
+// and -o/d is monotone in the coordinate, so fma(near) = min(fma(lo),
+// fma(hi)) and fma(far) = max(...) exactly: the same intervals as
+// box_hit's, with 6 fewer min/max per child box.  Offsets in planes.
+struct Sel4 {
+    int32_t x, y, z;             // 0 or n4 (hi plane of the axis is the near one)
+};
+
+__device__ __forceinline__ Sel4 make_sel4(const RayBox& rb, int32_t n4) {
+    return Sel4{rb.ix < 0.0f ? n4 : 0, rb.iy < 0.0f ? n4 : 0, rb.iz < 0.0f ? n4 : 0};
+}
 
 __device__ __forceinline__ float inv_dir(double d) {
     float f = static_cast<float>(d);
@@ -413,6 +434,32 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     }
 }
 
+// The part of a shadow query (raytrace.rs:41-49, see occluded_brute) that
+// needs no traversal: the planes (a NaN plane hit with a range means lit, any
+// plane hit without one or with t*t < r2 means shadowed) and then the sphere
+// the query starts on (`hint`, -1 for none).  Returns 0 = lit, 1 = shadowed,
+// 2 = undecided: only the spheres' any-hit traversal can tell, with the
+// planes and the hint left out (they cannot change the answer any more).
+__device__ __forceinline__ int shadow_prefilter(const DevScene& sc, const DevSphere* S, const Ray& r, bool has_range,
+                                                double r2, int32_t hint) {
+    bool plane_block = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        if (!has_range) return 1;
+        if (t != t) return 0;
+        plane_block |= t * t < r2;
+    }
+    if (plane_block) return 1;
+    if (sc.n_spheres == 0) return 0;
+    if (hint >= 0) {
+        const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+        double t;
+        if (sphere_t(S[hint], r, 2.0 * a, 4.0 * a, t) && (!has_range || t * t < r2)) return 1;
+    }
+    return 2;
+}
+
 // ---- 4-wide BVH --------------------------------------------------------
 // One node visit tests the 4 child boxes (same conservative slab test).  The
 // nearest query continues with the nearest hit child and pushes the others
@@ -462,6 +509,31 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
     for (int k = 0; k < 4; ++k) {
         const float n = widen_lo(tn[k]);
         const float f = widen_hi(tf[k]);
+        const bool hit = n <= f && f >= 0.0f && n <= tlim && ch.i[k] != kBvh4Empty;
+        o.t[k] = hit ? n : __builtin_inff();
+        o.c[k] = hit ? ch.i[k] : kBvh4Empty;
+    }
+    return o;
+}
+
+// node4_test with the ray's near/far planes chosen by Sel4 (same result).
+__device__ __forceinline__ Node4Hits node4_test_sel(const BvhView& v, int32_t node, const RayBox& rb, const Sel4& sel,
+                                                    float tlim) {
+    const int32_t N = v.n4;
+    const DevBvh4Plane* P = v.p4 + node;
+    const DevBvh4Plane nx = P[sel.x], fx = P[N - sel.x];
+    const DevBvh4Plane ny = P[2 * N + sel.y], fy = P[3 * N - sel.y];
+    const DevBvh4Plane nz = P[4 * N + sel.z], fz = P[5 * N - sel.z];
+    const DevBvh4Plane ch = P[6 * N];
+    Node4Hits o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float tn = fmaxf(fmaxf(slab_t(nx.f[k], rb.ix, rb.nox), slab_t(ny.f[k], rb.iy, rb.noy)),
+                               slab_t(nz.f[k], rb.iz, rb.noz));
+        const float tf = fminf(fminf(slab_t(fx.f[k], rb.ix, rb.nox), slab_t(fy.f[k], rb.iy, rb.noy)),
+                               slab_t(fz.f[k], rb.iz, rb.noz));
+        const float n = widen_lo(tn);
+        const float f = widen_hi(tf);
         const bool hit = n <= f && f >= 0.0f && n <= tlim && ch.i[k] != kBvh4Empty;
         o.t[k] = hit ? n : __builtin_inff();
         o.c[k] = hit ? ch.i[k] : kBvh4Empty;
@@ -552,21 +624,34 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
         if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
+    const Sel4 sel = make_sel4(rb, v.n4);
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
-    RT_STACK_DECL(0, int32_t);
+    // pushes are unconditional stores at the stack top (junk when nothing is
+    // pushed; the next push overwrites it): no branch per child
+    int32_t stk_m[kBvh4Stack];
+    int stk_n = 0;
     int32_t cur = sc.bvh4_root;
     for (;;) {
         if (cur >= 0) {
             // slot order (measured: near-to-far sorting costs more than it saves here)
+#if RT_SEL4
+            const Node4Hits n = node4_test_sel(v, cur, rb, sel, tlim);
+#else
             const Node4Hits n = node4_test(v, cur, rb, tlim);
+#endif
             if constexpr (kCount) w->boxes += 4;
             int32_t next = kBvh4Empty;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (n.c[k] != kBvh4Empty) {
-                    if (next != kBvh4Empty) stk_push(next);
-                    next = n.c[k];
-                }
+            for (int k = 0; k < 4; ++k) {
+                const bool hk = n.c[k] != kBvh4Empty;
+#if RT_PUSH_BRANCHLESS
+                stk_m[stk_n] = next;
+                stk_n += (hk && next != kBvh4Empty) ? 1 : 0;
+#else
+                if (hk && next != kBvh4Empty) stk_m[stk_n++] = next;
+#endif
+                next = hk ? n.c[k] : next;
+            }
             if (next != kBvh4Empty) { cur = next; continue; }
         } else {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
@@ -577,7 +662,7 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
             }
         }
         if (stk_n == 0) return false;
-        cur = stk_pop();
+        cur = stk_m[--stk_n];
     }
 }
 

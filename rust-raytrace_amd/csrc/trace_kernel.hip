@@ -246,7 +246,7 @@ __device__ __forceinline__ void tile_rect(const FrameParams& fp, const WfBufs& b
 }
 
 __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
-    return Ray{b.qo[q][0][i], b.qo[q][1][i], b.qo[q][2][i], b.qd[q][0][i], b.qd[q][1][i], b.qd[q][2][i]};
+    return Ray{b.qf(q, 0)[i], b.qf(q, 1)[i], b.qf(q, 2)[i], b.qf(q, 3)[i], b.qf(q, 4)[i], b.qf(q, 5)[i]};
 }
 
 // Sphere sources of the wavefront intersection kernels.
@@ -391,19 +391,23 @@ __device__ __forceinline__ void write_background_pixel(const FrameParams& fp, co
         if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
             for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k) fp.out_bgr[static_cast<size_t>(row) * fp.bgr_pitch + k] = 0;
     }
-    b.nlev[p] = kNlevDone;
+    b.nlev()[p] = kNlevDone;
 }
 
 __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
-    b.term[0][p] = c.r; b.term[1][p] = c.g; b.term[2][p] = c.b;
-    b.nlev[p] = static_cast<uint8_t>(k);
+    b.term(0)[p] = c.r; b.term(1)[p] = c.g; b.term(2)[p] = c.b;
+    b.nlev()[p] = static_cast<uint8_t>(k);
 }
 
 // LDS of a queue kernel after its staged data.
+constexpr int kMaxFusedLights = 24;         // shadow lists / fused shading: the light count lives in occ bits 24..31
+constexpr int kOccCount = 24;
+constexpr int kQueueCounters = 2 + kMaxFusedLights + 1;
+
 struct QueueLds {
     uint32_t* scan;     // G + 1
     uint32_t* wave;     // 16
-    uint32_t* count;    // 2: shade records, reflection rays appended by this workgroup
+    uint32_t* count;    // shade records, reflection rays, then one per shadow item list, appended by this workgroup
 };
 
 __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
@@ -411,14 +415,14 @@ __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
     return QueueLds{p, p + G + 1, p + G + 1 + kWfThreads / 64};
 }
 
-__host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + 2) * 4u; }
+__host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + kQueueCounters) * 4u; }
 
 // What follows a nearest hit (all 64 lanes call it; `live` lanes carry a
 // query): a miss or a cut-off ends the chain at once (terminal colour; a
 // camera miss writes its final pixel); a lit hit becomes a shade record of
 // generation k, and a specular one also queues its reflection ray in Q_{k+1}.
 // counts[0..1]: this workgroup's LDS append counters (records, rays).
-template <bool kCam, bool kFresnel>
+template <bool kCam, bool kFresnel, bool kLists>
 __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FrameParams& fp, const WfBufs& b,
                                                const DevSphere* sph, int k, bool live, const Ray& r, double sig,
                                                uint32_t p, const Hit& h, uint32_t* counts, size_t obase, size_t rbase) {
@@ -454,24 +458,50 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         }
     }
     const uint32_t slot = lds_append(&counts[0], shade);
+    uint32_t occ = 0u;
+    if constexpr (kLists) {
+        // shadow lists: decide what needs no traversal here (planes, the own
+        // sphere) and queue each undecided (record, light) pair in light l's list
+        const uint32_t L = static_cast<uint32_t>(sc.n_lights);
+        const size_t rk = static_cast<size_t>(k) * b.nlists;
+        uint32_t decided = 0u;
+        for (uint32_t l = 0; l < L; ++l) {
+            bool want = false;
+            if (shade) {
+                double lx, ly, lz, r2;
+                const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+                const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+                const int d = shadow_prefilter(sc, sph, sray, has_range, r2, h.prim);
+                occ |= d == 1 ? 1u << l : 0u;
+                decided += d != 2 ? 1u : 0u;
+                want = d == 2;
+            }
+            const uint32_t qs = lds_append(&counts[2 + l], want);
+            if (want) b.oq()[(rk + l) * b.qcap + obase + qs] = static_cast<uint32_t>(obase) + slot;
+        }
+        occ |= decided << kOccCount;
+        const bool none = shade && decided == L;           // nothing to trace: shade directly from the list
+        const uint32_t qs = lds_append(&counts[2 + L], none);
+        if (none) b.oq()[(rk + L) * b.qcap + obase + qs] = static_cast<uint32_t>(obase) + slot;
+    }
     if (shade) {
         const size_t at = rbase + slot;
-        b.sr_pt[0][at] = ptx; b.sr_pt[1][at] = pty; b.sr_pt[2][at] = ptz;
-        b.sr_d[0][at] = r.dx; b.sr_d[1][at] = r.dy; b.sr_d[2][at] = r.dz;
-        b.sr_sig[at] = sig;
-        b.sr_obj[at] = h.obj;
-        b.sr_prim[at] = h.prim;
-        b.sr_pix[at] = p;
-        b.occ[at] = 0u;
+        b.rf(0)[at] = ptx; b.rf(1)[at] = pty; b.rf(2)[at] = ptz;
+        b.rf(3)[at] = r.dx; b.rf(4)[at] = r.dy; b.rf(5)[at] = r.dz;
+        b.rf(6)[at] = sig;
+        b.ru(0)[at] = static_cast<uint32_t>(h.obj);
+        b.ru(1)[at] = static_cast<uint32_t>(h.prim);
+        b.ru(2)[at] = p;
+        b.ru(3)[at] = occ;
     }
     const uint32_t rslot = lds_append(&counts[1], refl);
     if (refl) {
         const int qn = (k + 1) & 1;
         const size_t at = obase + rslot;
-        b.qo[qn][0][at] = rr.ox; b.qo[qn][1][at] = rr.oy; b.qo[qn][2][at] = rr.oz;
-        b.qd[qn][0][at] = rr.dx; b.qd[qn][1][at] = rr.dy; b.qd[qn][2][at] = rr.dz;
-        b.qsig[qn][at] = nsig;
-        b.qpix[qn][at] = p;
+        b.qf(qn, 0)[at] = rr.ox; b.qf(qn, 1)[at] = rr.oy; b.qf(qn, 2)[at] = rr.oz;
+        b.qf(qn, 3)[at] = rr.dx; b.qf(qn, 4)[at] = rr.dy; b.qf(qn, 5)[at] = rr.dz;
+        b.qf(qn, 6)[at] = nsig;
+        b.qpix(qn)[at] = p;
     }
 }
 
@@ -483,27 +513,28 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
 // its reflection ray (raytrace.rs:58-64) to Q_{k+1} right here: the next
 // generation depends only on the hit, never on the shadow rays or the Phong
 // sum, so those run on the other stream, off the critical path.
-template <int kSrc, bool kCam, bool kCount, bool kFresnel>
+template <int kSrc, bool kCam, bool kCount, bool kFresnel, bool kLists>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
-    if (threadIdx.x < 2) ql.count[threadIdx.x] = 0;
+    if (threadIdx.x < kQueueCounters) ql.count[threadIdx.x] = 0;
     uint32_t n;
     if constexpr (kCam) {
         n = b.slots;
     } else {
-        region_scan(b.rq + k * b.G, b.G, ql.scan, ql.wave);
+        region_scan(b.rq() + k * b.G, b.G, ql.scan, ql.wave);
         n = ql.scan[b.G];
     }
     if (!wg_has_work(b, n)) {                  // nothing dealt here: publish empty regions, free the CU
-        if (threadIdx.x == 0) { b.rs[k * b.G + blockIdx.x] = 0; b.rq[(k + 1) * b.G + blockIdx.x] = 0; }
+        if (threadIdx.x == 0) { b.rs()[k * b.G + blockIdx.x] = 0; b.rq()[(k + 1) * b.G + blockIdx.x] = 0; }
+        if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = 0;
         return;
     }
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();                                       // publishes the LDS staging and counters
     Work w;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
-    const size_t rbase = static_cast<size_t>(k) * b.rstride + obase;
+    const size_t rbase = static_cast<size_t>(k) * b.qcap + obase;
     RT_FOR_CHUNKS(b, n, j) {
         Ray r{};
         double sig = 0.0;
@@ -522,8 +553,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             } else {
                 const size_t at = region_entry(ql.scan, b.G, b.R, j);
                 r = load_ray(b, k & 1, at);
-                sig = b.qsig[k & 1][at];
-                p = b.qpix[k & 1][at];
+                sig = b.qf(k & 1, 6)[at];
+                p = b.qpix(k & 1)[at];
                 live = true;
             }
         }
@@ -535,13 +566,14 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         if (live) {
             if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         }
-        finish_nearest<kCam, kFresnel>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
+        finish_nearest<kCam, kFresnel, kLists>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        b.rs[k * b.G + blockIdx.x] = ql.count[0];
-        b.rq[(k + 1) * b.G + blockIdx.x] = ql.count[1];
+        b.rs()[k * b.G + blockIdx.x] = ql.count[0];
+        b.rq()[(k + 1) * b.G + blockIdx.x] = ql.count[1];
     }
+    if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = ql.count[2 + threadIdx.x];
     flush_work<kCount>(b, 2, w);
 }
 
@@ -551,15 +583,15 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
 // ends the chain with it.
 template <bool kFresnel>
 __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
-    const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
-    const double dx = b.sr_d[0][at], dy = b.sr_d[1][at], dz = b.sr_d[2][at];
-    const double sig = b.sr_sig[at];
-    const int32_t obj = b.sr_obj[at];
-    const uint32_t p = b.sr_pix[at];
+    const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
+    const double dx = b.rf(3)[at], dy = b.rf(4)[at], dz = b.rf(5)[at];
+    const double sig = b.rf(6)[at];
+    const int32_t obj = static_cast<int32_t>(b.ru(0)[at]);
+    const uint32_t p = b.ru(2)[at];
     const DevMaterial& m = sc.mats[obj];
     Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
     double nx, ny, nz;
-    hit_normal(sc, sc.spheres, b.sr_prim[at], ptx, pty, ptz, nx, ny, nz);
+    hit_normal(sc, sc.spheres, static_cast<int32_t>(b.ru(1)[at]), ptx, pty, ptz, nx, ny, nz);
     const double nd = nx * dx + ny * dy + nz * dz;
     const Shading sh = shading_flags<kFresnel>(m, sig, nd);
     const bool diffuse = sh.diffuse, specular = sh.specular;
@@ -572,10 +604,10 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
         add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
     }
     if (specular) {
-        const size_t st = static_cast<size_t>(k) * b.cap + p;
-        b.st[0][st] = res.r; b.st[1][st] = res.g; b.st[2][st] = res.b;
-        b.st_obj[st] = obj;
-        if (kFresnel && m.kind == kMatFresnel) b.st_f[st] = sh.f;
+        const size_t st = static_cast<size_t>(k) * b.capa + p;
+        b.lf(0)[st] = res.r; b.lf(1)[st] = res.g; b.lf(2)[st] = res.b;
+        b.lobj()[st] = obj;
+        if (kFresnel && m.kind == kMatFresnel) b.lf(3)[st] = sh.f;
     } else {
         set_terminal(b, p, res, k);
     }
@@ -584,9 +616,7 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
 // Fused shadow + shading: each (record, light) item adds its shadow bit and
 // one to the record's finished-light count (bits kOccCount..) in a single
 // atomic; the item that completes the count shades the record with the
-// final mask.  Needs n_lights < 2^kOccCount.
-constexpr int kOccCount = 24;
-constexpr int kMaxFusedLights = 24;
+// final mask.  Needs n_lights <= kMaxFusedLights.
 
 // Record the answer of shadow query (record at, light l); kShade: the query
 // that completes the record's light count shades it.
@@ -595,10 +625,10 @@ __device__ __forceinline__ void occlusion_done(const DevScene& sc, const WfBufs&
                                                uint32_t L, bool occluded) {
     if constexpr (kShade) {
         const uint32_t inc = (occluded ? 1u << l : 0u) + (1u << kOccCount);
-        const uint32_t now = atomicAdd(&b.occ[at], inc) + inc;
+        const uint32_t now = atomicAdd(&b.ru(3)[at], inc) + inc;
         if ((now >> kOccCount) == L) shade_record<kFresnel>(sc, b, k, at, now & ((1u << kOccCount) - 1u));
     } else {
-        if (occluded) atomicOr(&b.occ[at], 1u << l);
+        if (occluded) atomicOr(&b.ru(3)[at], 1u << l);
     }
 }
 
@@ -610,27 +640,78 @@ template <int kSrc, bool kCount, bool kShade, bool kFresnel>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
-    region_scan(b.rs + k * b.G, b.G, ql.scan, ql.wave);
+    region_scan(b.rs() + k * b.G, b.G, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
     const uint32_t nrec = ql.scan[b.G], n = nrec * L;
     if (!wg_has_work(b, n)) return;
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();
     Work w;
-    const size_t rk = static_cast<size_t>(k) * b.rstride;
+    const size_t rk = static_cast<size_t>(k) * b.qcap;
     // light-major: a wave traces 64 consecutive records toward ONE light (coherent)
     RT_FOR_CHUNKS(b, n, qi) {
         if (qi >= n) continue;
         const uint32_t l = qi / nrec, j = qi - l * nrec;
         const size_t at = rk + region_entry(ql.scan, b.G, b.R, j);
-        const double ptx = b.sr_pt[0][at], pty = b.sr_pt[1][at], ptz = b.sr_pt[2][at];
+        const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
-        const int32_t hint = b.sr_prim[at];
+        const int32_t hint = static_cast<int32_t>(b.ru(1)[at]);
         const bool occluded = occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
         occlusion_done<kShade, kFresnel>(sc, b, k, at, l, L, occluded);
+    }
+    flush_work<kCount>(b, 4, w);
+}
+
+// The shadow lists of generation k: item i of list l < n_lights is the
+// any-hit sphere traversal of (record, light l) -- planes and the record's own
+// sphere were already decided by wf_nearest -- and the query that completes a
+// record's light count shades it; list n_lights holds the records that need
+// no traversal, shaded directly.  Lists are laid end to end, each starting on
+// a 64-item boundary so a wave's chunk belongs to one list (light-major).
+template <int kSrc, bool kCount, bool kFresnel>
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_shadow(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t NL = b.nlists, L = NL - 1u;
+    uint32_t* scans = reinterpret_cast<uint32_t*>(lds + staged_bytes<kSrc>(sc));   // NL x (G + 1)
+    __shared__ uint32_t s_wave[kWfThreads / 64];
+    __shared__ uint32_t s_start[kMaxFusedLights + 2];
+    for (uint32_t l = 0; l < NL; ++l)
+        region_scan(b.ro() + (k * NL + l) * b.G, b.G, scans + l * (b.G + 1), s_wave);
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t l = 0; l < NL; ++l) { s_start[l] = acc; acc += (scans[l * (b.G + 1) + b.G] + 63u) & ~63u; }
+        s_start[NL] = acc;
+    }
+    __syncthreads();
+    const uint32_t n = s_start[NL];
+    if (!wg_has_work(b, n)) return;
+    const BvhView v = stage_lds<kSrc>(sc, lds);
+    __syncthreads();
+    DevScene ss = sc;                                  // the traversal part only: planes decided upstream
+    ss.n_planes = 0;
+    Work w;
+    const size_t rk = static_cast<size_t>(k) * b.qcap;
+    RT_FOR_CHUNKS(b, n, qi) {
+        if (qi >= n) continue;
+        uint32_t l = 0;
+        while (l + 1 < NL && qi >= s_start[l + 1]) ++l;          // wave-uniform: chunks never straddle lists
+        const uint32_t j = qi - s_start[l];
+        const uint32_t* sl = scans + l * (b.G + 1);
+        if (j >= sl[b.G]) continue;                               // padding of the list's last chunk
+        const size_t at = rk + b.oq()[(static_cast<size_t>(k) * NL + l) * b.qcap + region_entry(sl, b.G, b.R, j)];
+        if (l == L) {                                             // nothing to trace
+            shade_record<kFresnel>(sc, b, k, at, b.ru(3)[at] & ((1u << kOccCount) - 1u));
+            continue;
+        }
+        const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
+        double lx, ly, lz, r2;
+        const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+        const bool occluded = occluded_any<kSrc, kCount>(ss, v, sray, has_range, r2, -1, &w);
+        occlusion_done<true, kFresnel>(sc, b, k, at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
 }
@@ -641,13 +722,13 @@ template <bool kFresnel>
 __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
     __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
-    region_scan(b.rs + k * b.G, b.G, s_scan, s_wave);
+    region_scan(b.rs() + k * b.G, b.G, s_scan, s_wave);
     const uint32_t n = s_scan[b.G];
-    const size_t rk = static_cast<size_t>(k) * b.rstride;
+    const size_t rk = static_cast<size_t>(k) * b.qcap;
     RT_FOR_CHUNKS(b, n, j) {
         if (j >= n) continue;
         const size_t at = rk + region_entry(s_scan, b.G, b.R, j);
-        shade_record<kFresnel>(sc, b, k, at, sc.n_lights > 0 ? b.occ[at] : 0u);
+        shade_record<kFresnel>(sc, b, k, at, sc.n_lights > 0 ? b.ru(3)[at] : 0u);
     }
 }
 
@@ -659,16 +740,16 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
     if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
-    Col acc{b.term[0][p], b.term[1][p], b.term[2][p]};
+    Col acc{b.term(0)[p], b.term(1)[p], b.term(2)[p]};
     for (int k = static_cast<int>(nlev) - 1; k >= 0; k -= 4) {
         double sr[4], sg[4], sb[4];
         int32_t ob[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (k - u >= 0) {
-                const size_t at = static_cast<size_t>(k - u) * b.cap + p;
-                ob[u] = b.st_obj[at];
-                sr[u] = b.st[0][at]; sg[u] = b.st[1][at]; sb[u] = b.st[2][at];
+                const size_t at = static_cast<size_t>(k - u) * b.capa + p;
+                ob[u] = b.lobj()[at];
+                sr[u] = b.lf(0)[at]; sg[u] = b.lf(1)[at]; sb[u] = b.lf(2)[at];
             }
         }
         double kr[4], kg[4], kb[4], kf[4];
@@ -677,7 +758,7 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
             if (k - u >= 0) {
                 const DevMaterial& m = sc.mats[ob[u]];
                 kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
-                kf[u] = kFresnel && m.kind == kMatFresnel ? b.st_f[static_cast<size_t>(k - u) * b.cap + p] : 1.0;
+                kf[u] = kFresnel && m.kind == kMatFresnel ? b.lf(3)[static_cast<size_t>(k - u) * b.capa + p] : 1.0;
             }
         }
 #pragma unroll
@@ -707,7 +788,7 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
     const uint32_t npix = fp.tile_w * fp.rows;
     const uint32_t base = blockIdx.x * kBlock;
     const uint32_t p = base + threadIdx.x;
-    const uint8_t nlev = p < npix ? b.nlev[p] : kNlevDone;
+    const uint8_t nlev = p < npix ? b.nlev()[p] : kNlevDone;
     // pixels marked done were written by wf_nearest; a workgroup of them has nothing to do
     if (__syncthreads_and(nlev == kNlevDone)) return;
     if constexpr (!kStaged) {
@@ -750,7 +831,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_tally(FrameParams fp, WfBufs b,
     // one wave per (generation, queue|records) pair, lanes striding the regions
     for (int item = wave; item < 2 * generations; item += kWfThreads / 64) {
         const int g = item >> 1;
-        const uint32_t* src = (item & 1) ? b.rs : b.rq;
+        const uint32_t* src = (item & 1) ? b.rs() : b.rq();
         unsigned long long v = 0;
         if ((item & 1) || g > 0)
             for (uint32_t r = lane; r < b.G; r += 64) v += src[g * b.G + r];
@@ -795,17 +876,24 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
     hipError_t e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
-#define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR>), grid, block, \
+#define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR, false>), grid, block, \
                                                staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+#define RT_NEARL(S, FR) hipLaunchKernelGGL((wf_nearest<S, false, kCount, FR, true>), grid, block, \
+                                           staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+    // shadow lists from generation 1 on (generation 0 feeds every (record, light) pair to the plain shadow kernel)
+    const bool lists = b.nlists != 0 && k >= 1;
     if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
         if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
     } else if (k == 0 && ws.cam == 2) {
         if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
-    } else if (sc.has_fresnel) {
-        if (k == 0) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, false, true);
+    } else if (k == 0) {
+        if (sc.has_fresnel) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, true, false);
+    } else if (lists) {
+        if (sc.has_fresnel) RT_NEARL(kSrcN, true); else RT_NEARL(kSrcN, false);
     } else {
-        if (k == 0) RT_NEAR(kSrcN, true, false); else RT_NEAR(kSrcN, false, false);
+        if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
     }
+#undef RT_NEARL
 #undef RT_NEAR
     (void)lds_n;
     e = ws.ma ? ws.ma->mark(ws.a, kKfNearest) : hipSuccess;
@@ -819,6 +907,13 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (sb != ws.a) {
         if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(sb, ws.near_done[k], 0)) != hipSuccess) return e;
+    }
+    if (lists) {                                 // shadow lists (planes and own sphere decided upstream)
+        if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+        const size_t lds_s = staged_bytes<kSrcO>(sc) + static_cast<size_t>(b.nlists) * (b.G + 1) * 4u;
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, true>), grid, block, lds_s, sb, sc, fp, b, k);
+        else hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, false>), grid, block, lds_s, sb, sc, fp, b, k);
+        return mb ? mb->mark(sb, kKfOcclusion) : hipSuccess;
     }
     const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && ws.fuse;
     if (sc.n_lights > 0) {
@@ -885,7 +980,6 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
     const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
     if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
-    // the Fresnel-capable fold costs registers; scenes without FresnelMaterial use the plain one
     if (sc.has_fresnel) {
         if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
         else hipLaunchKernelGGL((wf_fold<false, true>), gf, dim3(kBlock), 0, s, sc, fp, b);

@@ -16,7 +16,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "librtamd.so")
+# RT_LIBRTAMD: an alternative build of the same library (A/B measurement)
+LIB_PATH = os.environ.get("RT_LIBRTAMD") or os.path.join(PKG_DIR, "librtamd.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "raytrace_amd.h")
 
 RT_OK = 0

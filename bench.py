@@ -11,9 +11,13 @@ reported separately in DESIGN.md, never in `value`).
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
 Multi-GPU: the frame's rows are dealt in 16-row bands round-robin over ranks
-(libraytrace/shard.py); no collective touches the data path.  Total work is
-fixed as N grows ("scaling": "strong").  value = rays of the whole frame x K /
-max-over-ranks wall time of the K timed steps.
+(libraytrace/shard.py); no collective touches the data path (RCCL carries the
+barrier and the max-over-ranks timing only).  Default "scaling": "weak": at N
+GPUs the same scene and view are rendered at sqrt(N) x the resolution (frame
+side 4096*sqrt(N), rounded to whole bands), so every GPU renders the N=1
+frame's 16.7 M pixels; --scaling strong splits the 4096^2 frame instead.
+value = rays of the whole frame x K / max-over-ranks wall time of the K timed
+steps.  --config c4 / c5 select the larger configs of BASELINE.json.
 
 Rays = every Scene::intersect query the reference would issue (camera +
 reflection + shadow), counted by the kernel; identical to the oracle's count
@@ -38,13 +42,21 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--width", type=int, default=4096)
-    p.add_argument("--height", type=int, default=4096)
-    p.add_argument("--spheres", type=int, default=1000)
-    p.add_argument("--depth", type=int, default=8)
+    p.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
+                   help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16")
+    p.add_argument("--width", type=int, default=0)
+    p.add_argument("--height", type=int, default=0)
+    p.add_argument("--spheres", type=int, default=0)
+    p.add_argument("--depth", type=int, default=-1)
     p.add_argument("--algo", default="auto", choices=["auto", "wavefront", "lds", "global"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="N > 1: weak = the frame side grows by sqrt(N) (same scene and view, every GPU "
+                        "renders the N=1 pixel count); strong = the N=1 frame split N ways")
+    p.add_argument("--shard-of", type=int, default=0,
+                   help="(diagnostic, one process) render only rank 0's row bands of an N-rank frame; "
+                        "its time is what each rank of an N-GPU run spends")
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
     return p.parse_args()
@@ -93,23 +105,38 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=3, name="c3")
+    cfg = {"c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
+           "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}[args.config]       # scenes.config3/4/5
+    args.width = args.width or cfg[0]
+    args.height = args.height or cfg[0]
+    n_split = args.shard_of if (args.shard_of > 1 and world == 1) else world
+    if n_split > 1 and args.scaling == "weak":
+        # weak scaling: the same view at sqrt(N) x the resolution, so each of the N ranks renders
+        # (up to rounding to whole bands) the N=1 frame's pixel count
+        f = n_split ** 0.5
+        args.width = max(BAND, int(round(args.width * f / BAND)) * BAND)
+        args.height = max(BAND, int(round(args.height * f / BAND)) * BAND)
+    args.spheres = args.spheres or cfg[1]
+    args.depth = cfg[2] if args.depth < 0 else args.depth
+    spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=cfg[3],
+                                 box_scale=cfg[4], name=args.config)
     W, H = spec.width, spec.height
     ctx = lr.Context(local)
     scene = lr.Scene.deserialize(spec.to_text())
     ctx.upload(scene)
-    rows = shard.local_rows(H, BAND, world, rank)
-    tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, world) == rank else None
+    rows = shard.local_rows(H, BAND, band_world, rank)
+    tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, band_world) == rank else None
     assert tail is None or len(tail) == 0, "bench frames are whole bands"
     algo = {"auto": lr.RT_ALGO_AUTO, "wavefront": lr.RT_ALGO_WAVEFRONT, "lds": lr.RT_ALGO_BRUTE_LDS,
             "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
-    opts = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+    opts = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
                           max_depth=args.depth, spp=1, algo=algo,
                           flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8)
     pitch = 3 * W
@@ -123,7 +150,7 @@ def main():
     # events around every launch (RT_TIME_KERNELS), after the timed region: the
     # events sit between launches on both streams and would perturb the timing
     timed_flags = opts.flags | lr.RT_TIME_KERNELS
-    opts_timed = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+    opts_timed = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
                                 max_depth=args.depth, spp=1, algo=algo, flags=timed_flags)
 
     def step(o=opts):
@@ -159,7 +186,7 @@ def main():
         ktimes = ctx.kernel_times()        # {family: (ms summed over K instrumented frames, launches)}
 
     # one more, untimed frame with the instrumented kernels: exact box / sphere test counts
-    work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=world, band_phase=rank,
+    work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
                           max_depth=args.depth, spp=1, algo=algo,
                           flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK)
     ctx.render_device(work, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
@@ -200,7 +227,7 @@ def main():
         scene_bytes = args.spheres * (32 + 4) + args.spheres * 128 + 2 * 56
         algo_bytes = pixels_local * (12 + 3) + scene_bytes          # f32 RGB + u8 BGR writes + scene read once
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-        key = f"c3_{W}x{H}_n{args.spheres}_d{args.depth}"
+        key = f"{args.config}_{W}x{H}_n{args.spheres}_d{args.depth}"
         traffic = pmc_traffic(key)
         kernels = {}
         for fam, (ms, n) in ktimes.items():
@@ -213,9 +240,9 @@ def main():
             "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"C3: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
-                                   f"depth {args.depth}, 1 spp centre jitter (seed 3)",
+            "scaling": "weak" if (n_split > 1 and args.scaling == "weak") else "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
+                                   f"depth {args.depth}, 1 spp centre jitter (seed {cfg[3]})",
                        "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth,
                        "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}",
                        "algo": args.algo},

@@ -195,7 +195,14 @@ int rt_ctx_generation_counts(rt_ctx* ctx, uint32_t* queue, uint32_t* shaded, int
  * count; then resets.  Synchronises with the last timed launch.  Families:
  * rt_kernel_family.  Renders split over several chunk streams are not timed. */
 enum rt_kernel_family {
-    RT_KF_NEAREST = 0, RT_KF_OCCLUSION = 1, RT_KF_SHADE = 2, RT_KF_FOLD = 3, RT_KF_TALLY = 4, RT_KF_COUNT = 5
+    RT_KF_NEAREST = 0,      /* wf_nearest, generations >= 1 */
+    RT_KF_OCCLUSION = 1,    /* wf_occlusion: every (record, light) pair of a generation */
+    RT_KF_SHADE = 2,        /* wf_shade */
+    RT_KF_FOLD = 3,         /* wf_fold */
+    RT_KF_TALLY = 4,        /* wf_tally */
+    RT_KF_CAMERA = 5,       /* wf_nearest, generation 0 (camera rays) */
+    RT_KF_SHADOW = 6,       /* wf_shadow: the shadow item lists of a generation */
+    RT_KF_COUNT = 7
 };
 int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 

@@ -10,7 +10,9 @@
 namespace rtamd {
 
 // Kernel families of the wavefront schedule (rt_ctx_kernel_times indices).
-enum KernelFamily : int8_t { kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCount = 5 };
+enum KernelFamily : int8_t {
+    kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCamera = 5, kKfShadow = 6, kKfCount = 7
+};
 
 // Per-launch timing (RT_TIME_KERNELS): begin() records a start event before a
 // launch (after any cross-stream wait), mark() an end event after it, noting

@@ -896,7 +896,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
 #undef RT_NEARL
 #undef RT_NEAR
     (void)lds_n;
-    e = ws.ma ? ws.ma->mark(ws.a, kKfNearest) : hipSuccess;
+    e = ws.ma ? ws.ma->mark(ws.a, k == 0 ? kKfCamera : kKfNearest) : hipSuccess;
     if (e != hipSuccess) return e;
     if (static_cast<uint32_t>(k) > fp.max_depth) return hipSuccess;     // no shade records past the cut-off
     // shadows and shading of generation k: on a b stream once nearest_k is done
@@ -913,7 +913,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         const size_t lds_s = staged_bytes<kSrcO>(sc) + static_cast<size_t>(b.nlists) * (b.G + 1) * 4u;
         if (sc.has_fresnel) hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, true>), grid, block, lds_s, sb, sc, fp, b, k);
         else hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, false>), grid, block, lds_s, sb, sc, fp, b, k);
-        return mb ? mb->mark(sb, kKfOcclusion) : hipSuccess;
+        return mb ? mb->mark(sb, kKfShadow) : hipSuccess;
     }
     const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && ws.fuse;
     if (sc.n_lights > 0) {

@@ -338,10 +338,11 @@ def test_kernel_times(gpu_ctx):
         assert np.array_equal(plain[1], t[1])
     kt = gpu_ctx.kernel_times()
     gens = 8 + 2
-    assert kt["nearest"][1] == 2 * gens
-    # shadows + shading for the lit generations 0..max_depth (none past the cut-off)
-    assert kt["occlusion"][1] == 2 * (gens - 1)      # config3 has lights
-    # shading runs inside the shadow kernel (fused) unless RT_WF_FUSE=0
+    assert kt["camera"][1] == 2 and kt["nearest"][1] == 2 * (gens - 1)
+    # shadow queries of the lit generations 0..max_depth (none past the cut-off): the
+    # plain kernel for every (record, light) pair, or the item lists from generation 1 on
+    assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
+    # shading runs inside the shadow kernels (fused) unless RT_WF_FUSE=0
     assert kt["shade"][1] in (0, 2 * (gens - 1))
     assert kt["fold"][1] == 2 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)

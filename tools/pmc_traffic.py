@@ -16,19 +16,29 @@ import re
 import sys
 
 
+def targs(name):
+    return [a.strip() for a in name.split("<", 1)[1].split(">")[0].split(",")] if "<" in name else []
+
+
+def family(name):
+    fam = re.search(r"(wf_[a-z]+)", name).group(1)
+    if fam == "wf_nearest" and targs(name)[1:2] == ["true"]:
+        return "wf_camera"                       # generation 0 (kCam)
+    return fam
+
+
 def frames(path, counter):
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     out, cur = [], None
     for r in rows:
         name = r["Kernel_Name"]
-        if re.search(r"wf_nearest<\d+, true, (true|false)>", name):
-            cur = {"instrumented": ", true, true>" in name, "kernels": collections.defaultdict(float)}
+        if "wf_nearest<" in name and targs(name)[1:2] == ["true"]:      # a frame starts at generation 0
+            cur = {"instrumented": targs(name)[2] == "true", "kernels": collections.defaultdict(float)}
             out.append(cur)
         if cur is None or "wf_" not in name:
             continue
-        fam = re.search(r"(wf_[a-z]+)", name).group(1)
-        cur["kernels"][fam] += float(r["Counter_Value"]) * 1024.0
+        cur["kernels"][family(name)] += float(r["Counter_Value"]) * 1024.0
     return [f for f in out if not f["instrumented"]]
 
 

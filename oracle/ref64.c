@@ -80,6 +80,34 @@ static void rng_seed(rng_t* r, uint64_t seed) {
     r->x = (uint32_t)a; r->y = (uint32_t)(a >> 32); r->z = (uint32_t)b; r->w = (uint32_t)(b >> 32) | 1u;
 }
 
+/* ---- keyed counter-based RNG (REF_RNG_KEYED): the specification shared with
+ * the device path (trace_common.hpp).  A draw is a pure function of a 64-bit
+ * key and a draw id; keys follow the recursion:
+ *   pixel      kp = mix(mix(seed) + (y << 32 | x))         (frame coordinates)
+ *   AA sample  ka = child(kp, aa)      jitter: jx = f64(ka, 0), jy = f64(ka, 1)
+ *   camera     kc = child(ka, cs)      DoF: theta = f64(kc, 0) * 2pi, r2 = closed01(kc, 1)
+ *   path key of the camera ray = kc; a hit with path key K draws
+ *     AreaLight l:         u = f64(K, 2 + 2l), w = f64(K, 3 + 2l)
+ *     indirect sample i:   r1 = f64(K, 128 + 2i), r2 = f64(K, 129 + 2i)
+ *   child ray i of a hit (indirect sample i; mirror reflection 0,
+ *   Transparent refraction 1): key child(K, i).
+ * f64 / closed01 use the bit recipes of rand 0.3 (rng_f64 / rng_closed01). */
+static inline uint64_t kmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint64_t key_child(uint64_t k, uint64_t i) { return kmix(k + (i + 1) * 0x9E3779B97F4A7C15ull); }
+static inline uint64_t key_bits(uint64_t k, uint32_t id) { return kmix(k ^ ((uint64_t)(id + 1) * 0xD1B54A32D192ED03ull)); }
+static inline double key_f64(uint64_t k, uint32_t id) {
+    uint64_t bits = 0x3FF0000000000000ull | (key_bits(k, id) & 0xFFFFFFFFFFFFFull);
+    double d; memcpy(&d, &bits, 8); return d - 1.0;
+}
+static inline double key_closed01(uint64_t k, uint32_t id) { return (double)(key_bits(k, id) >> 11) / 9007199254740991.0; }
+static inline uint64_t key_pixel(uint64_t seed, uint32_t x, uint32_t y) {
+    return kmix(kmix(seed) + (((uint64_t)y << 32) | x));
+}
+
 /* ---- shapes.rs ---- */
 typedef struct { v3 origin, direction; } ray_t;
 /* shapes.rs:22-24 */
@@ -125,7 +153,13 @@ typedef struct {
     double cam_im_dist;
     ref_counts cnt;
     rng_t rng;
+    int keyed;              /* REF_RNG_KEYED */
 } ctx_t;
+
+/* A [0,1) draw: the next XorShift output, or the keyed draw (key, id). */
+static inline double draw_f64(ctx_t* c, uint64_t key, uint32_t id) {
+    return c->keyed ? key_f64(key, id) : rng_f64(&c->rng);
+}
 
 typedef struct { int hit; uint32_t obj; double t; v3 normal; } hit_t;
 
@@ -160,12 +194,12 @@ static hit_t scene_intersect(ctx_t* c, const ray_t* ray) {
 }
 
 /* scene.rs:117-155: returns 1 if the light has a range (Some(sq)) */
-static int light_dir(ctx_t* c, const ref_light* L, v3 pt, v3* ldir, double* sq) {
+static int light_dir(ctx_t* c, const ref_light* L, uint32_t li, uint64_t key, v3 pt, v3* ldir, double* sq) {
     if (L->kind == REF_POINT || L->kind == REF_AREA) {
         v3 loc;
         if (L->kind == REF_POINT) loc = from3(L->v);
         else {
-            double u = rng_f64(&c->rng), w = rng_f64(&c->rng);
+            double u = draw_f64(c, key, 2 + 2 * li), w = draw_f64(c, key, 3 + 2 * li);
             loc = vadd(vadd(from3(L->v), vmul(from3(L->v + 3), u)), vmul(from3(L->v + 6), w));
         }
         v3 dv = V(loc.x - pt.x, loc.y - pt.y, loc.z - pt.z);
@@ -187,9 +221,10 @@ static int in_shadow(ctx_t* c, v3 pt, v3 ldir, int has_range, double sq) {
     return 1;
 }
 
-static col ray_color(ctx_t* c, const ray_t* ray, double sig, uint32_t depth);
+static col ray_color(ctx_t* c, const ray_t* ray, double sig, uint32_t depth, uint64_t key);
 
-static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* ray, double sig, uint32_t depth) {
+static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* ray, double sig, uint32_t depth,
+                 uint64_t key) {
     col kd = cfrom3(m->diffuse), ks = cfrom3(m->specular), amb = cfrom3(m->ambient);
     switch (m->material) {
     case REF_PHONG: {                                  /* raytrace.rs:30-67 */
@@ -203,7 +238,7 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             if (!(diffuse || specular)) continue;
             const ref_light* L = &c->s->lights[li];
             v3 ldir; double sq = 0.0;
-            int rng_ = light_dir(c, L, pt, &ldir, &sq);
+            int rng_ = light_dir(c, L, li, key, pt, &ldir, &sq);
             if (in_shadow(c, pt, ldir, rng_, sq)) continue;
             col lc = cfrom3(L->color);
             if (diffuse)
@@ -216,7 +251,7 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             v3 d = ray->direction;
             v3 rd = vsub(d, vmul(normal, 2.0 * dot(d, normal)));
             ray_t refl; refl.origin = vadd(pt, vmul(rd, EPS_OFFSET)); refl.direction = rd;
-            res = cadd(res, cmulc(ks, ray_color(c, &refl, sig * significance(ks), depth + 1)));
+            res = cadd(res, cmulc(ks, ray_color(c, &refl, sig * significance(ks), depth + 1, key_child(key, 0))));
         }
         return res;
     }
@@ -231,7 +266,7 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             for (uint32_t li = 0; li < c->s->n_lights; ++li) {
                 const ref_light* L = &c->s->lights[li];
                 v3 ldir; double sq = 0.0;
-                int rng_ = light_dir(c, L, pt, &ldir, &sq);
+                int rng_ = light_dir(c, L, li, key, pt, &ldir, &sq);
                 if (in_shadow(c, pt, ldir, rng_, sq)) continue;
                 col lc = cfrom3(L->color);
                 if (diffuse)
@@ -241,15 +276,15 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
                                          pow(clamp_zero(dot(normal, normalize(vsub(ldir, ray->direction)))), m->exponent)));
             }
             for (uint32_t si = 0; si < m->samples; ++si) {
-                double r1 = rng_f64(&c->rng) * 2.0 - 1.0;
-                double r2 = rng_f64(&c->rng) * (2.0 * PI_);
+                double r1 = draw_f64(c, key, 128 + 2 * si) * 2.0 - 1.0;
+                double r2 = draw_f64(c, key, 129 + 2 * si) * (2.0 * PI_);
                 double sin_theta = 1.0 - r1 * r1;          /* quirk: no sqrt (raytrace.rs:103) */
                 double phi = r2;
                 double x = sin_theta * cos(phi), z = sin_theta * sin(phi);
                 v3 d0 = V(x, r1, z);
                 v3 dir = dot(d0, normal) >= 0.0 ? d0 : vneg(d0);
                 ray_t nr; nr.origin = vadd(pt, vmul(dir, EPS_OFFSET)); nr.direction = dir;
-                col cl = ray_color(c, &nr, sig, depth + 1);
+                col cl = ray_color(c, &nr, sig, depth + 1, key_child(key, si));
                 double fac = (double)m->samples * 0.5;
                 if (diffuse) res = cadd(res, cdiv(cmul(cmulc(kd, cl), dot(normal, dir)), fac));
                 if (specular)   /* quirk: `ray` here is the NEW ray, so dir - dir = 0 (raytrace.rs:108,115) */
@@ -276,7 +311,7 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             if (!(diffuse || specular)) continue;
             const ref_light* L = &c->s->lights[li];
             v3 ldir; double sq = 0.0;
-            int rng_ = light_dir(c, L, pt, &ldir, &sq);
+            int rng_ = light_dir(c, L, li, key, pt, &ldir, &sq);
             if (in_shadow(c, pt, ldir, rng_, sq)) continue;
             col lc = cfrom3(L->color);
             if (diffuse)
@@ -289,7 +324,8 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             v3 d = ray->direction;
             v3 rd = vsub(d, vmul(normal, 2.0 * dot(d, normal)));
             ray_t refl; refl.origin = vadd(pt, vmul(rd, EPS_OFFSET)); refl.direction = rd;
-            res = cadd(res, cmul(cmulc(ks, ray_color(c, &refl, fresnel * sig * significance(ks), depth + 1)), fresnel));
+            res = cadd(res, cmul(cmulc(ks, ray_color(c, &refl, fresnel * sig * significance(ks), depth + 1, key_child(key, 0))),
+                                 fresnel));
         }
         return res;
     }
@@ -318,7 +354,7 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
             if (!specular) continue;
             const ref_light* L = &c->s->lights[li];
             v3 ldir; double sq = 0.0;
-            int rng_ = light_dir(c, L, pt, &ldir, &sq);
+            int rng_ = light_dir(c, L, li, key, pt, &ldir, &sq);
             if (in_shadow(c, pt, ldir, rng_, sq)) continue;
             col lc = cfrom3(L->color);
             res = cadd(res, cmul(cmul(cmulc(ks, lc), fresnel),
@@ -327,13 +363,14 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
         if (specular) {
             v3 rd = vsub(ray->direction, vmul(normal, 2.0 * ndv));
             ray_t refl; refl.origin = vadd(pt, vmul(rd, EPS_OFFSET)); refl.direction = rd;
-            res = cadd(res, cmul(cmulc(ks, ray_color(c, &refl, fresnel * sig * significance(ks), depth + 1)), fresnel));
+            res = cadd(res, cmul(cmulc(ks, ray_color(c, &refl, fresnel * sig * significance(ks), depth + 1, key_child(key, 0))),
+                                 fresnel));
         }
         if (fresnel < 1.0 && has_refract) {
             double omf = clamp_one(1.0 - fresnel);
             v3 r = normalize(refract);
             ray_t rr; rr.origin = vadd(pt, vmul(r, EPS_OFFSET)); rr.direction = r;
-            res = cadd(res, cmul(ray_color(c, &rr, omf * sig, depth + 1), omf));
+            res = cadd(res, cmul(ray_color(c, &rr, omf * sig, depth + 1, key_child(key, 1)), omf));
         }
         return res;
     }
@@ -342,10 +379,10 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
 }
 
 /* raytrace.rs:261-267 */
-static col ray_color(ctx_t* c, const ray_t* ray, double sig, uint32_t depth) {
+static col ray_color(ctx_t* c, const ray_t* ray, double sig, uint32_t depth, uint64_t key) {
     hit_t h = scene_intersect(c, ray);
     if (!h.hit) return cfrom3(c->s->background);       /* raytrace.rs:228-232 */
-    return shade(c, &c->s->objects[h.obj], &h, ray, sig, depth);
+    return shade(c, &c->s->objects[h.obj], &h, ray, sig, depth, key);
 }
 
 /* camera.rs:51-73 */
@@ -377,7 +414,7 @@ static inline v3 mat_mul(const double* m, v3 p) {
 }
 
 /* camera.rs:76-80 (simple) and camera.rs:109-122 (depth of field) */
-static ray_t camera_project(ctx_t* c, double px, double py) {
+static ray_t camera_project(ctx_t* c, double px, double py, uint64_t key) {
     ray_t r;
     v3 dir = mat_mul(c->cam_m, V(px, py, 1.0));
     if (!c->s->camera.dof) {
@@ -386,8 +423,8 @@ static ray_t camera_project(ctx_t* c, double px, double py) {
     }
     v3 ip = vadd(c->cam_pos, dir);
     v3 fp = vadd(c->cam_pos, vmul(dir, c->s->camera.focus / c->cam_im_dist));
-    double theta = rng_f64(&c->rng) * (2.0 * PI_);
-    double r2 = rng_closed01(&c->rng);
+    double theta = draw_f64(c, key, 0) * (2.0 * PI_);
+    double r2 = c->keyed ? key_closed01(key, 1) : rng_closed01(&c->rng);
     double rad = sqrt(r2) * c->s->camera.aperture;
     v3 orig = vadd(ip, mat_mul(c->cam_m, V(cos(theta) * rad, sin(theta) * rad, 0.0)));
     r.origin = orig; r.direction = normalize(vsub(fp, orig));
@@ -469,6 +506,7 @@ static void* worker(void* arg) {
     const ref_scene* s = jb->s; const ref_opts* o = jb->o;
     ctx_t c; memset(&c, 0, sizeof c);
     c.s = s; c.max_depth = o->max_depth;
+    c.keyed = o->rng == REF_RNG_KEYED;
     double cpos[3];
     ref_camera_build(&s->camera, cpos, c.cam_m);
     c.cam_pos = from3(cpos);
@@ -488,18 +526,21 @@ static void* worker(void* arg) {
         rng_seed(&c.rng, o->seed * 0x100000001B3ull + y);
         for (uint32_t i = 0; i < o->tile_w; ++i) {
             uint32_t x = o->x0 + i;
+            const uint64_t kp = key_pixel(o->seed, x, y);
             col res = BLACK;
             for (uint32_t k = 0; k < aa; ++k) {
+                const uint64_t ka = key_child(kp, k);
                 double jx, jy;
                 if (o->jitter == REF_JITTER_CENTER) { jx = 0.5; jy = 0.5; }
-                else { jx = rng_f64(&c.rng); jy = rng_f64(&c.rng); }   /* x drawn before y */
+                else { jx = draw_f64(&c, ka, 0); jy = draw_f64(&c, ka, 1); }   /* x drawn before y */
                 double px = (((double)x + jx) - hw) * scale;
                 double py = (((double)y + jy) - hh) * scale;
                 /* raytrace.rs:270-276 */
                 col r = BLACK;
                 for (uint32_t cs = 0; cs < cam_samples; ++cs) {
-                    ray_t ray = camera_project(&c, px, py);
-                    r = cadd(r, ray_color(&c, &ray, 1.0, 0));
+                    const uint64_t kc = key_child(ka, cs);
+                    ray_t ray = camera_project(&c, px, py, kc);
+                    r = cadd(r, ray_color(&c, &ray, 1.0, 0, kc));
                 }
                 r = cdiv(r, (double)cam_samples);
                 res = cadd(res, r);

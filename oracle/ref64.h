@@ -80,6 +80,14 @@ typedef struct {
 } ref_scene;
 
 enum { REF_JITTER_CENTER = 0, REF_JITTER_RANDOM = 1 };
+/* Where the random draws come from.  XORSHIFT: the reference's rand 0.3
+ * XorShiftRng consumed sequentially (per row here; the reference seeds it from
+ * OS entropy, main.rs:43, so only its distribution is reproducible).  KEYED:
+ * a counter-based stream keyed on the draw's place in the recursion (pixel,
+ * AA sample, camera sample, path through the ray tree, draw id) -- the same
+ * specification the device path implements (trace_common.hpp "keyed RNG"),
+ * so device and oracle agree draw for draw, in any traversal order. */
+enum { REF_RNG_XORSHIFT = 0, REF_RNG_KEYED = 1 };
 
 typedef struct {
     uint32_t max_depth;      /* reference MAX_DEPTH = 4 (raytrace.rs:18) */
@@ -89,6 +97,7 @@ typedef struct {
     uint32_t y0, tile_h;     /* local row j -> global row y0 + ((j/band)*stride + phase)*band + j%band */
     uint32_t band, band_stride, band_phase;
     int32_t threads;         /* <=0: all online CPUs */
+    int32_t rng;             /* REF_RNG_XORSHIFT / REF_RNG_KEYED */
 } ref_opts;
 
 typedef struct {

@@ -45,7 +45,7 @@ class ref_opts(C.Structure):
     _fields_ = [("max_depth", C.c_uint32), ("jitter", C.c_int32), ("seed", C.c_uint64),
                 ("x0", C.c_uint32), ("tile_w", C.c_uint32), ("y0", C.c_uint32), ("tile_h", C.c_uint32),
                 ("band", C.c_uint32), ("band_stride", C.c_uint32), ("band_phase", C.c_uint32),
-                ("threads", C.c_int32)]
+                ("threads", C.c_int32), ("rng", C.c_int32)]
 
 
 class ref_counts(C.Structure):
@@ -151,14 +151,16 @@ class OracleScene:
 
 
 def render(spec, *, max_depth=None, x0=0, tile_w=None, y0=0, tile_h=None, band=1, band_stride=1,
-           band_phase=0, jitter=0, seed=1, threads=0, want_rgb64=True):
-    """Render a tile with the oracle -> dict(rgb64, rgb32, bgr, counts)."""
+           band_phase=0, jitter=0, seed=1, threads=0, want_rgb64=True, rng=0):
+    """Render a tile with the oracle -> dict(rgb64, rgb32, bgr, counts).
+    jitter: 0 centre, 1 random; rng: 0 XorShift (the reference's generator,
+    sequential), 1 keyed (the device's counter-based specification)."""
     sc = OracleScene(spec)
     tw = spec.width - x0 if tile_w is None else tile_w
     th = spec.height - y0 if tile_h is None else tile_h
     o = ref_opts(max_depth=spec.max_depth if max_depth is None else max_depth, jitter=jitter, seed=seed,
                  x0=x0, tile_w=tw, y0=y0, tile_h=th, band=band, band_stride=band_stride,
-                 band_phase=band_phase, threads=threads)
+                 band_phase=band_phase, threads=threads, rng=rng)
     rgb64 = np.zeros((th, tw, 3), np.float64) if want_rgb64 else None
     rgb32 = np.zeros((th, tw, 3), np.float32)
     pitch = 3 * tw

@@ -19,6 +19,7 @@ import pytest
 
 from oracle import ref64
 from libraytrace import scenes
+from cornell import check_out_bmp_statistics, cornell_spec
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -157,7 +158,8 @@ def test_ray_counts_follow_the_recursion():
 
 
 @pytest.mark.slow
-def test_indirect_phong_statistics():
+@pytest.mark.parametrize("rng", [0, 1], ids=["xorshift", "keyed"])
+def test_indirect_phong_statistics(rng):
     """Statistical parity with out.bmp (test_scene.txt, IndirectPhong, no lights).
 
     The reference render is 800x800 at 1024 spp with an OS-seeded RNG; we render
@@ -165,32 +167,8 @@ def test_indirect_phong_statistics():
     at the same 1024 spp and compare 8x8 block means of the sRGB bytes.
     Measured here: RMS 0.76 LSB, max 3.3 LSB over the 192 block-channel means
     (at 256 spp the sRGB curve's response to the 2x larger per-pixel noise
-    biases every block by -1.7 LSB, which is why the spp must match)."""
-    st = json.load(open(os.path.join(GOLD, "out_bmp_stats.json")))
-    spec = scenes.SceneSpec(width=200, height=200, antialias=1024, max_depth=4,
-                            background=(0.051, 0.051, 0.051),
-                            camera={"ctor": "new", "position": (0, 3, 17), "look": (0, 0, -1),
-                                    "up": (0, 1, 0), "im_dist": 3.6})
-    white = {"kind": "indirect_phong", "diffuse": (1, 1, 1), "specular": (0, 0, 0), "exponent": 1.0,
-             "ambient": (0, 0, 0), "samples": 1}
-    red = dict(white, diffuse=(1, 0, 0))
-    green = dict(white, diffuse=(0, 1, 0))
-    lamp = dict(white, ambient=(5, 5, 5))
-    spec.plane((0, 0, -3), (0, 0, 1), white)
-    spec.plane((0, 0, 0), (0, 1.0, 0), white)
-    spec.plane((0, 6, 0), (0, -1.0, 0), white)
-    spec.plane((-3, 0, 0), (1, 0, 0), red)
-    spec.plane((3, 0, 0), (-1, 0, 0), green)
-    spec.sphere((0, 1.5, 0), 1.5, white)
-    spec.sphere((0, 10.65, 0), 5, lamp)
-    out = ref64.render(spec, jitter=1, seed=12345, want_rgb64=False)
-    bgr = out["bgr"].reshape(200, 200, 3).astype(np.float64)
-    grid = bgr.reshape(8, 25, 8, 25, 3).mean(axis=(1, 3))
-    gold = np.array(st["grid"])
-    err = grid - gold
-    assert np.abs(err).max() < 4.5, np.abs(err).max()
-    assert np.sqrt((err ** 2).mean()) < 1.2
-    assert np.abs(grid.mean(axis=(0, 1)) - np.array(st["mean_bgr"])).max() < 1.0
-    # red wall on the left, green on the right (camera handedness, camera.rs:52)
-    assert grid[:, 0, 2].mean() > grid[:, 0, 1].mean() + 20
-    assert grid[:, 7, 1].mean() > grid[:, 7, 2].mean() + 20
+    biases every block by -1.7 LSB, which is why the spp must match).
+    rng=1: the keyed counter-based generator the device path uses must pass
+    the same check as the reference's own XorShift."""
+    out = ref64.render(cornell_spec(), jitter=1, seed=12345, want_rgb64=False, rng=rng)
+    check_out_bmp_statistics(out["bgr"])

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum rt_status {
     RT_OK = 0,
@@ -136,7 +136,10 @@ const char* rt_last_error(const rt_ctx* ctx);
  * not implement -> RT_E_UNSUPPORTED. */
 int rt_scene_upload(rt_ctx* ctx, const rt_scene* scene);
 
-enum rt_jitter { RT_JITTER_CENTER = 0 };   /* jx = jy = 0.5 (deterministic parity mode, main.rs:51-52) */
+enum rt_jitter {
+    RT_JITTER_CENTER = 0,   /* jx = jy = 0.5 (deterministic parity mode, main.rs:51-52) */
+    RT_JITTER_RANDOM = 1    /* jx, jy drawn per AA sample (main.rs:51-52) from the keyed RNG (rt_render_opts.seed) */
+};
 enum rt_out_flags {
     RT_OUT_RGB_F32 = 1,
     RT_OUT_BGR_U8 = 2,
@@ -148,7 +151,10 @@ enum rt_algo {
     RT_ALGO_BRUTE_LDS = 1,      /* megakernel, sphere list staged in LDS */
     RT_ALGO_BRUTE_GLOBAL = 2,   /* megakernel, sphere list read through the caches */
     RT_ALGO_WAVEFRONT = 3,      /* per-depth launches over compacted ray queues, sphere BVH (default) */
-    RT_ALGO_WAVEFRONT_BRUTE = 4 /* the same schedule, every sphere tested (linear scan like scene.rs:248) */
+    RT_ALGO_WAVEFRONT_BRUTE = 4, /* the same schedule, every sphere tested (linear scan like scene.rs:248) */
+    RT_ALGO_PATH = 5            /* per-pixel recursion over an HBM stack: every material / light / camera class
+                                   (IndirectPhong, Transparent, AreaLight, DepthOfField, random jitter); AUTO picks
+                                   it whenever the scene or the jitter mode needs it */
 };
 
 typedef struct {
@@ -163,6 +169,10 @@ typedef struct {
     int32_t algo;             /* rt_algo */
     uint32_t bgr_pitch;       /* bytes per output BGR row; 0 -> 3*tile_w */
     uint32_t _pad;
+    uint64_t seed;            /* keyed RNG seed: every random draw is a function of (seed, pixel, AA sample,
+                                 camera sample, path through the ray tree, draw id), so a frame is
+                                 reproducible and independent of tiling and GPU count.  The reference
+                                 seeds one sequential XorShift stream from OS entropy (main.rs:43). */
 } rt_render_opts;
 
 #define RT_MAX_DEPTH_LIMIT 30

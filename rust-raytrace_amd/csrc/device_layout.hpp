@@ -22,7 +22,9 @@ struct DevPlane {
 
 // Per OBJECT (indexed by file-order object id), only what shading reads.
 constexpr int32_t kMatPhong = 0;      // DevMaterial::kind (= rt_material_kind)
+constexpr int32_t kMatIndirect = 1;   // IndirectPhongMaterial (path kernel only)
 constexpr int32_t kMatFresnel = 2;
+constexpr int32_t kMatTransparent = 3;   // TransparentMaterial (path kernel only)
 
 // What the fold and the significance tests read (ks, ks_sig, kind) shares the
 // first 64-B line.
@@ -30,15 +32,17 @@ struct alignas(64) DevMaterial {
     double ks[3];
     double ks_sig;                  // Color::significance, color.rs:637-639
     int32_t kind;                   // rt_material_kind
-    int32_t _pad;
+    uint32_t samples;               // IndirectPhongMaterial::samples
     double kd_sig;
     double ior;
     double kd[3], amb[3];
     double exponent;
 };
 
+constexpr int32_t kLightArea = 2;     // DevLight::kind (= rt_light_kind)
+
 struct DevLight {
-    double v[3];                    // point: location; directional: direction
+    double v[9];                    // point: location; directional: direction; area: origin, side1, side2
     double color[3];
     int32_t kind;                   // rt_light_kind
     int32_t _pad;
@@ -99,6 +103,11 @@ struct DevScene {
     int32_t bvh4_root, n_bvh4;
     const DevCamNode* cam_nodes;    // camera view of the binary BVH (null: generation 0 traverses per ray)
     int32_t has_fresnel;            // some object uses FresnelMaterial
+    int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,
+                                    // AreaLight, DepthOfFieldCamera)
+    int32_t cam_dof;                // DepthOfFieldCamera (camera.rs:83-123)
+    uint32_t cam_samples;           // Camera::samples() (1 for the simple camera)
+    double cam_focus, cam_aperture, cam_im_dist;   // DepthOfFieldCamera focus, aperture, im_dist (camera.rs:98)
     double cam_pos[3];
     double cam_m[9];                // row-major
     double bg[3];
@@ -116,7 +125,11 @@ struct FrameParams {
     unsigned long long* counters;   // [kCounterShards] rays, then [kCounterShards] shadow rays
     float bg_rgb[3];                // output of a pixel whose camera ray misses: the background
     uint8_t bg_bgr[3];              //   averaged over spp (main.rs:56), f32 and sRGB B,G,R (host-computed)
+    int32_t jitter;                 // rt_jitter: 0 centre, 1 keyed random draws (path kernel)
+    uint64_t seed;                  // keyed RNG seed (path kernel)
+    const double* srgb;             // the 255 sRGB thresholds in HBM (path kernel stages them in LDS)
 };
+
 
 constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (camera ray missed)
 
@@ -125,6 +138,31 @@ constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (ca
 #else
 #define RT_HD
 #endif
+
+// Recursion stack of the path kernel: one frame per depth 0..max_depth for
+// every work-item of the (persistent) grid, SoA so a wave's lanes at the same
+// depth touch consecutive 8-B words: f64 fields [level][kPathF][T], then the
+// key [level][T], then i32 fields [level][kPathI][T].
+constexpr int kPathF = 17;            // point 3, normal 3, direction 3, significance, colour 3, factor, aux 3
+constexpr int kPathI = 3;             // object, next child, flags
+struct PathStack {
+    unsigned char* mem;
+    uint32_t T;                       // work-items of the grid (stride of every field)
+    uint32_t levels;
+    RT_HD double* f(int level, int field) const {
+        return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(level) * kPathF + field) * T;
+    }
+    RT_HD uint64_t* key(int level) const {
+        return reinterpret_cast<uint64_t*>(mem) + static_cast<uint64_t>(levels) * kPathF * T + static_cast<uint64_t>(level) * T;
+    }
+    RT_HD int32_t* i(int level, int field) const {
+        return reinterpret_cast<int32_t*>(reinterpret_cast<uint64_t*>(mem) + static_cast<uint64_t>(levels) * (kPathF + 1) * T) +
+               (static_cast<uint64_t>(level) * kPathI + field) * T;
+    }
+    static uint64_t bytes(uint32_t T, uint32_t levels) {
+        return static_cast<uint64_t>(levels) * T * ((kPathF + 1) * 8 + kPathI * 4);
+    }
+};
 
 // Wavefront working set for one chunk of a tile (HBM; sized by the host for
 // `cap` pixels / `slots` generation-0 slots; 288 GB leaves room).

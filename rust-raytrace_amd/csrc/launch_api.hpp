@@ -80,4 +80,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
 
+// The general path (path_kernel.hip): every material / light / camera class,
+// keyed random draws, one work-item per pixel over the HBM recursion stack.
+// staged: binary BVH + spheres in LDS (path_lds_bytes(sc, true) must fit).
+size_t path_lds_bytes(const DevScene& sc, bool staged);
+hipError_t launch_path(const DevScene& sc, const FrameParams& fp, const PathStack& st, bool staged, hipStream_t stream);
+
 }  // namespace rtamd

@@ -1,0 +1,379 @@
+// The general path on CDNA4 (gfx950): every material, light and camera class
+// of the reference, including the stochastic and branching ones the
+// wavefront chain does not carry:
+//   IndirectPhongMaterial  raytrace.rs:69-121   `samples` children per hit
+//   TransparentMaterial    raytrace.rs:169-226  reflection + refraction children
+//   AreaLight              scene.rs:142-155     keyed light position per hit
+//   DepthOfFieldCamera     camera.rs:83-123     `samples` lens samples per AA sample
+//   random AA jitter       main.rs:51-52        keyed (x, y) offset per AA sample
+// plus Phong / Fresnel / point / directional exactly as the wavefront path.
+//
+// One work-item per pixel runs main.rs:45-56 (AA samples, camera samples)
+// and the whole ray_color recursion as a loop over an explicit stack: a hit
+// that spawns a child stores its frame (hit point, flipped normal, incoming
+// direction, significance, partial colour, material factors, path key) at
+// its depth and descends; a returning colour is folded into the parent's
+// partial colour in the reference's operation order (`res = res + term`,
+// child by child), and the parent spawns its next child or returns.  The
+// stack lives in HBM, SoA per depth, so the lanes of a wave at the same depth
+// read and write consecutive words.  Queries go through the sphere BVH (exact
+// f64 leaf tests, trace_common.hpp), staged in LDS when it fits.
+//
+// Every random draw is keyed on its place in the recursion (trace_common.hpp
+// "keyed RNG"), so the image does not depend on the schedule and the oracle's
+// REF_RNG_KEYED mode reproduces it draw for draw.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_layout.hpp"
+#include "launch_api.hpp"
+#include "trace_common.hpp"
+
+namespace rtamd {
+
+namespace {
+
+constexpr int kPathBlock = 256;
+constexpr double kPi = 3.14159265358979323846264338327950288;      // f64::consts::PI
+constexpr int32_t kFlDiffuse = 1, kFlSpecular = 2, kFlRefract = 4;
+
+__device__ __forceinline__ double clamp_one(double x) { return x > 1.0 ? 1.0 : x; }   // raytrace.rs:26-28
+
+// One level of the recursion: what PhongMaterial / IndirectPhongMaterial /
+// FresnelMaterial / TransparentMaterial::color holds across its child calls.
+struct Frame {
+    double ptx, pty, ptz;       // pt = ray.cast(t)
+    double nx, ny, nz;          // normal flipped toward the viewer
+    double dx, dy, dz;          // incoming ray direction
+    double sig;                 // significance the hit was reached with
+    Col res;                    // colour so far
+    double f;                   // Fresnel / Transparent: Schlick factor; Phong / IndirectPhong: 1
+    double ax, ay, az;          // Transparent: unnormalised refraction vector; IndirectPhong: current sample dir
+    uint64_t key;               // path key of the hit
+    int32_t obj, next, flags;   // object id, index of the child in flight, kFl* bits
+};
+
+__device__ __forceinline__ void store_frame(const PathStack& st, int L, uint32_t t, const Frame& F) {
+    const double v[kPathF] = {F.ptx, F.pty, F.ptz, F.nx, F.ny, F.nz, F.dx, F.dy, F.dz, F.sig,
+                              F.res.r, F.res.g, F.res.b, F.f, F.ax, F.ay, F.az};
+#pragma unroll
+    for (int k = 0; k < kPathF; ++k) st.f(L, k)[t] = v[k];
+    st.key(L)[t] = F.key;
+    st.i(L, 0)[t] = F.obj;
+    st.i(L, 1)[t] = F.next;
+    st.i(L, 2)[t] = F.flags;
+}
+
+// After a child returned: only the colour, the sample direction and the child index change.
+__device__ __forceinline__ void store_resume(const PathStack& st, int L, uint32_t t, const Frame& F) {
+    st.f(L, 10)[t] = F.res.r; st.f(L, 11)[t] = F.res.g; st.f(L, 12)[t] = F.res.b;
+    st.f(L, 14)[t] = F.ax; st.f(L, 15)[t] = F.ay; st.f(L, 16)[t] = F.az;
+    st.i(L, 1)[t] = F.next;
+}
+
+__device__ __forceinline__ Frame load_frame(const PathStack& st, int L, uint32_t t) {
+    double v[kPathF];
+#pragma unroll
+    for (int k = 0; k < kPathF; ++k) v[k] = st.f(L, k)[t];
+    Frame F;
+    F.ptx = v[0]; F.pty = v[1]; F.ptz = v[2];
+    F.nx = v[3]; F.ny = v[4]; F.nz = v[5];
+    F.dx = v[6]; F.dy = v[7]; F.dz = v[8];
+    F.sig = v[9];
+    F.res = Col{v[10], v[11], v[12]};
+    F.f = v[13];
+    F.ax = v[14]; F.ay = v[15]; F.az = v[16];
+    F.key = st.key(L)[t];
+    F.obj = st.i(L, 0)[t];
+    F.next = st.i(L, 1)[t];
+    F.flags = st.i(L, 2)[t];
+    return F;
+}
+
+// camera.rs:76-80 (simple) and camera.rs:109-122 (depth of field; theta and
+// r2 keyed on the camera sample).
+__device__ __forceinline__ Ray camera_project(const DevScene& sc, double px, double py, uint64_t kc) {
+    const double* M = sc.cam_m;
+    const double dx = M[0] * px + M[1] * py + M[2] * 1.0;
+    const double dy = M[3] * px + M[4] * py + M[5] * 1.0;
+    const double dz = M[6] * px + M[7] * py + M[8] * 1.0;
+    if (!sc.cam_dof) {
+        const double l = sqrt(dx * dx + dy * dy + dz * dz);
+        return Ray{sc.cam_pos[0], sc.cam_pos[1], sc.cam_pos[2], dx / l, dy / l, dz / l};
+    }
+    const double ipx = sc.cam_pos[0] + dx, ipy = sc.cam_pos[1] + dy, ipz = sc.cam_pos[2] + dz;     // image plane
+    const double s = sc.cam_focus / sc.cam_im_dist;
+    const double fpx = sc.cam_pos[0] + dx * s, fpy = sc.cam_pos[1] + dy * s, fpz = sc.cam_pos[2] + dz * s;   // focal point
+    const double theta = key_f64(kc, 0) * (2.0 * kPi);
+    const double r2 = key_closed01(kc, 1);
+    const double rad = sqrt(r2) * sc.cam_aperture;
+    const double vx = cos(theta) * rad, vy = sin(theta) * rad, vz = 0.0;
+    const double ox = ipx + ((M[0] * vx + M[1] * vy) + M[2] * vz);
+    const double oy = ipy + ((M[3] * vx + M[4] * vy) + M[5] * vz);
+    const double oz = ipz + ((M[6] * vx + M[7] * vy) + M[8] * vz);
+    const double ex = fpx - ox, ey = fpy - oy, ez = fpz - oz;
+    const double l = sqrt(ex * ex + ey * ey + ez * ez);
+    return Ray{ox, oy, oz, ex / l, ey / l, ez / l};
+}
+
+// The part of Material::color before any child call: flags, the Schlick
+// factor, Transparent's refraction vector, and the direct lighting with its
+// shadow queries (raytrace.rs:31-56, 69-97, 125-157, 171-211).
+template <int kNodes>
+__device__ void shade_hit(const DevScene& sc, const BvhView& v, const DevMaterial& m, const Ray& r, const Hit& h,
+                          double sig, uint64_t key, Frame& F, uint64_t& rays, uint64_t& shadows) {
+    F.ptx = r.ox + r.dx * h.t; F.pty = r.oy + r.dy * h.t; F.ptz = r.oz + r.dz * h.t;   // ray.cast(t)
+    double rnx, rny, rnz;
+    hit_normal(sc, v.sph, h.prim, F.ptx, F.pty, F.ptz, rnx, rny, rnz);
+    const double nd = rnx * r.dx + rny * r.dy + rnz * r.dz;
+    const bool flip = nd > 0.0;
+    F.nx = flip ? -rnx : rnx; F.ny = flip ? -rny : rny; F.nz = flip ? -rnz : rnz;
+    F.dx = r.dx; F.dy = r.dy; F.dz = r.dz;
+    F.sig = sig;
+    F.key = key;
+    F.obj = h.obj;
+    F.next = -1;
+    F.ax = F.ay = F.az = 0.0;
+    bool diffuse, specular;
+    if (m.kind == kMatTransparent) {                                   // raytrace.rs:171-195
+        F.res = Col{0.0, 0.0, 0.0};
+        const double n = flip ? m.ior : 1.0 / m.ior;
+        const double sin2 = (n * n) * (1.0 - nd * nd);
+        const bool refr = sin2 < 1.0;
+        if (refr) {
+            const double cs = sqrt(1.0 - sin2);
+            const double k = n * fabs(nd) + cs;
+            F.ax = r.dx * n - F.nx * k; F.ay = r.dy * n - F.ny * k; F.az = r.dz * n - F.nz * k;
+        }
+        double r0 = (m.ior - 1.0) / (m.ior + 1.0);
+        r0 = r0 * r0;
+        const double omcos = flip ? (refr ? 1.0 - (F.nx * F.ax + F.ny * F.ay + F.nz * F.az) : 0.0) : 1.0 - fabs(nd);
+        const double omcos2 = omcos * omcos;
+        F.f = refr ? clamp_one(r0 + (((1.0 - r0) * omcos2) * omcos2) * omcos) : 1.0;
+        diffuse = false;
+        specular = (m.ks_sig * F.f) * sig > kMinSignificance;
+        F.flags = (specular ? kFlSpecular : 0) | (refr ? kFlRefract : 0);
+    } else {
+        F.res = Col{m.amb[0], m.amb[1], m.amb[2]};
+        const Shading s = shading_flags<true>(m, sig, nd);             // f = 1 unless Fresnel
+        F.f = s.f;
+        diffuse = s.diffuse;
+        specular = s.specular;
+        F.flags = (diffuse ? kFlDiffuse : 0) | (specular ? kFlSpecular : 0);
+    }
+    if (!(diffuse || specular)) return;
+    const int32_t hint = h.prim >= 0 ? h.prim : -1;                    // the sphere the point lies on
+    for (int l = 0; l < sc.n_lights; ++l) {
+        const DevLight& Lt = sc.lights[l];
+        double lx, ly, lz, r2;
+        const bool has_range = light_dir_keyed(Lt, l, key, F.ptx, F.pty, F.ptz, lx, ly, lz, r2);
+        const Ray sray{F.ptx + lx * kEps, F.pty + ly * kEps, F.ptz + lz * kEps, lx, ly, lz};
+        ++rays;
+        ++shadows;
+        if (occluded_bvh<false, kNodes, 0>(sc, v, sray, has_range, r2, hint)) continue;
+        add_light(F.res, m, Lt, diffuse, specular, F.f, lx, ly, lz, F.nx, F.ny, F.nz, F.dx, F.dy, F.dz);
+    }
+}
+
+// The first child ray of frame F with index >= i, or -1: its ray and
+// significance (raytrace.rs:58-64, 98-106, 159-164, 212-224).
+__device__ __forceinline__ int next_child(Frame& F, const DevMaterial& m, int i, Ray& cr, double& csig) {
+    const bool specular = (F.flags & kFlSpecular) != 0;
+    if (m.kind == kMatIndirect) {
+        if (i >= static_cast<int>(m.samples) || !(F.flags & (kFlDiffuse | kFlSpecular))) return -1;
+        const double r1 = key_f64(F.key, 128u + 2u * static_cast<uint32_t>(i)) * 2.0 - 1.0;
+        const double r2 = key_f64(F.key, 129u + 2u * static_cast<uint32_t>(i)) * (2.0 * kPi);
+        const double sin_theta = 1.0 - r1 * r1;                        // sic: no sqrt (raytrace.rs:103)
+        const double x = sin_theta * cos(r2), z = sin_theta * sin(r2);
+        const bool keep = (x * F.nx + r1 * F.ny + z * F.nz) >= 0.0;
+        F.ax = keep ? x : -x; F.ay = keep ? r1 : -r1; F.az = keep ? z : -z;
+        cr = Ray{F.ptx + F.ax * kEps, F.pty + F.ay * kEps, F.ptz + F.az * kEps, F.ax, F.ay, F.az};
+        csig = F.sig;                                                 // significance passed unchanged
+        return i;
+    }
+    if (i == 0 && specular) {                                          // mirror reflection
+        cr = reflect_ray(Ray{0.0, 0.0, 0.0, F.dx, F.dy, F.dz}, F.ptx, F.pty, F.ptz, F.nx, F.ny, F.nz);
+        csig = (F.f * F.sig) * m.ks_sig;                               // Phong: (1 * sig) * ks_sig == sig * ks_sig
+        return 0;
+    }
+    if (m.kind == kMatTransparent && i <= 1 && F.f < 1.0 && (F.flags & kFlRefract)) {   // raytrace.rs:216-224
+        const double omf = clamp_one(1.0 - F.f);
+        const double l = sqrt(F.ax * F.ax + F.ay * F.ay + F.az * F.az);
+        const double rx = F.ax / l, ry = F.ay / l, rz = F.az / l;
+        cr = Ray{F.ptx + rx * kEps, F.pty + ry * kEps, F.ptz + rz * kEps, rx, ry, rz};
+        csig = omf * F.sig;
+        return 1;
+    }
+    return -1;
+}
+
+// Fold the colour c of child F.next into F.res (the `res = res + ...` lines).
+__device__ __forceinline__ void fold_child(Frame& F, const DevMaterial& m, const Col& c) {
+    if (m.kind == kMatIndirect) {                                      // raytrace.rs:107-118
+        const double fac = static_cast<double>(m.samples) * 0.5;
+        if (F.flags & kFlDiffuse) {
+            const double d = F.nx * F.ax + F.ny * F.ay + F.nz * F.az;
+            F.res.r = F.res.r + ((m.kd[0] * c.r) * d) / fac;
+            F.res.g = F.res.g + ((m.kd[1] * c.g) * d) / fac;
+            F.res.b = F.res.b + ((m.kd[2] * c.b) * d) / fac;
+        }
+        if (F.flags & kFlSpecular) {       // sic: (dir - ray.direction) with ray the NEW ray: 0/0 (raytrace.rs:108,115)
+            const double hx = F.ax - F.ax, hy = F.ay - F.ay, hz = F.az - F.az;
+            const double hl = sqrt(hx * hx + hy * hy + hz * hz);
+            const double p = pow(clamp_zero(F.nx * (hx / hl) + F.ny * (hy / hl) + F.nz * (hz / hl)), m.exponent);
+            F.res.r = F.res.r + ((m.ks[0] * c.r) * p) / fac;
+            F.res.g = F.res.g + ((m.ks[1] * c.g) * p) / fac;
+            F.res.b = F.res.b + ((m.ks[2] * c.b) * p) / fac;
+        }
+        return;
+    }
+    if (F.next == 0) {                      // reflection: res + (ks * child) * f  (raytrace.rs:63 / 163 / 214)
+        F.res.r = F.res.r + (m.ks[0] * c.r) * F.f;
+        F.res.g = F.res.g + (m.ks[1] * c.g) * F.f;
+        F.res.b = F.res.b + (m.ks[2] * c.b) * F.f;
+    } else {                                // refraction: res + child * omf  (raytrace.rs:222)
+        const double omf = clamp_one(1.0 - F.f);
+        F.res.r = F.res.r + c.r * omf;
+        F.res.g = F.res.g + c.g * omf;
+        F.res.b = F.res.b + c.b * omf;
+    }
+}
+
+// ray_color(camera ray, 1.0, 0, key) -- raytrace.rs:261-267 -- with the
+// recursion unrolled over the HBM stack (levels 0 .. max_depth hold frames).
+template <int kNodes>
+__device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParams& fp, const PathStack& st, uint32_t t,
+                          Ray ray, uint64_t key, uint64_t& rays, uint64_t& shadows) {
+    double sig = 1.0;
+    int L = 0;
+    for (;;) {
+        Col c;
+        const Hit h = nearest_bvh<false, kNodes, 0>(sc, v, ray);
+        ++rays;
+        Frame F;
+        Ray cr;
+        double csig = 0.0;
+        int child = -1;
+        if (h.obj == INT32_MAX) {
+            c = Col{sc.bg[0], sc.bg[1], sc.bg[2]};                     // SolidColorBackground (raytrace.rs:228-232)
+        } else {
+            const DevMaterial& m = sc.mats[h.obj];
+            if (static_cast<uint32_t>(L) > fp.max_depth) {             // raytrace.rs:33 / 72 / 126 / 172
+                c = m.kind == kMatTransparent ? Col{0.0, 0.0, 0.0} : Col{m.amb[0], m.amb[1], m.amb[2]};
+            } else {
+                shade_hit<kNodes>(sc, v, m, ray, h, sig, key, F, rays, shadows);
+                child = next_child(F, m, 0, cr, csig);
+                c = F.res;
+            }
+        }
+        if (child >= 0) {                                              // descend
+            F.next = child;
+            store_frame(st, L, t, F);
+            ray = cr;
+            sig = csig;
+            key = key_child(F.key, static_cast<uint64_t>(child));
+            ++L;
+            continue;
+        }
+        bool resumed = false;                                          // return c to the parents
+        while (L > 0) {
+            --L;
+            Frame P = load_frame(st, L, t);
+            const DevMaterial& m = sc.mats[P.obj];
+            fold_child(P, m, c);
+            const int nx = next_child(P, m, P.next + 1, cr, csig);
+            if (nx >= 0) {
+                P.next = nx;
+                store_resume(st, L, t, P);
+                ray = cr;
+                sig = csig;
+                key = key_child(P.key, static_cast<uint64_t>(nx));
+                ++L;
+                resumed = true;
+                break;
+            }
+            c = P.res;
+        }
+        if (!resumed) return c;
+    }
+}
+
+// kNodes: 2 = binary BVH, spheres and object ids staged in LDS; 0 = read through the caches.
+template <int kNodes>
+__global__ __launch_bounds__(kPathBlock, 4) void path_kernel(DevScene sc, FrameParams fp, PathStack st) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    double* s_srgb = reinterpret_cast<double*>(lds);
+    for (int i = threadIdx.x; i < 255; i += kPathBlock) s_srgb[i] = fp.srgb[i];
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, sc.cam_nodes, nullptr};
+    if constexpr (kNodes == 2) {
+        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds + 2048);
+        for (int i = threadIdx.x; i < sc.n_bvh; i += kPathBlock) ln[i] = sc.bvh[i];
+        DevSphere* ls = reinterpret_cast<DevSphere*>(ln + sc.n_bvh);
+        int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
+        for (int i = threadIdx.x; i < sc.n_spheres; i += kPathBlock) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
+        v.lnodes = ln;
+        v.nl = sc.n_bvh;
+        v.sph = ls;
+        v.obj = lo;
+    }
+    __syncthreads();
+    const uint32_t t = blockIdx.x * kPathBlock + threadIdx.x;
+    const uint64_t npix = static_cast<uint64_t>(fp.tile_w) * fp.rows;
+    uint64_t rays = 0, shadows = 0;
+    const double ns = static_cast<double>(sc.cam_samples), aa = static_cast<double>(fp.spp);
+    for (uint64_t p = t; p < npix; p += st.T) {                        // main.rs:45-56
+        const uint32_t lx = static_cast<uint32_t>(p % fp.tile_w);
+        const uint32_t lr = fp.row0 + static_cast<uint32_t>(p / fp.tile_w);
+        const uint32_t x = fp.x0 + lx;
+        const uint32_t y = fp.y0 + ((lr / fp.band) * fp.band_stride + fp.band_phase) * fp.band + lr % fp.band;
+        const uint64_t kp = key_pixel(fp.seed, x, y);
+        Col res{0.0, 0.0, 0.0};
+        for (uint32_t a = 0; a < fp.spp; ++a) {
+            const uint64_t ka = key_child(kp, a);
+            const double jx = fp.jitter ? key_f64(ka, 0) : 0.5;       // x drawn before y (main.rs:51-52)
+            const double jy = fp.jitter ? key_f64(ka, 1) : 0.5;
+            const double px = ((static_cast<double>(x) + jx) - fp.hw) * fp.scale;
+            const double py = ((static_cast<double>(y) + jy) - fp.hh) * fp.scale;
+            Col r{0.0, 0.0, 0.0};                                      // raytrace.rs:270-276
+            for (uint32_t cs = 0; cs < sc.cam_samples; ++cs) {
+                const uint64_t kc = key_child(ka, cs);
+                const Col c = trace_path<kNodes>(sc, v, fp, st, t, camera_project(sc, px, py, kc), kc, rays, shadows);
+                r = Col{r.r + c.r, r.g + c.g, r.b + c.b};
+            }
+            r = Col{r.r / ns, r.g / ns, r.b / ns};
+            res = Col{res.r + r.r, res.g + r.g, res.b + r.b};
+        }
+        res = Col{res.r / aa, res.g / aa, res.b / aa};
+        write_pixel(fp, lx, lr, res, s_srgb);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        rays += __shfl_xor(rays, off, 64);
+        shadows += __shfl_xor(shadows, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        const uint32_t shard = (t >> 6) % kCounterShards;
+        atomicAdd(&fp.counters[shard], static_cast<unsigned long long>(rays));
+        atomicAdd(&fp.counters[kCounterShards + shard], static_cast<unsigned long long>(shadows));
+    }
+}
+
+}  // namespace
+
+size_t path_lds_bytes(const DevScene& sc, bool staged) {
+    size_t b = 2048;
+    if (staged) b += static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode) + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + 4);
+    return b;
+}
+
+hipError_t launch_path(const DevScene& sc, const FrameParams& fp, const PathStack& st, bool staged, hipStream_t stream) {
+    const uint64_t npix = static_cast<uint64_t>(fp.tile_w) * fp.rows;
+    const uint64_t want = (npix + kPathBlock - 1) / kPathBlock;
+    const dim3 grid(static_cast<uint32_t>(want < st.T / kPathBlock ? want : st.T / kPathBlock));
+    if (grid.x == 0) return hipSuccess;
+    if (staged) hipLaunchKernelGGL(path_kernel<2>, grid, dim3(kPathBlock), path_lds_bytes(sc, true), stream, sc, fp, st);
+    else hipLaunchKernelGGL(path_kernel<0>, grid, dim3(kPathBlock), path_lds_bytes(sc, false), stream, sc, fp, st);
+    return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -30,6 +30,9 @@ struct rt_ctx {
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
     unsigned long long* d_counters = nullptr;
+    double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
+    void* d_path = nullptr;           // path kernel recursion stack (PathStack)
+    size_t path_bytes = 0;
     float* d_rgb = nullptr;
     size_t rgb_cap = 0;
     uint8_t* d_bgr = nullptr;
@@ -87,7 +90,10 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 constexpr int kTotals = 2 * kCounterShards;
 constexpr int kGenTotals = kTotals + 8;
 constexpr int kCounterWords = kGenTotals + kCntWords;
-static_assert(kMatPhong == RT_MAT_PHONG && kMatFresnel == RT_MAT_FRESNEL, "DevMaterial::kind mirrors rt_material_kind");
+static_assert(kMatPhong == RT_MAT_PHONG && kMatFresnel == RT_MAT_FRESNEL && kMatIndirect == RT_MAT_INDIRECT_PHONG &&
+                  kMatTransparent == RT_MAT_TRANSPARENT,
+              "DevMaterial::kind mirrors rt_material_kind");
+static_assert(kLightArea == RT_LIGHT_AREA, "DevLight::kind mirrors rt_light_kind");
 // LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
 constexpr size_t kLdsBudget = 72 * 1024;
 
@@ -220,6 +226,8 @@ int rt_ctx_create(int device, rt_ctx** out) {
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_srgb, 255 * sizeof(double)) != hipSuccess ||
+        hipMemcpy(c->d_srgb, srgb_average_table(), 255 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         upload_srgb_table(srgb_average_table()) != hipSuccess)
         return cleanup(fail(nullptr, RT_E_HIP, "context initialisation failed"));
     *out = c;
@@ -232,6 +240,8 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_blob) (void)hipFree(c->d_blob);
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_srgb) (void)hipFree(c->d_srgb);
+    if (c->d_path) (void)hipFree(c->d_path);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_bgr) (void)hipFree(c->d_bgr);
     for (auto& L : c->lanes) {
@@ -258,12 +268,16 @@ const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : thread_
 int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
-    // The device path implements the deterministic Phong chain;
-    // the stochastic and branching classes are "next" rows (§8(f)).
-    if (s->camera.kind != RT_CAMERA_SIMPLE)
-        return fail(c, RT_E_UNSUPPORTED, "DepthOfFieldCamera is not implemented on the device path");
+    // Every class of the reference except SkyboxBackground (textures) has a
+    // device implementation: Phong / Fresnel chains on the wavefront path,
+    // the stochastic and branching classes on the path kernel (needs_path).
     if (s->background_kind != RT_BG_SOLID)
         return fail(c, RT_E_UNSUPPORTED, "only SolidColorBackground is implemented on the device path");
+    if (s->camera.kind != RT_CAMERA_SIMPLE && s->camera.kind != RT_CAMERA_DOF)
+        return fail(c, RT_E_INVALID, "bad camera kind");
+    if (s->camera.kind == RT_CAMERA_DOF && s->camera.samples == 0)
+        return fail(c, RT_E_INVALID, "DepthOfFieldCamera with 0 samples");
+    bool needs_path = s->camera.kind == RT_CAMERA_DOF;
     std::vector<DevSphere> spheres;
     std::vector<double> sx, sy, sz, srad;
     std::vector<int32_t> sphere_obj, plane_obj;
@@ -272,9 +286,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     std::vector<DevLight> lights;
     for (size_t i = 0; i < s->objects.size(); ++i) {
         const rt_object& o = s->objects[i];
-        if (o.material != RT_MAT_PHONG && o.material != RT_MAT_FRESNEL)
-            return fail(c, RT_E_UNSUPPORTED, "object " + std::to_string(i) +
-                                                 ": only PhongMaterial and FresnelMaterial are implemented on the device path");
+        if (o.material < RT_MAT_PHONG || o.material > RT_MAT_TRANSPARENT)
+            return fail(c, RT_E_INVALID, "object " + std::to_string(i) + ": bad material kind");
+        needs_path |= o.material == RT_MAT_INDIRECT_PHONG || o.material == RT_MAT_TRANSPARENT;
         if (o.shape == RT_SHAPE_SPHERE) {
             spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
             sphere_obj.push_back(static_cast<int32_t>(i));
@@ -295,13 +309,15 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
         m.ks_sig = significance(o.specular);
         m.ior = o.ior;
         m.kind = o.material;
+        m.samples = o.material == RT_MAT_INDIRECT_PHONG ? o.samples : 0;
     }
     for (size_t i = 0; i < s->lights.size(); ++i) {
         const rt_light& l = s->lights[i];
-        if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_DIRECTIONAL)
-            return fail(c, RT_E_UNSUPPORTED, "light " + std::to_string(i) + ": AreaLight is not implemented on the device path");
+        if (l.kind < RT_LIGHT_POINT || l.kind > RT_LIGHT_AREA)
+            return fail(c, RT_E_INVALID, "light " + std::to_string(i) + ": bad light kind");
+        needs_path |= l.kind == RT_LIGHT_AREA;
         DevLight d{};
-        for (int k = 0; k < 3; ++k) d.v[k] = l.v[k];
+        for (int k = 0; k < 9; ++k) d.v[k] = l.v[k];
         d.color[0] = l.color.r; d.color[1] = l.color.g; d.color[2] = l.color.b;
         d.kind = l.kind;
         lights.push_back(d);
@@ -385,6 +401,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.cam_nodes = reinterpret_cast<const DevCamNode*>(base + o_cam);
     d.has_fresnel = 0;
     for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
+    d.needs_path = needs_path ? 1 : 0;
+    d.cam_dof = s->camera.kind == RT_CAMERA_DOF ? 1 : 0;
+    d.cam_samples = d.cam_dof ? s->camera.samples : 1u;
+    d.cam_focus = s->camera.focus;
+    d.cam_aperture = s->camera.aperture;
+    {   // camera.rs:98: im_dist = (matrix * Vec3(0, 0, 1)).norm()
+        const double* M = s->camera.matrix;
+        const double zx = (M[0] * 0.0 + M[1] * 0.0) + M[2] * 1.0;
+        const double zy = (M[3] * 0.0 + M[4] * 0.0) + M[5] * 1.0;
+        const double zz = (M[6] * 0.0 + M[7] * 0.0) + M[8] * 1.0;
+        d.cam_im_dist = std::sqrt(zx * zx + zy * zy + zz * zz);
+    }
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
     for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
     d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;
@@ -395,7 +423,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
 static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_t& band, uint32_t& stride, uint32_t& pitch) {
     if (!o) return fail(c, RT_E_INVALID, "null opts");
     if (o->width == 0 || o->height == 0) return fail(c, RT_E_INVALID, "empty frame");
-    if (o->jitter != RT_JITTER_CENTER) return fail(c, RT_E_UNSUPPORTED, "only centre jitter is implemented on the device path");
+    if (o->jitter != RT_JITTER_CENTER && o->jitter != RT_JITTER_RANDOM) return fail(c, RT_E_INVALID, "bad jitter mode");
     if (o->max_depth > RT_MAX_DEPTH_LIMIT) return fail(c, RT_E_INVALID, "max_depth above RT_MAX_DEPTH_LIMIT");
     band = o->band ? o->band : 1;
     stride = o->band_stride ? o->band_stride : 1;
@@ -410,7 +438,7 @@ static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_
     if (spp == 0) return fail(c, RT_E_INVALID, "spp must be set (the scene's antialias value for reference behaviour)");
     pitch = o->bgr_pitch ? o->bgr_pitch : 3 * o->tile_w;
     if (pitch < 3 * o->tile_w) return fail(c, RT_E_INVALID, "bgr_pitch < 3*tile_w");
-    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_WAVEFRONT_BRUTE) return fail(c, RT_E_INVALID, "bad algo");
+    if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_PATH) return fail(c, RT_E_INVALID, "bad algo");
     return RT_OK;
 }
 
@@ -434,6 +462,9 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     fp.out_rgb = (o->flags & RT_OUT_RGB_F32) ? static_cast<float*>(d_rgb) : nullptr;
     fp.out_bgr = (o->flags & RT_OUT_BGR_U8) ? static_cast<uint8_t*>(d_bgr) : nullptr;
     fp.counters = c->d_counters;
+    fp.jitter = o->jitter;
+    fp.seed = o->seed;
+    fp.srgb = c->d_srgb;
     {
         // The background pixel exactly as average_samples + to_srgb produce it on the
         // device (same f64 operations): camera misses are written by wf_nearest directly.
@@ -454,7 +485,14 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     const size_t lds_bytes = static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere);
     const bool fits_lds = lds_bytes <= 64 * 1024;
     int mode = o->algo;
-    if (mode == RT_ALGO_AUTO) mode = c->dsc.n_lights <= 32 ? RT_ALGO_WAVEFRONT : (fits_lds ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL);
+    // the stochastic / branching classes and random jitter run on the path kernel only
+    const bool path_only = c->dsc.needs_path || o->jitter != RT_JITTER_CENTER;
+    if (mode == RT_ALGO_AUTO)
+        mode = path_only ? RT_ALGO_PATH
+                         : (c->dsc.n_lights <= 32 ? RT_ALGO_WAVEFRONT : (fits_lds ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL));
+    if (path_only && mode != RT_ALGO_PATH)
+        return fail(c, RT_E_UNSUPPORTED,
+                    "IndirectPhong / Transparent materials, AreaLight, DepthOfFieldCamera and random jitter need RT_ALGO_PATH");
     if (mode == RT_ALGO_BRUTE_LDS && lds_bytes > 160 * 1024)
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
     if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)
@@ -588,6 +626,29 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         }
         HIP_TRY(c, hipEventRecord(c->ev1, st));
         c->wf_used = true;
+    } else if (mode == RT_ALGO_PATH) {
+        // persistent grid: enough work-items to fill every CU; each owns one
+        // recursion stack of max_depth + 1 frames (PathStack)
+        const uint64_t npix = static_cast<uint64_t>(o->tile_w) * o->tile_h;
+        const uint32_t T_full = static_cast<uint32_t>(c->n_cu) * 2048u;
+        const uint32_t T = static_cast<uint32_t>(std::min<uint64_t>(T_full, (npix + 255) / 256 * 256));
+        PathStack ps{};
+        ps.T = T;
+        ps.levels = o->max_depth + 1;
+        const size_t need = PathStack::bytes(T, ps.levels);
+        if (need > c->path_bytes) {
+            HIP_TRY(c, hipStreamSynchronize(st));
+            if (c->d_path) (void)hipFree(c->d_path);
+            c->d_path = nullptr;
+            c->path_bytes = 0;
+            HIP_TRY(c, hipMalloc(&c->d_path, need));
+            c->path_bytes = need;
+        }
+        ps.mem = static_cast<unsigned char*>(c->d_path);
+        const bool staged = path_lds_bytes(c->dsc, true) <= 48 * 1024;
+        HIP_TRY(c, hipEventRecord(c->ev0, st));
+        HIP_TRY(c, launch_path(c->dsc, fp, ps, staged, st));
+        HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));

@@ -861,4 +861,54 @@ __device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, 
     }
 }
 
+// ---- keyed RNG --------------------------------------------------------------
+// The reference draws from ONE sequential XorShiftRng seeded from OS entropy
+// (main.rs:43): no run can be reproduced and the stream order is the serial
+// pixel loop's.  The device path instead makes every draw a pure function of
+// its place in the recursion, so any schedule gives the same image and the
+// oracle (oracle/ref64.c, REF_RNG_KEYED) reproduces it draw for draw:
+//   pixel      kp = mix(mix(seed) + (y << 32 | x))        (frame coordinates)
+//   AA sample  ka = child(kp, a)    jitter jx = f64(ka, 0), jy = f64(ka, 1)  (main.rs:51-52)
+//   camera     kc = child(ka, cs)   DoF theta = f64(kc, 0), r2 = closed01(kc, 1)  (camera.rs:115-117)
+//   a hit with path key K draws     AreaLight l: u = f64(K, 2+2l), w = f64(K, 3+2l)  (scene.rs:153)
+//                                   indirect sample i: f64(K, 128+2i), f64(K, 129+2i)  (raytrace.rs:101-102)
+//   child ray i of a hit has key child(K, i) (mirror reflection 0, refraction 1,
+//   indirect sample i).
+// f64 / closed01 follow rand 0.3's bit recipes (52 mantissa bits; 53 bits over 2^53 - 1).
+__device__ __forceinline__ uint64_t kmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t key_child(uint64_t k, uint64_t i) { return kmix(k + (i + 1) * 0x9E3779B97F4A7C15ull); }
+__device__ __forceinline__ uint64_t key_bits(uint64_t k, uint32_t id) {
+    return kmix(k ^ (static_cast<uint64_t>(id + 1) * 0xD1B54A32D192ED03ull));
+}
+__device__ __forceinline__ double key_f64(uint64_t k, uint32_t id) {
+    return __longlong_as_double(static_cast<long long>(0x3FF0000000000000ull | (key_bits(k, id) & 0xFFFFFFFFFFFFFull))) - 1.0;
+}
+__device__ __forceinline__ double key_closed01(uint64_t k, uint32_t id) {
+    return static_cast<double>(key_bits(k, id) >> 11) / 9007199254740991.0;
+}
+__device__ __forceinline__ uint64_t key_pixel(uint64_t seed, uint32_t x, uint32_t y) {
+    return kmix(kmix(seed) + ((static_cast<uint64_t>(y) << 32) | x));
+}
+
+// AreaLight (scene.rs:142-155): a PointLight at origin + side1*u + side2*w, u
+// drawn before w, both keyed on the hit's path key and the light's index.
+__device__ __forceinline__ bool light_dir_keyed(const DevLight& L, int l, uint64_t key, double ptx, double pty, double ptz,
+                                                double& lx, double& ly, double& lz, double& r2) {
+    if (L.kind != kLightArea) return light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
+    const double u = key_f64(key, 2u + 2u * static_cast<uint32_t>(l));
+    const double w = key_f64(key, 3u + 2u * static_cast<uint32_t>(l));
+    const double qx = (L.v[0] + L.v[3] * u) + L.v[6] * w;
+    const double qy = (L.v[1] + L.v[4] * u) + L.v[7] * w;
+    const double qz = (L.v[2] + L.v[5] * u) + L.v[8] * w;
+    const double vx = qx - ptx, vy = qy - pty, vz = qz - ptz;
+    r2 = vx * vx + vy * vy + vz * vz;
+    const double n = sqrt(r2);
+    lx = vx / n; ly = vy / n; lz = vz / n;
+    return true;
+}
+
 }  // namespace rtamd

@@ -31,6 +31,8 @@ RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
 RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK, RT_TIME_KERNELS = 1, 2, 4, 8
 KERNEL_FAMILIES = ("nearest", "occlusion", "shade", "fold", "tally", "camera", "shadow")   # rt_kernel_family
 RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL, RT_ALGO_WAVEFRONT, RT_ALGO_WAVEFRONT_BRUTE = 0, 1, 2, 3, 4
+RT_ALGO_PATH = 5
+RT_JITTER_CENTER, RT_JITTER_RANDOM = 0, 1
 RT_MAX_DEPTH_LIMIT = 30
 
 
@@ -71,7 +73,7 @@ class rt_render_opts(C.Structure):
                 ("y0", C.c_uint32), ("tile_h", C.c_uint32), ("band", C.c_uint32), ("band_stride", C.c_uint32),
                 ("band_phase", C.c_uint32), ("max_depth", C.c_uint32), ("spp", C.c_uint32),
                 ("jitter", C.c_int32), ("flags", C.c_uint32), ("algo", C.c_int32),
-                ("bgr_pitch", C.c_uint32), ("_pad", C.c_uint32)]
+                ("bgr_pitch", C.c_uint32), ("_pad", C.c_uint32), ("seed", C.c_uint64)]
 
 
 class rt_stats(C.Structure):

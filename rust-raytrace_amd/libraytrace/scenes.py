@@ -66,6 +66,18 @@ class SceneSpec:
         self.lights.append({"kind": "directional", "direction": tuple(direction), "color": tuple(color)})
         return self
 
+    def area_light(self, origin, side1, side2, color):
+        """AreaLight (scene.rs:142-155): a parallelogram sampled once per shading point."""
+        self.lights.append({"kind": "area", "origin": tuple(origin), "side1": tuple(side1), "side2": tuple(side2),
+                            "color": tuple(color)})
+        return self
+
+    def depth_of_field(self, focus_dist, aperture, samples):
+        """Wrap the camera in a DepthOfFieldCamera (camera.rs:83-123)."""
+        self.camera = dict(self.camera, dof=True, focus_dist=float(focus_dist), aperture=float(aperture),
+                           samples=int(samples))
+        return self
+
     # ---- reference grammar ----
     def to_text(self):
         out = ["{", "    objects: ["]
@@ -115,6 +127,17 @@ def fresnel(diffuse, specular, exponent, ambient, ior):
     """FresnelMaterial (raytrace.rs:123-167): Phong with a Schlick-weighted specular."""
     return {"kind": "fresnel", "diffuse": tuple(diffuse), "specular": tuple(specular),
             "exponent": float(exponent), "ambient": tuple(ambient), "ior": float(ior)}
+
+
+def indirect_phong(diffuse, specular, exponent, ambient, samples):
+    """IndirectPhongMaterial (raytrace.rs:69-121): Phong plus `samples` random bounce rays per hit."""
+    return {"kind": "indirect_phong", "diffuse": tuple(diffuse), "specular": tuple(specular),
+            "exponent": float(exponent), "ambient": tuple(ambient), "samples": int(samples)}
+
+
+def transparent(specular, exponent, ior):
+    """TransparentMaterial (raytrace.rs:169-226): Schlick-weighted reflection + refraction."""
+    return {"kind": "transparent", "specular": tuple(specular), "exponent": float(exponent), "ior": float(ior)}
 
 
 def _material_text(m):
@@ -190,6 +213,28 @@ def config2_fresnel(width=1920, height=1080, max_depth=6):
     s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), fresnel((0.6, 0.6, 0.6), (0.8, 0.8, 0.8), 16.0, (0.01, 0.01, 0.01), 1.33))
     _lights(s)
     s.directional_light((0.3, -1.0, -0.2), (0.3, 0.3, 0.35))
+    return s
+
+
+def stochastic(width=96, height=64, antialias=4, max_depth=4, samples=2, dof=False, area=True):
+    """Every stochastic / branching class of the reference in one scene (SURVEY.md
+    §8(f) rows 3-4): glass (Transparent) and IndirectPhong spheres next to Phong and
+    Fresnel ones, a ground plane, a point and an AreaLight, optionally a
+    DepthOfFieldCamera.  Rendered with random jitter by the tests."""
+    s = SceneSpec(width=width, height=height, antialias=antialias, max_depth=max_depth, name="stoch",
+                  camera=dict(DEFAULT_CAMERA), background=(0.1, 0.12, 0.15))
+    s.sphere((-2.5, 1.0, -6.0), 1.0, transparent((0.9, 0.9, 0.9), 64.0, 1.5))
+    s.sphere((0.0, 1.0, -7.0), 1.0, indirect_phong((0.7, 0.3, 0.2), (0.0, 0.0, 0.0), 1.0, (0.02, 0.01, 0.0), samples))
+    s.sphere((2.5, 1.0, -6.0), 1.0, fresnel((0.2, 0.3, 0.7), (0.9, 0.9, 0.9), 64.0, (0.0, 0.01, 0.02), 1.6))
+    s.sphere((1.0, 0.5, -4.0), 0.5, phong((0.3, 0.8, 0.3), (0.3, 0.3, 0.3), 32.0, (0.0, 0.02, 0.0)))
+    s.sphere((-1.0, 0.4, -3.5), 0.4, transparent((1.0, 1.0, 1.0), 128.0, 1.33))
+    s.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), indirect_phong((0.6, 0.6, 0.6), (0.0, 0.0, 0.0), 1.0,
+                                                             (0.01, 0.01, 0.01), 1))
+    s.point_light((-10.0, 10.0, 5.0), (0.7, 0.7, 0.7))
+    if area:
+        s.area_light((3.0, 8.0, -2.0), (2.0, 0.0, 0.0), (0.0, 0.0, 2.0), (0.6, 0.55, 0.5))
+    if dof:
+        s.depth_of_field(7.0, 0.15, 2)
     return s
 
 

@@ -224,15 +224,25 @@ def test_sharded_frame_is_bit_identical(gpu_ctx):
         assert rays == full[2].rays
 
 
-def test_unsupported_classes_fail_loudly(gpu_ctx):
-    text = open(os.path.join(GOLD, "test_scene.txt")).read()      # IndirectPhongMaterial
-    with pytest.raises(lr.RtError) as e:
-        gpu_ctx.upload(lr.Scene.deserialize(text))
-    assert e.value.code == lr.RT_E_UNSUPPORTED
+def test_stochastic_classes_need_the_path_kernel(gpu_ctx):
+    """test_scene.txt (IndirectPhongMaterial) and a DepthOfFieldCamera upload, but
+    only the path kernel renders them: the chain algorithms fail loudly."""
+    text = open(os.path.join(GOLD, "test_scene.txt")).read()
+    gpu_ctx.upload(lr.Scene.deserialize(text))
+    o = lr.render_opts(16, 16, spp=1, max_depth=1)
+    for algo in (lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE, lr.RT_ALGO_BRUTE_GLOBAL):
+        o.algo = algo
+        with pytest.raises(lr.RtError) as e:
+            gpu_ctx.render(o)
+        assert e.value.code == lr.RT_E_UNSUPPORTED
+    o.algo = lr.RT_ALGO_AUTO
+    _, _, st = gpu_ctx.render(o)
+    assert st.rays > 0
     s = scenes.config2(8, 8)
     s.camera = dict(s.camera, dof=True, focus_dist=5.0, aperture=0.1, samples=4)
+    gpu_ctx.upload(lr.Scene.deserialize(s.to_text()))
     with pytest.raises(lr.RtError) as e:
-        gpu_ctx.upload(lr.Scene.deserialize(s.to_text()))
+        gpu_ctx.render(lr.render_opts(8, 8, spp=1, algo=lr.RT_ALGO_WAVEFRONT))
     assert e.value.code == lr.RT_E_UNSUPPORTED
 
 

@@ -27,7 +27,8 @@ def test_library_exports_every_header_symbol():
 def test_abi_struct_sizes_match_header():
     # ctypes mirrors must agree with the C layout (checked through the library's own writers)
     assert C.sizeof(lr.rt_object) == 4 + 4 + 48 + 72 + 8 + 8 + 4 + 4
-    assert C.sizeof(lr.rt_render_opts) == 16 * 4
+    assert C.sizeof(lr.rt_render_opts) == 16 * 4 + 8     # ABI 2: + seed
+    assert C.sizeof(lr.rt_light) == 8 + 72 + 24
 
 
 def test_parse_reference_test_scene():

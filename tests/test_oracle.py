@@ -172,3 +172,17 @@ def test_indirect_phong_statistics(rng):
     the same check as the reference's own XorShift."""
     out = ref64.render(cornell_spec(), jitter=1, seed=12345, want_rgb64=False, rng=rng)
     check_out_bmp_statistics(out["bgr"])
+
+
+def test_keyed_rng_is_independent_of_threads_and_tiles():
+    """REF_RNG_KEYED (the device's draw specification): every draw is a function of
+    its place in the recursion, so thread count and tiling cannot change a pixel."""
+    spec = scenes.stochastic(48, 32, antialias=2, samples=2, dof=True)
+    a = ref64.render(spec, jitter=1, seed=5, rng=1, threads=1)
+    b = ref64.render(spec, jitter=1, seed=5, rng=1, threads=4)
+    assert np.array_equal(a["rgb64"].view(np.uint64), b["rgb64"].view(np.uint64))
+    assert a["counts"] == b["counts"]
+    t = ref64.render(spec, jitter=1, seed=5, rng=1, x0=8, tile_w=24, y0=4, tile_h=20)
+    assert np.array_equal(t["rgb64"].view(np.uint64), a["rgb64"][4:24, 8:32].view(np.uint64))
+    c = ref64.render(spec, jitter=1, seed=6, rng=1)
+    assert not np.array_equal(c["bgr"], a["bgr"])

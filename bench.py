@@ -17,7 +17,9 @@ GPUs the same scene and view are rendered at sqrt(N) x the resolution (frame
 side 4096*sqrt(N), rounded to whole bands), so every GPU renders the N=1
 frame's 16.7 M pixels; --scaling strong splits the 4096^2 frame instead.
 value = rays of the whole frame x K / max-over-ranks wall time of the K timed
-steps.  --config c4 / c5 select the larger configs of BASELINE.json.
+steps.  --config c4 / c5 select the larger configs of BASELINE.json; --config
+c1 the reference's own scene (test_scene.txt: IndirectPhong Cornell box, 1024
+random AA samples, 256x256, depth 1) on the path kernel.
 
 Rays = every Scene::intersect query the reference would issue (camera +
 reflection + shadow), counted by the kernel; identical to the oracle's count
@@ -42,8 +44,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
-                   help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16")
+    p.add_argument("--config", default="c3", choices=["c1", "c3", "c4", "c5"],
+                   help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16; "
+                        "c1 test_scene.txt 256^2, 1024 random AA samples, depth 1 (path kernel)")
+    p.add_argument("--spp", type=int, default=0, help="c1: AA samples (default: the scene's 1024)")
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--spheres", type=int, default=0)
@@ -73,9 +77,10 @@ def pmc_traffic(config_key):
         return None
 
 
-def cpu_baseline(spec, args):
+def cpu_baseline(spec, args, **draws):
     """Oracle (algorithmically the reference: same recursion, same linear scan,
-    f64) on the host, on a deterministic row sample of the same frame."""
+    f64) on the host, on a deterministic row sample of the same frame.
+    draws: jitter / seed / rng of a stochastic workload (the device's keyed draws)."""
     from oracle import ref64
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     rows, stride = 8, max(1, spec.height // 8)
@@ -85,7 +90,7 @@ def cpu_baseline(spec, args):
         rows = spec.height // stride
         t0 = time.time()
         r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads,
-                         want_rgb64=False)
+                         want_rgb64=False, **draws)
         dt = time.time() - t0
         if dt >= 0.6 * args.cpu_seconds or stride == 1:
             break
@@ -112,8 +117,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    cfg = {"c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
-           "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}[args.config]       # scenes.config3/4/5
+    cfg = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
+           "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}[args.config]       # scenes.config1/3/4/5
+    path_cfg = args.config == "c1"
     args.width = args.width or cfg[0]
     args.height = args.height or cfg[0]
     n_split = args.shard_of if (args.shard_of > 1 and world == 1) else world
@@ -125,8 +131,15 @@ def main():
         args.height = max(BAND, int(round(args.height * f / BAND)) * BAND)
     args.spheres = args.spheres or cfg[1]
     args.depth = cfg[2] if args.depth < 0 else args.depth
-    spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=cfg[3],
-                                 box_scale=cfg[4], name=args.config)
+    if path_cfg:
+        spec = scenes.config1(args.width, args.height, max_depth=args.depth)
+        if args.spp:
+            spec.antialias = args.spp
+    else:
+        spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=cfg[3],
+                                     box_scale=cfg[4], name=args.config)
+    spp = spec.antialias
+    jitter = lr.RT_JITTER_RANDOM if path_cfg else lr.RT_JITTER_CENTER
     W, H = spec.width, spec.height
     ctx = lr.Context(local)
     scene = lr.Scene.deserialize(spec.to_text())
@@ -136,9 +149,9 @@ def main():
     assert tail is None or len(tail) == 0, "bench frames are whole bands"
     algo = {"auto": lr.RT_ALGO_AUTO, "wavefront": lr.RT_ALGO_WAVEFRONT, "lds": lr.RT_ALGO_BRUTE_LDS,
             "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
-    opts = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
-                          max_depth=args.depth, spp=1, algo=algo,
-                          flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8)
+    common = dict(tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank, max_depth=args.depth,
+                  spp=spp, algo=algo, jitter=jitter, seed=cfg[3])
+    opts = lr.render_opts(W, H, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8, **common)
     pitch = 3 * W
     out_rgb = torch.empty((len(rows), W, 3), dtype=torch.float32, device=dev)
     out_bgr = torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)
@@ -150,8 +163,7 @@ def main():
     # events around every launch (RT_TIME_KERNELS), after the timed region: the
     # events sit between launches on both streams and would perturb the timing
     timed_flags = opts.flags | lr.RT_TIME_KERNELS
-    opts_timed = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
-                                max_depth=args.depth, spp=1, algo=algo, flags=timed_flags)
+    opts_timed = lr.render_opts(W, H, flags=timed_flags, **common)
 
     def step(o=opts):
         ctx.render_device(o, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
@@ -186,9 +198,7 @@ def main():
         ktimes = ctx.kernel_times()        # {family: (ms summed over K instrumented frames, launches)}
 
     # one more, untimed frame with the instrumented kernels: exact box / sphere test counts
-    work = lr.render_opts(W, H, tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank,
-                          max_depth=args.depth, spp=1, algo=algo,
-                          flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK)
+    work = lr.render_opts(W, H, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK, **common)
     ctx.render_device(work, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize(dev)
     wst = ctx.stats()
@@ -235,21 +245,30 @@ def main():
                 kernels["wf_" + fam] = {"avg_launch_us": round(ms / n * 1e3, 2),
                                         "launches_per_frame": round(n / args.steps, 2),
                                         "ms_per_frame": round(ms / args.steps, 4)}
+        if path_cfg:        # one launch of path_kernel per frame: its duration is the render's
+            kernels = {"path_kernel": {"avg_launch_us": round(avg_kernel_ms * 1e3, 2), "launches_per_frame": 1.0,
+                                       "ms_per_frame": round(avg_kernel_ms, 4)}}
         dominant = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else None
+        if path_cfg:
+            workload = (f"C1: test_scene.txt (IndirectPhong Cornell box, no lights) at {W}x{H}, {spp} random AA "
+                        f"samples per pixel (keyed draws, seed {cfg[3]}), depth {args.depth}")
+        else:
+            workload = (f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
+                        f"depth {args.depth}, 1 spp centre jitter (seed {cfg[3]})")
         line = {
             "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak" if (n_split > 1 and args.scaling == "weak") else "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
-                                   f"depth {args.depth}, 1 spp centre jitter (seed {cfg[3]})",
-                       "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth,
+            "config": {"workload": workload,
+                       "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth, "spp": spp,
                        "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}",
                        "algo": args.algo},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
+                         "kernel": "path_kernel" if path_cfg else
+                                   "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
                                    "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "kernels": kernels or None, "dominant_kernel": dominant,
@@ -267,11 +286,13 @@ def main():
         if world == 1:
             line["pcie_inclusive"] = {"ms_per_frame": round(host_ms, 3),
                                       "value": round(total_rays / (host_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s",
-                                      "note": "rt_render to pageable host buffers: kernels + D2H of 201 MB f32 RGB "
-                                              "+ 50 MB BGR (+ host allocation)"}
+                                      "note": f"rt_render to pageable host buffers: kernels + D2H of "
+                                              f"{W * H * 12 / 1e6:.0f} MB f32 RGB + {W * H * 3 / 1e6:.0f} MB BGR "
+                                              f"(+ host allocation)"}
         if world == 1 and not args.no_cpu:
             try:
-                line["cpu_baseline"] = cpu_baseline(spec, args)
+                draws = dict(jitter=1, seed=cfg[3], rng=1) if path_cfg else {}
+                line["cpu_baseline"] = cpu_baseline(spec, args, **draws)
             except Exception as e:  # the oracle is optional on a box where it was not built
                 line["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(line), flush=True)

@@ -216,6 +216,25 @@ def config2_fresnel(width=1920, height=1080, max_depth=6):
     return s
 
 
+def config1(width=256, height=256, antialias=1024, max_depth=1):
+    """C1: the reference's own scene, test_scene.txt (a Cornell box of
+    IndirectPhongMaterial walls and spheres lit only by an emissive sphere, no
+    lights; camera new((0,3,17), (0,0,-1), (0,1,0), 3.6); 1024 AA samples).
+    BASELINE.json configs[0]: 256x256, depth 1."""
+    s = SceneSpec(width=width, height=height, antialias=antialias, max_depth=max_depth, name="c1",
+                  background=(0.051, 0.051, 0.051),
+                  camera={"ctor": "new", "position": (0, 3, 17), "look": (0, 0, -1), "up": (0, 1, 0), "im_dist": 3.6})
+    white = indirect_phong((1, 1, 1), (0, 0, 0), 1.0, (0, 0, 0), 1)
+    s.plane((0, 0, -3), (0, 0, 1), white)
+    s.plane((0, 0, 0), (0, 1.0, 0), white)
+    s.plane((0, 6, 0), (0, -1.0, 0), white)
+    s.plane((-3, 0, 0), (1, 0, 0), dict(white, diffuse=(1, 0, 0)))
+    s.plane((3, 0, 0), (-1, 0, 0), dict(white, diffuse=(0, 1, 0)))
+    s.sphere((0, 1.5, 0), 1.5, white)
+    s.sphere((0, 10.65, 0), 5, dict(white, ambient=(5, 5, 5)))
+    return s
+
+
 def stochastic(width=96, height=64, antialias=4, max_depth=4, samples=2, dof=False, area=True):
     """Every stochastic / branching class of the reference in one scene (SURVEY.md
     §8(f) rows 3-4): glass (Transparent) and IndirectPhong spheres next to Phong and

@@ -13,23 +13,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 def cornell_spec(width=200, height=200, antialias=1024, max_depth=4):
     """test_scene.txt (IndirectPhong walls, spheres and a lamp, no lights) at 200x200:
     each pixel spans a 4x4 block of out.bmp's 800x800."""
-    spec = scenes.SceneSpec(width=width, height=height, antialias=antialias, max_depth=max_depth,
-                            background=(0.051, 0.051, 0.051),
-                            camera={"ctor": "new", "position": (0, 3, 17), "look": (0, 0, -1),
-                                    "up": (0, 1, 0), "im_dist": 3.6})
-    white = {"kind": "indirect_phong", "diffuse": (1, 1, 1), "specular": (0, 0, 0), "exponent": 1.0,
-             "ambient": (0, 0, 0), "samples": 1}
-    red = dict(white, diffuse=(1, 0, 0))
-    green = dict(white, diffuse=(0, 1, 0))
-    lamp = dict(white, ambient=(5, 5, 5))
-    spec.plane((0, 0, -3), (0, 0, 1), white)
-    spec.plane((0, 0, 0), (0, 1.0, 0), white)
-    spec.plane((0, 6, 0), (0, -1.0, 0), white)
-    spec.plane((-3, 0, 0), (1, 0, 0), red)
-    spec.plane((3, 0, 0), (-1, 0, 0), green)
-    spec.sphere((0, 1.5, 0), 1.5, white)
-    spec.sphere((0, 10.65, 0), 5, lamp)
-    return spec
+    return scenes.config1(width, height, antialias, max_depth)
 
 
 def check_out_bmp_statistics(bgr):

@@ -142,9 +142,14 @@ constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (ca
 // Recursion stack of the path kernel: one frame per depth 0..max_depth for
 // every work-item of the (persistent) grid, SoA so a wave's lanes at the same
 // depth touch consecutive 8-B words: f64 fields [level][kPathF][T], then the
-// key [level][T], then i32 fields [level][kPathI][T].
-constexpr int kPathF = 17;            // point 3, normal 3, direction 3, significance, colour 3, factor, aux 3
-constexpr int kPathI = 3;             // object, next child, flags
+// key [level][T], then i32 fields [level][kPathI][T].  A frame whose child in
+// flight is its last one stores only the compact part (what folding the
+// child's colour needs: colour so far and the two fold factors); a frame with
+// more children to spawn (IndirectPhong samples > 1, Transparent reflection
+// before refraction) also stores the extension and the path key.
+constexpr int kPathCompact = 5;       // colour 3, fold factor, second fold factor (IndirectPhong specular)
+constexpr int kPathF = kPathCompact + 14;   // + point 3, normal 3, direction 3, significance, Schlick f, aux 3
+constexpr int kPathI = 3;             // object, child in flight, flags
 struct PathStack {
     unsigned char* mem;
     uint32_t T;                       // work-items of the grid (stride of every field)

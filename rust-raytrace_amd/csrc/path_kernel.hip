@@ -37,58 +37,61 @@ namespace {
 constexpr int kPathBlock = 256;
 constexpr double kPi = 3.14159265358979323846264338327950288;      // f64::consts::PI
 constexpr int32_t kFlDiffuse = 1, kFlSpecular = 2, kFlRefract = 4;
+constexpr int32_t kFlMore = 8;          // the frame has children left after the one in flight (extension stored)
 
 __device__ __forceinline__ double clamp_one(double x) { return x > 1.0 ? 1.0 : x; }   // raytrace.rs:26-28
 
 // One level of the recursion: what PhongMaterial / IndirectPhongMaterial /
 // FresnelMaterial / TransparentMaterial::color holds across its child calls.
 struct Frame {
+    Col res;                    // colour so far
+    double g, g2;               // fold factors of the child in flight (see fold_child)
     double ptx, pty, ptz;       // pt = ray.cast(t)
     double nx, ny, nz;          // normal flipped toward the viewer
     double dx, dy, dz;          // incoming ray direction
     double sig;                 // significance the hit was reached with
-    Col res;                    // colour so far
     double f;                   // Fresnel / Transparent: Schlick factor; Phong / IndirectPhong: 1
-    double ax, ay, az;          // Transparent: unnormalised refraction vector; IndirectPhong: current sample dir
+    double ax, ay, az;          // Transparent: unnormalised refraction vector; IndirectPhong: sample direction
     uint64_t key;               // path key of the hit
     int32_t obj, next, flags;   // object id, index of the child in flight, kFl* bits
 };
 
-__device__ __forceinline__ void store_frame(const PathStack& st, int L, uint32_t t, const Frame& F) {
-    const double v[kPathF] = {F.ptx, F.pty, F.ptz, F.nx, F.ny, F.nz, F.dx, F.dy, F.dz, F.sig,
-                              F.res.r, F.res.g, F.res.b, F.f, F.ax, F.ay, F.az};
-#pragma unroll
-    for (int k = 0; k < kPathF; ++k) st.f(L, k)[t] = v[k];
-    st.key(L)[t] = F.key;
+// Compact part: colour, fold factors, object, child, flags.
+__device__ __forceinline__ void store_compact(const PathStack& st, int L, uint32_t t, const Frame& F) {
+    st.f(L, 0)[t] = F.res.r; st.f(L, 1)[t] = F.res.g; st.f(L, 2)[t] = F.res.b;
+    st.f(L, 3)[t] = F.g; st.f(L, 4)[t] = F.g2;
     st.i(L, 0)[t] = F.obj;
     st.i(L, 1)[t] = F.next;
     st.i(L, 2)[t] = F.flags;
 }
 
-// After a child returned: only the colour, the sample direction and the child index change.
-__device__ __forceinline__ void store_resume(const PathStack& st, int L, uint32_t t, const Frame& F) {
-    st.f(L, 10)[t] = F.res.r; st.f(L, 11)[t] = F.res.g; st.f(L, 12)[t] = F.res.b;
-    st.f(L, 14)[t] = F.ax; st.f(L, 15)[t] = F.ay; st.f(L, 16)[t] = F.az;
-    st.i(L, 1)[t] = F.next;
+__device__ __forceinline__ void store_extension(const PathStack& st, int L, uint32_t t, const Frame& F) {
+    const double v[kPathF - kPathCompact] = {F.ptx, F.pty, F.ptz, F.nx, F.ny, F.nz, F.dx, F.dy, F.dz,
+                                             F.sig, F.f, F.ax, F.ay, F.az};
+#pragma unroll
+    for (int k = 0; k < kPathF - kPathCompact; ++k) st.f(L, kPathCompact + k)[t] = v[k];
+    st.key(L)[t] = F.key;
 }
 
-__device__ __forceinline__ Frame load_frame(const PathStack& st, int L, uint32_t t) {
-    double v[kPathF];
+__device__ __forceinline__ void load_compact(const PathStack& st, int L, uint32_t t, Frame& F) {
+    F.res = Col{st.f(L, 0)[t], st.f(L, 1)[t], st.f(L, 2)[t]};
+    F.g = st.f(L, 3)[t]; F.g2 = st.f(L, 4)[t];
+    F.obj = st.i(L, 0)[t];
+    F.next = st.i(L, 1)[t];
+    F.flags = st.i(L, 2)[t];
+}
+
+__device__ __forceinline__ void load_extension(const PathStack& st, int L, uint32_t t, Frame& F) {
+    double v[kPathF - kPathCompact];
 #pragma unroll
-    for (int k = 0; k < kPathF; ++k) v[k] = st.f(L, k)[t];
-    Frame F;
+    for (int k = 0; k < kPathF - kPathCompact; ++k) v[k] = st.f(L, kPathCompact + k)[t];
     F.ptx = v[0]; F.pty = v[1]; F.ptz = v[2];
     F.nx = v[3]; F.ny = v[4]; F.nz = v[5];
     F.dx = v[6]; F.dy = v[7]; F.dz = v[8];
     F.sig = v[9];
-    F.res = Col{v[10], v[11], v[12]};
-    F.f = v[13];
-    F.ax = v[14]; F.ay = v[15]; F.az = v[16];
+    F.f = v[10];
+    F.ax = v[11]; F.ay = v[12]; F.az = v[13];
     F.key = st.key(L)[t];
-    F.obj = st.i(L, 0)[t];
-    F.next = st.i(L, 1)[t];
-    F.flags = st.i(L, 2)[t];
-    return F;
 }
 
 // camera.rs:76-80 (simple) and camera.rs:109-122 (depth of field; theta and
@@ -135,6 +138,7 @@ __device__ void shade_hit(const DevScene& sc, const BvhView& v, const DevMateria
     F.obj = h.obj;
     F.next = -1;
     F.ax = F.ay = F.az = 0.0;
+    F.g = F.g2 = 0.0;
     bool diffuse, specular;
     if (m.kind == kMatTransparent) {                                   // raytrace.rs:171-195
         F.res = Col{0.0, 0.0, 0.0};
@@ -177,9 +181,12 @@ __device__ void shade_hit(const DevScene& sc, const BvhView& v, const DevMateria
 }
 
 // The first child ray of frame F with index >= i, or -1: its ray and
-// significance (raytrace.rs:58-64, 98-106, 159-164, 212-224).
+// significance (raytrace.rs:58-64, 98-106, 159-164, 212-224), the fold factors
+// F.g / F.g2 its colour will be folded with, and kFlMore when F has children
+// left after it.
 __device__ __forceinline__ int next_child(Frame& F, const DevMaterial& m, int i, Ray& cr, double& csig) {
     const bool specular = (F.flags & kFlSpecular) != 0;
+    F.flags &= ~kFlMore;
     if (m.kind == kMatIndirect) {
         if (i >= static_cast<int>(m.samples) || !(F.flags & (kFlDiffuse | kFlSpecular))) return -1;
         const double r1 = key_f64(F.key, 128u + 2u * static_cast<uint32_t>(i)) * 2.0 - 1.0;
@@ -190,53 +197,60 @@ __device__ __forceinline__ int next_child(Frame& F, const DevMaterial& m, int i,
         F.ax = keep ? x : -x; F.ay = keep ? r1 : -r1; F.az = keep ? z : -z;
         cr = Ray{F.ptx + F.ax * kEps, F.pty + F.ay * kEps, F.ptz + F.az * kEps, F.ax, F.ay, F.az};
         csig = F.sig;                                                 // significance passed unchanged
+        F.g = F.nx * F.ax + F.ny * F.ay + F.nz * F.az;                // dot(normal, dir)
+        if (specular) {   // sic: (dir - ray.direction) with ray the NEW ray: 0/0 (raytrace.rs:108,115)
+            const double hx = F.ax - F.ax, hy = F.ay - F.ay, hz = F.az - F.az;
+            const double hl = sqrt(hx * hx + hy * hy + hz * hz);
+            F.g2 = pow(clamp_zero(F.nx * (hx / hl) + F.ny * (hy / hl) + F.nz * (hz / hl)), m.exponent);
+        }
+        if (i + 1 < static_cast<int>(m.samples)) F.flags |= kFlMore;
         return i;
     }
+    const bool refract = m.kind == kMatTransparent && F.f < 1.0 && (F.flags & kFlRefract);   // raytrace.rs:216-224
     if (i == 0 && specular) {                                          // mirror reflection
         cr = reflect_ray(Ray{0.0, 0.0, 0.0, F.dx, F.dy, F.dz}, F.ptx, F.pty, F.ptz, F.nx, F.ny, F.nz);
         csig = (F.f * F.sig) * m.ks_sig;                               // Phong: (1 * sig) * ks_sig == sig * ks_sig
+        F.g = F.f;
+        if (refract) F.flags |= kFlMore;
         return 0;
     }
-    if (m.kind == kMatTransparent && i <= 1 && F.f < 1.0 && (F.flags & kFlRefract)) {   // raytrace.rs:216-224
+    if (i <= 1 && refract) {
         const double omf = clamp_one(1.0 - F.f);
         const double l = sqrt(F.ax * F.ax + F.ay * F.ay + F.az * F.az);
         const double rx = F.ax / l, ry = F.ay / l, rz = F.az / l;
         cr = Ray{F.ptx + rx * kEps, F.pty + ry * kEps, F.ptz + rz * kEps, rx, ry, rz};
         csig = omf * F.sig;
+        F.g = omf;
         return 1;
     }
     return -1;
 }
 
-// Fold the colour c of child F.next into F.res (the `res = res + ...` lines).
+// Fold the colour c of child F.next into F.res (the `res = res + ...` lines)
+// with the factors next_child recorded.
 __device__ __forceinline__ void fold_child(Frame& F, const DevMaterial& m, const Col& c) {
     if (m.kind == kMatIndirect) {                                      // raytrace.rs:107-118
         const double fac = static_cast<double>(m.samples) * 0.5;
-        if (F.flags & kFlDiffuse) {
-            const double d = F.nx * F.ax + F.ny * F.ay + F.nz * F.az;
-            F.res.r = F.res.r + ((m.kd[0] * c.r) * d) / fac;
-            F.res.g = F.res.g + ((m.kd[1] * c.g) * d) / fac;
-            F.res.b = F.res.b + ((m.kd[2] * c.b) * d) / fac;
+        if (F.flags & kFlDiffuse) {                                    // ((kd * c) * dot(n, dir)) / fac
+            F.res.r = F.res.r + ((m.kd[0] * c.r) * F.g) / fac;
+            F.res.g = F.res.g + ((m.kd[1] * c.g) * F.g) / fac;
+            F.res.b = F.res.b + ((m.kd[2] * c.b) * F.g) / fac;
         }
-        if (F.flags & kFlSpecular) {       // sic: (dir - ray.direction) with ray the NEW ray: 0/0 (raytrace.rs:108,115)
-            const double hx = F.ax - F.ax, hy = F.ay - F.ay, hz = F.az - F.az;
-            const double hl = sqrt(hx * hx + hy * hy + hz * hz);
-            const double p = pow(clamp_zero(F.nx * (hx / hl) + F.ny * (hy / hl) + F.nz * (hz / hl)), m.exponent);
-            F.res.r = F.res.r + ((m.ks[0] * c.r) * p) / fac;
-            F.res.g = F.res.g + ((m.ks[1] * c.g) * p) / fac;
-            F.res.b = F.res.b + ((m.ks[2] * c.b) * p) / fac;
+        if (F.flags & kFlSpecular) {                                   // ((ks * c) * pow) / fac
+            F.res.r = F.res.r + ((m.ks[0] * c.r) * F.g2) / fac;
+            F.res.g = F.res.g + ((m.ks[1] * c.g) * F.g2) / fac;
+            F.res.b = F.res.b + ((m.ks[2] * c.b) * F.g2) / fac;
         }
         return;
     }
     if (F.next == 0) {                      // reflection: res + (ks * child) * f  (raytrace.rs:63 / 163 / 214)
-        F.res.r = F.res.r + (m.ks[0] * c.r) * F.f;
-        F.res.g = F.res.g + (m.ks[1] * c.g) * F.f;
-        F.res.b = F.res.b + (m.ks[2] * c.b) * F.f;
+        F.res.r = F.res.r + (m.ks[0] * c.r) * F.g;
+        F.res.g = F.res.g + (m.ks[1] * c.g) * F.g;
+        F.res.b = F.res.b + (m.ks[2] * c.b) * F.g;
     } else {                                // refraction: res + child * omf  (raytrace.rs:222)
-        const double omf = clamp_one(1.0 - F.f);
-        F.res.r = F.res.r + c.r * omf;
-        F.res.g = F.res.g + c.g * omf;
-        F.res.b = F.res.b + c.b * omf;
+        F.res.r = F.res.r + c.r * F.g;
+        F.res.g = F.res.g + c.g * F.g;
+        F.res.b = F.res.b + c.b * F.g;
     }
 }
 
@@ -269,7 +283,8 @@ __device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParam
         }
         if (child >= 0) {                                              // descend
             F.next = child;
-            store_frame(st, L, t, F);
+            store_compact(st, L, t, F);
+            if (F.flags & kFlMore) store_extension(st, L, t, F);
             ray = cr;
             sig = csig;
             key = key_child(F.key, static_cast<uint64_t>(child));
@@ -279,13 +294,15 @@ __device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParam
         bool resumed = false;                                          // return c to the parents
         while (L > 0) {
             --L;
-            Frame P = load_frame(st, L, t);
+            Frame P;
+            load_compact(st, L, t, P);
             const DevMaterial& m = sc.mats[P.obj];
             fold_child(P, m, c);
-            const int nx = next_child(P, m, P.next + 1, cr, csig);
-            if (nx >= 0) {
+            if (P.flags & kFlMore) {                                   // spawn the next child
+                load_extension(st, L, t, P);
+                const int nx = next_child(P, m, P.next + 1, cr, csig);
                 P.next = nx;
-                store_resume(st, L, t, P);
+                store_compact(st, L, t, P);                            // the extension is unchanged
                 ray = cr;
                 sig = csig;
                 key = key_child(P.key, static_cast<uint64_t>(nx));

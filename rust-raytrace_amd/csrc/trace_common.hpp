@@ -624,7 +624,9 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
         if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
+#if RT_SEL4
     const Sel4 sel = make_sel4(rb, v.n4);
+#endif
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
     // pushes are unconditional stores at the stack top (junk when nothing is
     // pushed; the next push overwrites it): no branch per child

@@ -485,14 +485,17 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     const size_t lds_bytes = static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere);
     const bool fits_lds = lds_bytes <= 64 * 1024;
     int mode = o->algo;
-    // the stochastic / branching classes and random jitter run on the path kernel only
-    const bool path_only = c->dsc.needs_path || o->jitter != RT_JITTER_CENTER;
+    // the stochastic / branching classes, and random jitter with several AA
+    // samples per pixel, run on the path kernel only (the chain schedules trace
+    // one camera ray per pixel: centre jitter, or random jitter with spp = 1)
+    const bool path_only = c->dsc.needs_path || (o->jitter != RT_JITTER_CENTER && spp > 1);
     if (mode == RT_ALGO_AUTO)
         mode = path_only ? RT_ALGO_PATH
                          : (c->dsc.n_lights <= 32 ? RT_ALGO_WAVEFRONT : (fits_lds ? RT_ALGO_BRUTE_LDS : RT_ALGO_BRUTE_GLOBAL));
     if (path_only && mode != RT_ALGO_PATH)
         return fail(c, RT_E_UNSUPPORTED,
-                    "IndirectPhong / Transparent materials, AreaLight, DepthOfFieldCamera and random jitter need RT_ALGO_PATH");
+                    "IndirectPhong / Transparent materials, AreaLight, DepthOfFieldCamera and random jitter with "
+                    "spp > 1 need RT_ALGO_PATH");
     if (mode == RT_ALGO_BRUTE_LDS && lds_bytes > 160 * 1024)
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
     if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)

@@ -38,6 +38,39 @@ struct Col {
     double r, g, b;
 };
 
+// ---- keyed RNG --------------------------------------------------------------
+// The reference draws from ONE sequential XorShiftRng seeded from OS entropy
+// (main.rs:43): no run can be reproduced and the stream order is the serial
+// pixel loop's.  The device path instead makes every draw a pure function of
+// its place in the recursion, so any schedule gives the same image and the
+// oracle (oracle/ref64.c, REF_RNG_KEYED) reproduces it draw for draw:
+//   pixel      kp = mix(mix(seed) + (y << 32 | x))        (frame coordinates)
+//   AA sample  ka = child(kp, a)    jitter jx = f64(ka, 0), jy = f64(ka, 1)  (main.rs:51-52)
+//   camera     kc = child(ka, cs)   DoF theta = f64(kc, 0), r2 = closed01(kc, 1)  (camera.rs:115-117)
+//   a hit with path key K draws     AreaLight l: u = f64(K, 2+2l), w = f64(K, 3+2l)  (scene.rs:153)
+//                                   indirect sample i: f64(K, 128+2i), f64(K, 129+2i)  (raytrace.rs:101-102)
+//   child ray i of a hit has key child(K, i) (mirror reflection 0, refraction 1,
+//   indirect sample i).
+// f64 / closed01 follow rand 0.3's bit recipes (52 mantissa bits; 53 bits over 2^53 - 1).
+__device__ __forceinline__ uint64_t kmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t key_child(uint64_t k, uint64_t i) { return kmix(k + (i + 1) * 0x9E3779B97F4A7C15ull); }
+__device__ __forceinline__ uint64_t key_bits(uint64_t k, uint32_t id) {
+    return kmix(k ^ (static_cast<uint64_t>(id + 1) * 0xD1B54A32D192ED03ull));
+}
+__device__ __forceinline__ double key_f64(uint64_t k, uint32_t id) {
+    return __longlong_as_double(static_cast<long long>(0x3FF0000000000000ull | (key_bits(k, id) & 0xFFFFFFFFFFFFFull))) - 1.0;
+}
+__device__ __forceinline__ double key_closed01(uint64_t k, uint32_t id) {
+    return static_cast<double>(key_bits(k, id) >> 11) / 9007199254740991.0;
+}
+__device__ __forceinline__ uint64_t key_pixel(uint64_t seed, uint32_t x, uint32_t y) {
+    return kmix(kmix(seed) + ((static_cast<uint64_t>(y) << 32) | x));
+}
+
 __device__ __forceinline__ double clamp_zero(double x) { return x < 0.0 ? 0.0 : x; }   // raytrace.rs:20-23
 
 // color.rs:593-600 as a binary search over the strictly increasing table.
@@ -810,12 +843,20 @@ __device__ __forceinline__ void add_light(Col& res, const DevMaterial& m, const 
     }
 }
 
-// Pixel -> camera ray (main.rs:50-53 with the centre jitter; camera.rs:78).
+// Pixel -> camera ray (main.rs:50-53; camera.rs:78) of AA sample 0: the
+// centre jitter, or the keyed draws of the pixel's first sample (fp.jitter;
+// the chain schedules take random jitter only with one sample per pixel).
 __device__ __forceinline__ Ray camera_ray(const DevScene& sc, const FrameParams& fp, uint32_t lx, uint32_t local_row) {
     const uint32_t x = fp.x0 + lx;
     const uint32_t y = fp.y0 + ((local_row / fp.band) * fp.band_stride + fp.band_phase) * fp.band + local_row % fp.band;
-    const double px = ((static_cast<double>(x) + 0.5) - fp.hw) * fp.scale;
-    const double py = ((static_cast<double>(y) + 0.5) - fp.hh) * fp.scale;
+    double jx = 0.5, jy = 0.5;
+    if (fp.jitter) {
+        const uint64_t ka = key_child(key_pixel(fp.seed, x, y), 0);
+        jx = key_f64(ka, 0);
+        jy = key_f64(ka, 1);
+    }
+    const double px = ((static_cast<double>(x) + jx) - fp.hw) * fp.scale;
+    const double py = ((static_cast<double>(y) + jy) - fp.hh) * fp.scale;
     const double* M = sc.cam_m;
     const double dx = M[0] * px + M[1] * py + M[2] * 1.0;
     const double dy = M[3] * px + M[4] * py + M[5] * 1.0;
@@ -861,39 +902,6 @@ __device__ __forceinline__ void write_pixel(const FrameParams& fp, uint32_t lx, 
             for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k)
                 fp.out_bgr[static_cast<size_t>(out_row) * fp.bgr_pitch + k] = 0;
     }
-}
-
-// ---- keyed RNG --------------------------------------------------------------
-// The reference draws from ONE sequential XorShiftRng seeded from OS entropy
-// (main.rs:43): no run can be reproduced and the stream order is the serial
-// pixel loop's.  The device path instead makes every draw a pure function of
-// its place in the recursion, so any schedule gives the same image and the
-// oracle (oracle/ref64.c, REF_RNG_KEYED) reproduces it draw for draw:
-//   pixel      kp = mix(mix(seed) + (y << 32 | x))        (frame coordinates)
-//   AA sample  ka = child(kp, a)    jitter jx = f64(ka, 0), jy = f64(ka, 1)  (main.rs:51-52)
-//   camera     kc = child(ka, cs)   DoF theta = f64(kc, 0), r2 = closed01(kc, 1)  (camera.rs:115-117)
-//   a hit with path key K draws     AreaLight l: u = f64(K, 2+2l), w = f64(K, 3+2l)  (scene.rs:153)
-//                                   indirect sample i: f64(K, 128+2i), f64(K, 129+2i)  (raytrace.rs:101-102)
-//   child ray i of a hit has key child(K, i) (mirror reflection 0, refraction 1,
-//   indirect sample i).
-// f64 / closed01 follow rand 0.3's bit recipes (52 mantissa bits; 53 bits over 2^53 - 1).
-__device__ __forceinline__ uint64_t kmix(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t key_child(uint64_t k, uint64_t i) { return kmix(k + (i + 1) * 0x9E3779B97F4A7C15ull); }
-__device__ __forceinline__ uint64_t key_bits(uint64_t k, uint32_t id) {
-    return kmix(k ^ (static_cast<uint64_t>(id + 1) * 0xD1B54A32D192ED03ull));
-}
-__device__ __forceinline__ double key_f64(uint64_t k, uint32_t id) {
-    return __longlong_as_double(static_cast<long long>(0x3FF0000000000000ull | (key_bits(k, id) & 0xFFFFFFFFFFFFFull))) - 1.0;
-}
-__device__ __forceinline__ double key_closed01(uint64_t k, uint32_t id) {
-    return static_cast<double>(key_bits(k, id) >> 11) / 9007199254740991.0;
-}
-__device__ __forceinline__ uint64_t key_pixel(uint64_t seed, uint32_t x, uint32_t y) {
-    return kmix(kmix(seed) + ((static_cast<uint64_t>(y) << 32) | x));
 }
 
 // AreaLight (scene.rs:142-155): a PointLight at origin + side1*u + side2*w, u

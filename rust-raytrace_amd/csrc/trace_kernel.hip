@@ -237,10 +237,12 @@ __device__ __forceinline__ void tile_rect(const FrameParams& fp, const WfBufs& b
         const uint32_t lr = fp.row0 + l;
         return fp.y0 + ((lr / fp.band) * fp.band_stride + fp.band_phase) * fp.band + lr % fp.band;
     };
-    const double px0 = ((static_cast<double>(fp.x0 + xa) + 0.5) - fp.hw) * fp.scale;
-    const double px1 = ((static_cast<double>(fp.x0 + xb) + 0.5) - fp.hw) * fp.scale;
-    const double py0 = ((static_cast<double>(row(la)) + 0.5) - fp.hh) * fp.scale;
-    const double py1 = ((static_cast<double>(row(lb)) + 0.5) - fp.hh) * fp.scale;
+    // jitter in [0, 1) (random) or 0.5 (centre): x + j is monotone in both
+    const double j0 = fp.jitter ? 0.0 : 0.5, j1 = fp.jitter ? 1.0 : 0.5;
+    const double px0 = ((static_cast<double>(fp.x0 + xa) + j0) - fp.hw) * fp.scale;
+    const double px1 = ((static_cast<double>(fp.x0 + xb) + j1) - fp.hw) * fp.scale;
+    const double py0 = ((static_cast<double>(row(la)) + j0) - fp.hh) * fp.scale;
+    const double py1 = ((static_cast<double>(row(lb)) + j1) - fp.hh) * fp.scale;
     tx0 = __double2float_rd(px0); tx1 = __double2float_ru(px1);
     ty0 = __double2float_rd(py0); ty1 = __double2float_ru(py1);
 }

@@ -2,7 +2,7 @@
 
 The path kernel carries the classes the wavefront chain does not: IndirectPhong
 and Transparent materials, AreaLight, DepthOfFieldCamera and random AA jitter
-(SURVEY.md §8(f) rows 3-4).  Random draws are keyed on their place in the
+with several samples per pixel.  Random draws are keyed on their place in the
 recursion (trace_common.hpp "keyed RNG"); the oracle's REF_RNG_KEYED mode
 draws the same numbers, so:
   * scenes whose random draws feed only + - * / sqrt (random jitter, AreaLight,
@@ -147,6 +147,17 @@ def test_path_classes_rejected_by_chain_algorithms(gpu_ctx):
         with pytest.raises(lr.RtError) as e:
             render(gpu_ctx, spec, algo=algo)
         assert e.value.code == lr.RT_E_UNSUPPORTED
-    with pytest.raises(lr.RtError) as e:
-        render(gpu_ctx, scenes.config2(32, 32), algo=lr.RT_ALGO_WAVEFRONT)   # random jitter
+    with pytest.raises(lr.RtError) as e:     # random jitter with several samples per pixel
+        render(gpu_ctx, scenes.config2(32, 32), algo=lr.RT_ALGO_WAVEFRONT, spp=2)
     assert e.value.code == lr.RT_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE, lr.RT_ALGO_BRUTE_LDS,
+                                  lr.RT_ALGO_PATH])
+def test_random_jitter_one_sample_on_every_schedule(gpu_ctx, algo):
+    """main.rs:51-52 jitters every sample; with one sample per pixel the chain
+    schedules (wavefront, megakernel) take the keyed jitter too, and agree with
+    the oracle and the path kernel bit for bit (camera tiles widened to whole pixels)."""
+    spec = scenes.config3(160, 120, n=300)
+    rgb, bgr, st = render(gpu_ctx, spec, seed=21, algo=algo)
+    assert_exact(rgb, bgr, st, oracle(spec, seed=21))

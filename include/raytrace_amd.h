@@ -18,6 +18,8 @@
  *                         main.rs:39-57 + raytrace.rs:270-276 (raytrace) + raytrace.rs:261-267
  *                         (ray_color) + raytrace.rs:30-67 (PhongMaterial::color) + scene.rs:247-249
  *                         (Scene::intersect) + shapes.rs:50-112 (Sphere/Plane::intersect)
+ *   rt_scene_set_skybox   scene.rs:174-188       SkyboxBackground { px, nx, py, ny, pz, nz }
+ *   rt_texture_load       texture.rs:34-37       Texture::load (BMP and binary PPM here; the image crate decodes more)
  *   rt_to_srgb            color.rs:593-600       fn to_srgb (used by Color::write_bgr, color.rs:628-632)
  *   rt_bmp_header         bmp.rs:10-61           pub fn write_header
  *   rt_write_bmp          main.rs:34-59          header + bottom-up BGR rows to a file
@@ -101,10 +103,16 @@ typedef struct {
     const rt_object* objects; uint32_t n_objects;
     const rt_light* lights;   uint32_t n_lights;
     rt_camera camera;
-    int32_t background_kind;  /* only RT_BG_SOLID is representable through a desc */
+    int32_t background_kind;  /* a desc carries RT_BG_SOLID; textures go through rt_scene_set_skybox */
     rt_color background;
     uint32_t width, height, antialias;   /* scene.rs:191-198 Options */
 } rt_scene_desc;
+
+/* texture.rs:22-26: an RGB8 image, rows top-down, width*height*3 bytes (caller-owned). */
+typedef struct {
+    uint32_t width, height;
+    const uint8_t* rgb;
+} rt_texture;
 
 typedef struct rt_scene rt_scene;   /* host-side parsed scene (opaque) */
 typedef struct rt_ctx rt_ctx;       /* one device context (opaque) */
@@ -115,6 +123,11 @@ int rt_scene_from_desc(const rt_scene_desc* desc, rt_scene** out);
 /* Borrow the flattened view of a scene (valid until rt_scene_free). */
 int rt_scene_get_desc(const rt_scene* scene, rt_scene_desc* out);
 void rt_scene_free(rt_scene* scene);
+/* Make the scene's background a SkyboxBackground with faces px, nx, py, ny, pz, nz (copied). */
+int rt_scene_set_skybox(rt_scene* scene, const rt_texture faces[6]);
+/* Decode an image file as Texture::load does (RGB8, rows top-down).  rgb == NULL: only the size.
+ * Formats: uncompressed BMP (24/32 bit) and binary PPM; others -> RT_E_UNSUPPORTED. */
+int rt_texture_load(const char* path, uint32_t* width, uint32_t* height, uint8_t* rgb, size_t cap);
 
 int rt_camera_simple_new(const double position[3], const double look[3], const double up[3],
                          double im_dist, rt_camera* out);

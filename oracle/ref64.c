@@ -378,10 +378,48 @@ static col shade(ctx_t* c, const ref_object* m, const hit_t* hit, const ray_t* r
     return BLACK;
 }
 
+/* texture.rs:28-31, 40-58 and color.rs:611-613 (Color::from_srgb) */
+static double SRGB_VALUES_[256];
+static double tex_clamp(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }
+static col tex_at(const ref_texture* t, uint32_t x, uint32_t y) {
+    const uint8_t* p = t->rgb + 3 * ((size_t)x + (size_t)y * t->width);
+    col c; c.r = SRGB_VALUES_[p[0]]; c.g = SRGB_VALUES_[p[1]]; c.b = SRGB_VALUES_[p[2]];
+    return c;
+}
+static uint32_t as_u32(double x) { return x >= 0.0 ? (uint32_t)x : 0u; }   /* Rust `as u32`: NaN -> 0 */
+static col tex_sample(const ref_texture* t, double xs, double ys) {
+    double x = tex_clamp(xs) * (double)(t->width - 1);
+    double y = tex_clamp(ys) * (double)(t->height - 1);
+    uint32_t x0 = as_u32(x), y0 = as_u32(y);
+    uint32_t x1 = x0 >= t->width - 1 ? t->width - 1 : x0 + 1;
+    uint32_t y1 = y0 >= t->height - 1 ? t->height - 1 : y0 + 1;
+    double xx = x - (double)x0, yy = y - (double)y0;
+    col cx0 = cadd(cmul(tex_at(t, x0, y0), 1.0 - yy), cmul(tex_at(t, x0, y1), yy));
+    col cx1 = cadd(cmul(tex_at(t, x1, y0), 1.0 - yy), cmul(tex_at(t, x1, y1), yy));
+    return cadd(cmul(cx0, 1.0 - xx), cmul(cx1, xx));
+}
+/* raytrace.rs:234-256: x axis, then y, then z (skybox_axis! macro order) */
+static col skybox_color(const ref_texture* f, v3 d) {
+    if (fabs(d.x) > fabs(d.z) && fabs(d.x) > fabs(d.y)) {
+        double px = -d.z / d.x, py = -d.y / fabs(d.x);
+        return tex_sample(&f[d.x > 0.0 ? 0 : 1], px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    if (fabs(d.y) > fabs(d.x) && fabs(d.y) > fabs(d.z)) {
+        double px = d.x / fabs(d.y), py = d.z / d.y;
+        return tex_sample(&f[d.y > 0.0 ? 2 : 3], px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    if (fabs(d.z) > fabs(d.x) && fabs(d.z) > fabs(d.y)) {
+        double px = d.x / d.z, py = -d.y / fabs(d.z);
+        return tex_sample(&f[d.z > 0.0 ? 4 : 5], px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    return BLACK;
+}
+
 /* raytrace.rs:261-267 */
 static col ray_color(ctx_t* c, const ray_t* ray, double sig, uint32_t depth, uint64_t key) {
     hit_t h = scene_intersect(c, ray);
-    if (!h.hit) return cfrom3(c->s->background);       /* raytrace.rs:228-232 */
+    if (!h.hit)                                         /* raytrace.rs:228-256 */
+        return c->s->skybox ? skybox_color(c->s->skybox, ray->direction) : cfrom3(c->s->background);
     return shade(c, &c->s->objects[h.obj], &h, ray, sig, depth, key);
 }
 
@@ -433,7 +471,6 @@ static ray_t camera_project(ctx_t* c, double px, double py, uint64_t key) {
 
 /* ---- color.rs sRGB quantiser: tables generated, asserted against the
  * reference's literal tables by tests/test_oracle.py ---- */
-static double SRGB_VALUES_[256];
 static double SRGB_AVERAGE_[255];
 static pthread_once_t srgb_once = PTHREAD_ONCE_INIT;
 static void srgb_init(void) {

@@ -15,7 +15,7 @@
  *   raytrace.rs:69-121   IndirectPhongMaterial::color (stochastic)
  *   raytrace.rs:123-167  FresnelMaterial::color
  *   raytrace.rs:169-226  TransparentMaterial::color
- *   raytrace.rs:228-232  SolidColorBackground
+ *   raytrace.rs:228-256  SolidColorBackground, SkyboxBackground (texture.rs:46-58 sampling)
  *   raytrace.rs:261-276  ray_color / raytrace
  *   scene.rs:117-155     Point / Directional / Area lights
  *   scene.rs:223-249     Scene::intersect (first-wins ties, NaN-t wins)
@@ -71,12 +71,19 @@ typedef struct {
     uint32_t dof_samples;
 } ref_camera;
 
+/* texture.rs:22-26: RGB8, rows top-down (what image::open(..).to_rgb() yields) */
+typedef struct {
+    uint32_t width, height;
+    const uint8_t* rgb;
+} ref_texture;
+
 typedef struct {
     const ref_object* objects; uint32_t n_objects;
     const ref_light* lights;   uint32_t n_lights;
     ref_camera camera;
     double background[3];
     uint32_t width, height, antialias;
+    const ref_texture* skybox;   /* NULL: SolidColorBackground; else SkyboxBackground px, nx, py, ny, pz, nz */
 } ref_scene;
 
 enum { REF_JITTER_CENTER = 0, REF_JITTER_RANDOM = 1 };

@@ -34,11 +34,37 @@ class ref_camera(C.Structure):
                 ("aperture", C.c_double), ("dof_samples", C.c_uint32)]
 
 
+class ref_texture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgb", C.POINTER(C.c_uint8))]
+
+
 class ref_scene(C.Structure):
     _fields_ = [("objects", C.POINTER(ref_object)), ("n_objects", C.c_uint32),
                 ("lights", C.POINTER(ref_light)), ("n_lights", C.c_uint32),
                 ("camera", ref_camera), ("background", C.c_double * 3),
-                ("width", C.c_uint32), ("height", C.c_uint32), ("antialias", C.c_uint32)]
+                ("width", C.c_uint32), ("height", C.c_uint32), ("antialias", C.c_uint32),
+                ("skybox", C.POINTER(ref_texture))]
+
+
+def read_ppm(path):
+    """Binary PPM (P6, maxval 255) -> uint8 [h, w, 3], rows top-down (the checker's own decoder)."""
+    data = open(path, "rb").read()
+    fields, i = [], 2
+    while len(fields) < 3:
+        while data[i:i + 1].isspace():
+            i += 1
+        if data[i:i + 1] == b"#":
+            while data[i:i + 1] != b"\n":
+                i += 1
+            continue
+        j = i
+        while data[j:j + 1].isdigit():
+            j += 1
+        fields.append(int(data[i:j]))
+        i = j
+    w, h, mx = fields
+    assert data[:2] == b"P6" and mx == 255
+    return np.frombuffer(data[i + 1:i + 1 + w * h * 3], np.uint8).reshape(h, w, 3)
 
 
 class ref_opts(C.Structure):
@@ -146,7 +172,17 @@ class OracleScene:
         s.camera = cam
         s.background[:] = [float(x) for x in spec.background]
         s.width, s.height, s.antialias = spec.width, spec.height, spec.antialias
-        self._keep = (objs, lights)
+        keep = [objs, lights]
+        if getattr(spec, "skybox", None):
+            tex = (ref_texture * 6)()
+            for t, p in zip(tex, spec.skybox):
+                a = np.ascontiguousarray(read_ppm(p))
+                keep.append(a)
+                t.width, t.height = a.shape[1], a.shape[0]
+                t.rgb = a.ctypes.data_as(C.POINTER(C.c_uint8))
+            keep.append(tex)
+            s.skybox = tex
+        self._keep = keep
         self.scene = s
 
 

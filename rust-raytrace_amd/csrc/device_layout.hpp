@@ -89,6 +89,12 @@ struct alignas(16) DevBvh4Plane {
 constexpr int kBvh4Planes = 7;
 constexpr int32_t kBvh4Empty = INT32_MIN;
 
+// One skybox face (texture.rs:22-26): RGB8 rows top-down at DevScene::tex + off.
+struct DevTexFace {
+    uint32_t w, h;
+    uint64_t off;
+};
+
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -105,6 +111,10 @@ struct DevScene {
     int32_t has_fresnel;            // some object uses FresnelMaterial
     int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,
                                     // AreaLight, DepthOfFieldCamera)
+    int32_t skybox;                 // SkyboxBackground (raytrace.rs:234-256; path kernel only)
+    const uint8_t* tex;             // skybox texels
+    const double* srgb_values;      // color.rs SRGB_VALUES (Color::from_srgb, color.rs:611-613)
+    DevTexFace faces[6];            // px, nx, py, ny, pz, nz
     int32_t cam_dof;                // DepthOfFieldCamera (camera.rs:83-123)
     uint32_t cam_samples;           // Camera::samples() (1 for the simple camera)
     double cam_focus, cam_aperture, cam_im_dist;   // DepthOfFieldCamera focus, aperture, im_dist (camera.rs:98)

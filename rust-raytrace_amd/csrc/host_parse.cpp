@@ -14,7 +14,8 @@
 //
 // Deliberate differences (documented in DESIGN.md): an unterminated /* */
 // comment is an error here (the reference loops forever at EOF), and
-// SkyboxBackground is rejected as unsupported (textures are out of scope).
+// SkyboxBackground textures are decoded from BMP / binary PPM only
+// (host_texture.cpp; the reference's image crate decodes more formats).
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -469,8 +470,25 @@ public:
                 if (f == "color") { if (!p) s.background = color(); return 0; }
                 return -1;
             }, 1, seen);
-        } else if (c == "SkyboxBackground") {
-            fail("SkyboxBackground needs texture loading, which this build does not implement", RT_E_UNSUPPORTED);
+        } else if (c == "SkyboxBackground") {                                  // serialize.rs:759-776
+            static const char* kFaces[6] = {"px", "nx", "py", "ny", "pz", "nz"};
+            structure([&](const std::string& f, bool p) -> int {
+                for (int k = 0; k < 6; ++k) {
+                    if (f != kFaces[k]) continue;
+                    if (!p) {                                                  // load(path)
+                        expect_ident("load");
+                        expect(Tok::LParen, "LParen");
+                        const std::string path = expect(Tok::Str, "String").text;
+                        expect(Tok::RParen, "RParen");
+                        std::string why;
+                        const int rc = load_texture_file(path, s.skybox[k], why);
+                        if (rc != RT_OK) fail("error loading texture " + path + ": " + why, rc == RT_E_UNSUPPORTED ? rc : RT_E_PARSE);
+                    }
+                    return k;
+                }
+                return -1;
+            }, 6, seen);
+            s.background_kind = RT_BG_SKYBOX;
         } else {
             fail("no such class: " + c);
         }

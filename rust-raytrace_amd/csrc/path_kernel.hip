@@ -94,6 +94,52 @@ __device__ __forceinline__ void load_extension(const PathStack& st, int L, uint3
     F.key = st.key(L)[t];
 }
 
+// Texture::sample (texture.rs:46-58) of skybox face k: bilinear over
+// Color::from_srgb texels (color.rs:611-613), coordinates clamped to [0, 1].
+__device__ __forceinline__ double clamp01(double x) { return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x); }   // texture.rs:28-31
+
+__device__ __forceinline__ Col texel(const DevScene& sc, const DevTexFace& f, uint32_t x, uint32_t y) {
+    const uint8_t* p = sc.tex + f.off + 3ull * (x + static_cast<uint64_t>(y) * f.w);
+    return Col{sc.srgb_values[p[0]], sc.srgb_values[p[1]], sc.srgb_values[p[2]]};
+}
+
+__device__ __forceinline__ Col tex_sample(const DevScene& sc, int k, double u, double v) {
+    const DevTexFace f = sc.faces[k];
+    const double x = clamp01(u) * static_cast<double>(f.w - 1);
+    const double y = clamp01(v) * static_cast<double>(f.h - 1);
+    const uint32_t x0 = x >= 0.0 ? static_cast<uint32_t>(x) : 0u;   // `as u32`: NaN -> 0
+    const uint32_t y0 = y >= 0.0 ? static_cast<uint32_t>(y) : 0u;
+    const uint32_t x1 = x0 >= f.w - 1 ? f.w - 1 : x0 + 1;
+    const uint32_t y1 = y0 >= f.h - 1 ? f.h - 1 : y0 + 1;
+    const double xx = x - static_cast<double>(x0), yy = y - static_cast<double>(y0);
+    const Col a = texel(sc, f, x0, y0), b = texel(sc, f, x0, y1), c = texel(sc, f, x1, y0), d = texel(sc, f, x1, y1);
+    const Col cx0{a.r * (1.0 - yy) + b.r * yy, a.g * (1.0 - yy) + b.g * yy, a.b * (1.0 - yy) + b.b * yy};
+    const Col cx1{c.r * (1.0 - yy) + d.r * yy, c.g * (1.0 - yy) + d.g * yy, c.b * (1.0 - yy) + d.b * yy};
+    return Col{cx0.r * (1.0 - xx) + cx1.r * xx, cx0.g * (1.0 - xx) + cx1.g * xx, cx0.b * (1.0 - xx) + cx1.b * xx};
+}
+
+// Background::color (raytrace.rs:228-256): the solid colour, or the skybox
+// face the direction's dominant axis points at (x, then y, then z; no strict
+// winner: BLACK).
+__device__ __forceinline__ Col background(const DevScene& sc, const Ray& r) {
+    if (!sc.skybox) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};
+    const double dx = r.dx, dy = r.dy, dz = r.dz;
+    const double ax = fabs(dx), ay = fabs(dy), az = fabs(dz);
+    if (ax > az && ax > ay) {
+        const double px = -dz / dx, py = -dy / ax;
+        return tex_sample(sc, dx > 0.0 ? 0 : 1, px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    if (ay > ax && ay > az) {
+        const double px = dx / ay, py = dz / dy;
+        return tex_sample(sc, dy > 0.0 ? 2 : 3, px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    if (az > ax && az > ay) {
+        const double px = dx / dz, py = -dy / az;
+        return tex_sample(sc, dz > 0.0 ? 4 : 5, px * 0.5 + 0.5, py * 0.5 + 0.5);
+    }
+    return Col{0.0, 0.0, 0.0};
+}
+
 // camera.rs:76-80 (simple) and camera.rs:109-122 (depth of field; theta and
 // r2 keyed on the camera sample).
 __device__ __forceinline__ Ray camera_project(const DevScene& sc, double px, double py, uint64_t kc) {
@@ -270,7 +316,7 @@ __device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParam
         double csig = 0.0;
         int child = -1;
         if (h.obj == INT32_MAX) {
-            c = Col{sc.bg[0], sc.bg[1], sc.bg[2]};                     // SolidColorBackground (raytrace.rs:228-232)
+            c = background(sc, ray);                                    // raytrace.rs:228-256
         } else {
             const DevMaterial& m = sc.mats[h.obj];
             if (static_cast<uint32_t>(L) > fp.max_depth) {             // raytrace.rs:33 / 72 / 126 / 172

@@ -271,13 +271,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     // Every class of the reference except SkyboxBackground (textures) has a
     // device implementation: Phong / Fresnel chains on the wavefront path,
     // the stochastic and branching classes on the path kernel (needs_path).
-    if (s->background_kind != RT_BG_SOLID)
-        return fail(c, RT_E_UNSUPPORTED, "only SolidColorBackground is implemented on the device path");
+    if (s->background_kind != RT_BG_SOLID && s->background_kind != RT_BG_SKYBOX)
+        return fail(c, RT_E_INVALID, "bad background kind");
+    const bool skybox = s->background_kind == RT_BG_SKYBOX;
+    if (skybox)
+        for (const HostTexture& t : s->skybox)
+            if (t.width == 0 || t.height == 0 || t.rgb.size() != static_cast<size_t>(t.width) * t.height * 3)
+                return fail(c, RT_E_INVALID, "skybox face without texels");
     if (s->camera.kind != RT_CAMERA_SIMPLE && s->camera.kind != RT_CAMERA_DOF)
         return fail(c, RT_E_INVALID, "bad camera kind");
     if (s->camera.kind == RT_CAMERA_DOF && s->camera.samples == 0)
         return fail(c, RT_E_INVALID, "DepthOfFieldCamera with 0 samples");
-    bool needs_path = s->camera.kind == RT_CAMERA_DOF;
+    bool needs_path = s->camera.kind == RT_CAMERA_DOF || skybox;
     std::vector<DevSphere> spheres;
     std::vector<double> sx, sy, sz, srad;
     std::vector<int32_t> sphere_obj, plane_obj;
@@ -361,6 +366,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
     const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
     const size_t o_cam = place(camn.size() * sizeof(DevCamNode));
+    const size_t o_srgbv = place(256 * sizeof(double));
+    size_t tex_bytes = 0;
+    uint64_t face_off[6] = {0, 0, 0, 0, 0, 0};
+    if (skybox)
+        for (int k = 0; k < 6; ++k) { face_off[k] = tex_bytes; tex_bytes += s->skybox[k].rgb.size(); }
+    const size_t o_tex = place(tex_bytes);
     const size_t total = off ? off : 256;
     std::vector<uint8_t> host(total, 0);
     auto put = [&](size_t at, const void* p, size_t bytes) { if (bytes) std::memcpy(host.data() + at, p, bytes); };
@@ -373,6 +384,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
     put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
     put(o_cam, camn.data(), camn.size() * sizeof(DevCamNode));
+    put(o_srgbv, srgb_values_table(), 256 * sizeof(double));
+    if (skybox)
+        for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
     if (!c->d_blob) {
@@ -402,6 +416,11 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.has_fresnel = 0;
     for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
     d.needs_path = needs_path ? 1 : 0;
+    d.skybox = skybox ? 1 : 0;
+    d.tex = base + o_tex;
+    d.srgb_values = reinterpret_cast<const double*>(base + o_srgbv);
+    for (int k = 0; k < 6; ++k)
+        d.faces[k] = DevTexFace{skybox ? s->skybox[k].width : 0u, skybox ? s->skybox[k].height : 0u, face_off[k]};
     d.cam_dof = s->camera.kind == RT_CAMERA_DOF ? 1 : 0;
     d.cam_samples = d.cam_dof ? s->camera.samples : 1u;
     d.cam_focus = s->camera.focus;

@@ -61,6 +61,10 @@ class rt_camera(C.Structure):
                 ("matrix", C.c_double * 9), ("focus", C.c_double), ("aperture", C.c_double)]
 
 
+class rt_texture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgb", C.POINTER(C.c_uint8))]
+
+
 class rt_scene_desc(C.Structure):
     _fields_ = [("objects", C.POINTER(rt_object)), ("n_objects", C.c_uint32),
                 ("lights", C.POINTER(rt_light)), ("n_lights", C.c_uint32),
@@ -93,6 +97,8 @@ def _load():
         "rt_scene_from_desc": (C.c_int, [P(rt_scene_desc), P(C.c_void_p)]),
         "rt_scene_get_desc": (C.c_int, [C.c_void_p, P(rt_scene_desc)]),
         "rt_scene_free": (None, [C.c_void_p]),
+        "rt_scene_set_skybox": (C.c_int, [C.c_void_p, P(rt_texture)]),
+        "rt_texture_load": (C.c_int, [C.c_char_p, P(C.c_uint32), P(C.c_uint32), P(C.c_uint8), C.c_size_t]),
         "rt_camera_simple_new": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double), C.c_double, P(rt_camera)]),
         "rt_camera_look_at": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double), C.c_double, C.c_double,
                                         P(rt_camera)]),
@@ -162,6 +168,16 @@ def bmp_header(width, height):
     return bytes(buf), bw.value
 
 
+def texture_load(path):
+    """texture.rs:34-37 Texture::load -> uint8 [height, width, 3], rows top-down (BMP / binary PPM)."""
+    w, h = C.c_uint32(), C.c_uint32()
+    _check(lib.rt_texture_load(path.encode(), C.byref(w), C.byref(h), None, 0))
+    out = np.zeros((h.value, w.value, 3), np.uint8)
+    _check(lib.rt_texture_load(path.encode(), C.byref(w), C.byref(h), out.ctypes.data_as(C.POINTER(C.c_uint8)),
+                               out.size))
+    return out
+
+
 def write_bmp(path, width, height, bgr, pitch):
     arr = np.ascontiguousarray(bgr, dtype=np.uint8)
     _check(lib.rt_write_bmp(path.encode(), width, height, arr.ctypes.data_as(C.POINTER(C.c_uint8)), pitch))
@@ -189,6 +205,16 @@ class Scene:
         h = C.c_void_p()
         _check(lib.rt_scene_from_desc(C.byref(desc), C.byref(h)))
         return cls(h.value)
+
+    def set_skybox(self, faces):
+        """SkyboxBackground { px, nx, py, ny, pz, nz } from six uint8 [h, w, 3] arrays (copied)."""
+        arrs = [np.ascontiguousarray(f, dtype=np.uint8) for f in faces]
+        assert len(arrs) == 6 and all(a.ndim == 3 and a.shape[2] == 3 for a in arrs)
+        tex = (rt_texture * 6)()
+        for t, a in zip(tex, arrs):
+            t.width, t.height = a.shape[1], a.shape[0]
+            t.rgb = a.ctypes.data_as(C.POINTER(C.c_uint8))
+        _check(lib.rt_scene_set_skybox(self._h, tex))
 
     def desc(self):
         d = rt_scene_desc()

@@ -48,6 +48,7 @@ class SceneSpec:
     antialias: int = 1
     max_depth: int = 4          # not part of the file format (raytrace.rs:18 is a constant)
     name: str = "scene"
+    skybox: list = None         # six texture paths px, nx, py, ny, pz, nz (SkyboxBackground), or None
 
     # ---- builders ----
     def sphere(self, center, radius, material):
@@ -112,7 +113,11 @@ class SceneSpec:
                        f"{_f(cam['aperture'])}, {int(cam['samples'])})")
         else:
             out.append(f"    camera: SimplePerspectiveCamera {inner}")
-        out.append(f"    background: SolidColorBackground {{ color: {_rgb(self.background)} }}")
+        if self.skybox:
+            faces = " ".join(f'{k}: load("{p}")' for k, p in zip(("px", "nx", "py", "ny", "pz", "nz"), self.skybox))
+            out.append(f"    background: SkyboxBackground {{ {faces} }}")
+        else:
+            out.append(f"    background: SolidColorBackground {{ color: {_rgb(self.background)} }}")
         out.append(f"    options: {{ width: {self.width} height: {self.height} antialias: {self.antialias} }}")
         out.append("}")
         return "\n".join(out) + "\n"
@@ -254,6 +259,39 @@ def stochastic(width=96, height=64, antialias=4, max_depth=4, samples=2, dof=Fal
         s.area_light((3.0, 8.0, -2.0), (2.0, 0.0, 0.0), (0.0, 0.0, 2.0), (0.6, 0.55, 0.5))
     if dof:
         s.depth_of_field(7.0, 0.15, 2)
+    return s
+
+
+def write_ppm(path, rgb):
+    """Binary PPM (P6) of a uint8 [h, w, 3] array, rows top-down."""
+    import numpy as np
+    a = np.ascontiguousarray(rgb, dtype=np.uint8)
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (a.shape[1], a.shape[0]))
+        f.write(a.tobytes())
+
+
+def skybox_faces(size=16, seed=1):
+    """Six synthetic sky textures (gradients + noise, a distinct tint per face)."""
+    import numpy as np
+    rng = SplitMix64(seed)
+    faces = []
+    for k in range(6):
+        yy, xx = np.mgrid[0:size, 0:size]
+        base = np.stack([40 + 30 * k + 6 * xx, 200 - 8 * yy, 90 + 20 * ((xx + yy + k) % 5)], axis=-1)
+        noise = np.array([rng.next() % 23 for _ in range(size * size * 3)]).reshape(size, size, 3)
+        faces.append(np.clip(base + noise, 0, 255).astype(np.uint8))
+    return faces
+
+
+def skybox_scene(paths, width=96, height=64, max_depth=4):
+    """Mirror-like Phong and Fresnel spheres reflecting a SkyboxBackground (raytrace.rs:234-256)."""
+    s = SceneSpec(width=width, height=height, antialias=1, max_depth=max_depth, name="sky",
+                  camera=dict(DEFAULT_CAMERA), skybox=list(paths))
+    s.sphere((-1.5, 1.0, -6.0), 1.0, phong((0.1, 0.1, 0.1), (0.8, 0.8, 0.8), 64.0, (0.0, 0.0, 0.0)))
+    s.sphere((1.5, 1.0, -6.0), 1.0, fresnel((0.2, 0.2, 0.3), (1.0, 1.0, 1.0), 32.0, (0.0, 0.0, 0.0), 1.5))
+    s.sphere((0.0, 2.5, -9.0), 1.5, transparent((0.9, 0.9, 0.9), 64.0, 1.4))
+    s.point_light((-10.0, 10.0, 5.0), (0.8, 0.8, 0.8))
     return s
 
 

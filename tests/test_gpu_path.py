@@ -161,3 +161,30 @@ def test_random_jitter_one_sample_on_every_schedule(gpu_ctx, algo):
     spec = scenes.config3(160, 120, n=300)
     rgb, bgr, st = render(gpu_ctx, spec, seed=21, algo=algo)
     assert_exact(rgb, bgr, st, oracle(spec, seed=21))
+
+
+@pytest.mark.parametrize("jitter,spp", [(lr.RT_JITTER_CENTER, 1), (lr.RT_JITTER_RANDOM, 3)])
+def test_skybox_bit_exact(gpu_ctx, tmp_path, jitter, spp):
+    """SkyboxBackground (raytrace.rs:234-256, texture.rs:46-58): camera misses and
+    reflections sample the faces; only + - * / and table lookups, so bit-exact."""
+    faces = scenes.skybox_faces(size=24, seed=4)
+    paths = [str(tmp_path / f"f{k}.ppm") for k in range(6)]
+    for p, f in zip(paths, faces):
+        scenes.write_ppm(p, f)
+    spec = scenes.skybox_scene(paths, 128, 96)
+    spec.antialias = spp
+    rgb, bgr, st = render(gpu_ctx, spec, jitter=jitter, seed=13)
+    assert_exact(rgb, bgr, st, oracle(spec, jitter=jitter, seed=13))
+    # the C ABI route (rt_scene_set_skybox) gives the same image as the parsed file
+    sc = lr.Scene.deserialize(scenes.skybox_scene(paths, 128, 96).to_text())
+    sc2 = lr.Scene.deserialize(scenes.config2(8, 8).to_text())
+    gpu_ctx.upload(sc)
+    o = lr.render_opts(128, 96, max_depth=spec.max_depth, spp=spp, jitter=jitter, seed=13)
+    a = gpu_ctx.render(o)[1]
+    txt = scenes.skybox_scene(paths, 128, 96)
+    txt.skybox = None
+    sc3 = lr.Scene.deserialize(txt.to_text())
+    sc3.set_skybox(faces)
+    gpu_ctx.upload(sc3)
+    assert np.array_equal(gpu_ctx.render(o)[1], a)
+    del sc2

@@ -125,7 +125,8 @@ def test_depth_of_field_camera_parses():
     ("{ objects: [] lights: [] options: { width: 1.2.3", lr.RT_E_PARSE, "invalid number"),
     ("{ objects: [ { bounds: Cube { } } ] }", lr.RT_E_PARSE, "no such class: Cube"),
     ("{ objects: [", lr.RT_E_PARSE, "end of file"),
-    ("{ background: SkyboxBackground { } }", lr.RT_E_UNSUPPORTED, "Skybox"),
+    ("{ background: SkyboxBackground { } }", lr.RT_E_PARSE, "missing"),
+    ('{ background: SkyboxBackground { px: load("/nonexistent/sky.ppm") } }', lr.RT_E_PARSE, "error loading texture"),
     ("{ /* never closed ", lr.RT_E_PARSE, "unterminated"),
     ("{ objects: [ { bounds: Sphere { center: (1 2 3) radius: 1 } } ] }", lr.RT_E_PARSE, "expected Comma"),
 ])
@@ -198,3 +199,43 @@ def test_device_calls_fail_loudly_without_gpu():
     with pytest.raises(lr.RtError) as e:
         lr.Context(0)
     assert e.value.code == lr.RT_E_NODEVICE
+
+
+def test_texture_load_ppm_and_bmp(tmp_path):
+    """texture.rs:34-37: RGB8, rows top-down, from binary PPM and from a BMP (bottom-up BGR rows)."""
+    img = scenes.skybox_faces(size=5)[3][:, :4]            # 5 rows x 4 columns (odd row pitch in BMP)
+    ppm = str(tmp_path / "a.ppm")
+    scenes.write_ppm(ppm, img)
+    assert np.array_equal(lr.texture_load(ppm), img)
+    h, w = img.shape[:2]
+    pitch = (3 * w + 3) & ~3
+    rows = np.zeros((h, pitch), np.uint8)
+    for y in range(h):                                       # BMP row 0 = bottom = image row h-1
+        rows[y, :3 * w] = img[h - 1 - y][:, ::-1].reshape(-1)
+    bmp = str(tmp_path / "a.bmp")
+    lr.write_bmp(bmp, w, h, rows, pitch)
+    assert np.array_equal(lr.texture_load(bmp), img)
+    bad = tmp_path / "a.png"
+    bad.write_bytes(b"\x89PNG\r\n\x1a\n" + bytes(64))
+    with pytest.raises(lr.RtError) as e:
+        lr.texture_load(str(bad))
+    assert e.value.code == lr.RT_E_UNSUPPORTED
+
+
+def test_parse_skybox_background(tmp_path):
+    faces = scenes.skybox_faces(size=6)
+    paths = [str(tmp_path / f"f{k}.ppm") for k in range(6)]
+    for p, f in zip(paths, faces):
+        scenes.write_ppm(p, f)
+    sc = lr.Scene.deserialize(scenes.skybox_scene(paths).to_text())
+    assert sc.desc().background_kind == lr.RT_BG_SKYBOX
+    bad = tmp_path / "f.png"
+    bad.write_bytes(b"\x89PNG" + bytes(16))
+    spec = scenes.skybox_scene(paths[:5] + [str(bad)])
+    with pytest.raises(lr.RtError) as e:
+        lr.Scene.deserialize(spec.to_text())
+    assert e.value.code == lr.RT_E_UNSUPPORTED and "f.png" in str(e.value)
+    # the C ABI route: a solid-background scene turned into a skybox scene
+    sc2 = lr.Scene.deserialize(scenes.config2(8, 8).to_text())
+    sc2.set_skybox(faces)
+    assert sc2.desc().background_kind == lr.RT_BG_SKYBOX

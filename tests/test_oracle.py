@@ -186,3 +186,31 @@ def test_keyed_rng_is_independent_of_threads_and_tiles():
     assert np.array_equal(t["rgb64"].view(np.uint64), a["rgb64"][4:24, 8:32].view(np.uint64))
     c = ref64.render(spec, jitter=1, seed=6, rng=1)
     assert not np.array_equal(c["bgr"], a["bgr"])
+
+
+def test_skybox_known_answers(tmp_path):
+    """raytrace.rs:234-256 + texture.rs:46-58: a camera ray that misses samples the
+    face of its dominant axis; uniform faces give exactly Color::from_srgb."""
+    vals, _ = ref64.srgb_tables()
+    faces = [np.full((3, 3, 3), 10 * (k + 1), np.uint8) for k in range(6)]
+    paths = [str(tmp_path / f"f{k}.ppm") for k in range(6)]
+    for p, f in zip(paths, faces):
+        scenes.write_ppm(p, f)
+    for look, face in (((0, 0, -1), 5), ((0, 0, 1), 4), ((1, 0, 0), 0), ((-1, 0, 0), 1), ((0, 1, 0.01), 2),
+                       ((0, -1, 0.01), 3)):
+        up = (0, 1, 0) if abs(look[1]) < 0.5 else (0, 0, 1)
+        spec = scenes.SceneSpec(width=1, height=1, max_depth=0, skybox=paths,
+                                camera={"ctor": "new", "position": (0, 0, 0), "look": look, "up": up,
+                                        "im_dist": 1.0})
+        r = ref64.render(spec)
+        assert tuple(r["rgb64"][0, 0]) == (vals[10 * (face + 1)],) * 3, (look, face)
+    # bilinear: a 2x2 face sampled at its centre is the mean of the four texels' linear values
+    quad = np.array([[[0, 0, 0], [255, 255, 255]], [[255, 255, 255], [0, 0, 0]]], np.uint8)
+    for p in paths:
+        scenes.write_ppm(p, quad)
+    spec = scenes.SceneSpec(width=1, height=1, max_depth=0, skybox=paths,
+                            camera={"ctor": "new", "position": (0, 0, 0), "look": (0, 0, -1), "up": (0, 1, 0),
+                                    "im_dist": 1.0})
+    c = ref64.render(spec)["rgb64"][0, 0]
+    half = (vals[0] * 0.5 + vals[255] * 0.5) * 0.5 + (vals[255] * 0.5 + vals[0] * 0.5) * 0.5
+    assert tuple(c) == (half,) * 3

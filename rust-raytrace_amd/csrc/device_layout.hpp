@@ -109,6 +109,7 @@ struct DevScene {
     int32_t bvh4_root, n_bvh4;
     const DevCamNode* cam_nodes;    // camera view of the binary BVH (null: generation 0 traverses per ray)
     int32_t has_fresnel;            // some object uses FresnelMaterial
+    int32_t pfx2, pfx4;             // prefix sources: nodes of the binary / 4-wide tree staged in LDS (set per render)
     int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,
                                     // AreaLight, DepthOfFieldCamera)
     int32_t skybox;                 // SkyboxBackground (raytrace.rs:234-256; path kernel only)

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(kPathBlock, 4) void path_kernel(DevScene sc, FrameP
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     double* s_srgb = reinterpret_cast<double*>(lds);
     for (int i = threadIdx.x; i < 255; i += kPathBlock) s_srgb[i] = fp.srgb[i];
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, sc.cam_nodes, nullptr};
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     if constexpr (kNodes == 2) {
         DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds + 2048);
         for (int i = threadIdx.x; i < sc.n_bvh; i += kPathBlock) ln[i] = sc.bvh[i];

@@ -537,22 +537,33 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool fit2 = node_bytes + sph_bytes <= kLdsBudget;
             const bool fit4 = node4_bytes + sph_bytes <= kLdsBudget;
-            src = fit2 ? 7 : 2;
-            src_occ = fit4 ? 10 : 11;
-            if (!fit2 || !fit4) { src = 2; src_occ = 11; }
-            if (c->deep_bvh4) src_occ = src;                 // the 4-wide stack could overflow
+            // trees too large for LDS: the breadth-first top of each tree in LDS (8, 13)
+            src = fit2 ? 7 : 8;
+            src_occ = fit4 ? 10 : 13;
+            if (!fit2 || !fit4) { src = 8; src_occ = 13; }
+            if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;  // the 4-wide stack could overflow
             if (const char* force = std::getenv("RT_WF_SRC")) {
                 int n = -1, oc = -1;
                 const int got = std::sscanf(force, "%d,%d", &n, &oc);
                 if (got >= 1) { src = n; src_occ = got == 2 ? oc : n; }
             }
-            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || (v >= 10 && v <= 12); };
+            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
             const bool pair_ok = ok(src) && ok(src_occ) &&
-                                 (src == src_occ || (src == 7 && src_occ == 10) || (src == 2 && src_occ == 11));
-            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src >= 12) && !fit4) &&
-                              !((src_occ == 10 || src_occ >= 12) && !fit4);
+                                 ((src == src_occ && src != 8 && src != 13) || (src == 7 && src_occ == 10) ||
+                                  (src == 2 && src_occ == 11) || (src == 8 && (src_occ == 13 || src_occ == 11)) ||
+                                  (src == 2 && src_occ == 13));
+            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
+                              !((src_occ == 10 || src_occ == 12) && !fit4);
             if (!pair_ok || !fits) { src = 2; src_occ = 11; }
             if (c->deep_bvh4 && src_occ >= 10) src_occ = src = 2;
+            // LDS prefix sizes (RT_WF_PREFIX_KB = "nearest,shadow" overrides): measured at C4,
+            // 64 KB of binary nodes for the nearest-hit kernels; the 4-wide shadow tree stays in
+            // HBM/L2 by default (src 11), a prefix there costs more in co-residency than it saves
+            int kb2 = 64, kb4 = 0;
+            if (const char* pk = std::getenv("RT_WF_PREFIX_KB")) std::sscanf(pk, "%d,%d", &kb2, &kb4);
+            c->dsc.pfx2 = static_cast<int32_t>(static_cast<size_t>(std::max(kb2, 1)) * 1024 / sizeof(DevBvhNode));
+            c->dsc.pfx4 = static_cast<int32_t>(static_cast<size_t>(std::max(kb4, 1)) * 1024 / (kBvh4Planes * sizeof(DevBvh4Plane)));
+            if (src_occ == 13 && kb4 <= 0) src_occ = 11;
         } else {
             src = src_occ = fits_lds ? 1 : 0;
         }
@@ -588,7 +599,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // generation 0 by camera tile (RT_WF_CAM=0: per-ray like the other generations);
         // only with the binary-tree sources, whose node order the camera view shares
         int cam = 0;
-        if (src == 2 || src == 4 || src == 7) {
+        if (src == 2 || src == 4 || src == 7 || src == 8) {
             const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
             cam = cam_lds <= kLdsBudget ? 1 : 2;
             const int ce = env_int("RT_WF_CAM", -1);
@@ -596,6 +607,9 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             else if (ce == 2) cam = 2;
         }
         const uint32_t wg_major = env_int("RT_WF_DEAL", 1) != 0 ? 1u : 0u;
+        if (env_int("RT_WF_VERBOSE", 0))
+            std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d pfx %d/%d\n", src, src_occ, cam,
+                         nlists, c->deep_bvh4 ? 1 : 0, c->dsc.pfx2, c->dsc.pfx4);
         for (int l = 0; l < n_lanes; ++l) {
             if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
             rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1, nlists);

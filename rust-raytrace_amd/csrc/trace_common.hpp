@@ -304,6 +304,8 @@ struct BvhView {
     const int32_t* obj;
     const DevBvh4Plane* p4;      // 4-wide tree planes (LDS or HBM), stride n4
     int32_t n4;
+    const DevBvh4Plane* p4l;     // prefix sources: planes of 4-wide nodes [0, nl4) in LDS, stride nl4
+    int32_t nl4;
     const DevCamNode* cn;        // camera view of the binary tree (LDS or HBM)
     int32_t* stk;                // this wave's LDS traversal stack (camera sources)
 };
@@ -504,10 +506,16 @@ struct Node4Hits {
     int32_t c[4];
 };
 
+// kPrefix: nodes below v.nl4 (the breadth-first top of the tree) are read from
+// the LDS copy, the rest from HBM/L2.
+template <bool kPrefix = false>
 __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, const RayBox& rb, float tlim) {
     // axis by axis (as box_hit, same operations), so only two planes are live at a time
-    const int32_t N = v.n4;
+    int32_t N = v.n4;
     const DevBvh4Plane* P = v.p4 + node;
+    if constexpr (kPrefix) {
+        if (node < v.nl4) { N = v.nl4; P = v.p4l + node; }
+    }
     float tn[4], tf[4];
     {
         const DevBvh4Plane lo = P[0], hi = P[N];
@@ -636,7 +644,7 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
 // sphere the shadow ray starts on, which occludes it whenever the light is
 // behind that surface.  Any-hit: testing one sphere early cannot change the
 // answer (and the planes, with the NaN rule, are decided before it).
-template <bool kCount = false>
+template <bool kCount = false, bool kPrefix = false>
 __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                               double r2, int32_t hint, Work* w = nullptr) {
     bool plane_block = false;
@@ -672,7 +680,7 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
 #if RT_SEL4
             const Node4Hits n = node4_test_sel(v, cur, rb, sel, tlim);
 #else
-            const Node4Hits n = node4_test(v, cur, rb, tlim);
+            const Node4Hits n = node4_test<kPrefix>(v, cur, rb, tlim);
 #endif
             if constexpr (kCount) w->boxes += 4;
             int32_t next = kBvh4Empty;

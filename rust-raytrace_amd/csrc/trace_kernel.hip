@@ -260,6 +260,11 @@ constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-threa
 constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
 constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
 constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
+// Trees too large for LDS: the breadth-first top of the tree (DevScene::pfx2 /
+// pfx4 nodes, chosen by the host) in LDS, the rest and the spheres from HBM/L2
+// (64 VGPRs).
+constexpr int kSrcBvhP = 8;         // binary BVH, LDS prefix
+constexpr int kSrcBvh4P = 13;       // 4-wide BVH, LDS prefix
 // Generation 0 only: camera rays by 8x8 tile, a wave-uniform traversal of the
 // binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
 constexpr int kSrcCamL = 20;        // camera nodes + spheres in LDS
@@ -269,22 +274,34 @@ template <int kSrc>
 struct Src {
     static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
     static constexpr bool bvh = kSrc >= kSrcBvhG;
-    static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4L4;
+    static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P;
+    static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
                                     kSrc == kSrcCamL;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds;
-    static constexpr int nodes = all_lds ? 2 : 0;
+    static constexpr int nodes = all_lds ? 2 : prefix ? 1 : 0;
     static constexpr int waves = kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 ? 8 : 4;   // min waves per SIMD
 };
 
 // Per-wave traversal stack of the camera sources (wave-uniform entries).
 constexpr int kCamStack = 64;
 
+// Nodes of the LDS prefix of a prefix source.
+template <int kSrc>
+__host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
+    if (kSrc == kSrcBvhP) return min(sc.n_bvh, sc.pfx2);
+    if (kSrc == kSrcBvh4P) return min(sc.n_bvh4, sc.pfx4);
+    return 0;
+}
+
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
+    if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
+    if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
     if (Src<kSrc>::nodes > 0)
         bytes += Src<kSrc>::cam    ? static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode)
@@ -299,8 +316,23 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
 template <int kSrc>
 __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, sc.cam_nodes, nullptr};
+    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     size_t off = 0;
+    if constexpr (kSrc == kSrcBvhP) {
+        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
+        const int32_t nl = prefix_nodes<kSrc>(sc);
+        for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh[i];
+        v.lnodes = ln;
+        v.nl = nl;
+        return v;
+    } else if constexpr (kSrc == kSrcBvh4P) {
+        DevBvh4Plane* lp = reinterpret_cast<DevBvh4Plane*>(lds);
+        const int32_t nl = prefix_nodes<kSrc>(sc);
+        for (int i = threadIdx.x; i < kBvh4Planes * nl; i += T) lp[i] = sc.bvh4[(i / nl) * sc.n_bvh4 + i % nl];
+        v.p4l = lp;
+        v.nl4 = nl;
+        return v;
+    }
     if constexpr (Src<kSrc>::cam) {
         v.stk = reinterpret_cast<int32_t*>(lds) + (threadIdx.x >> 6) * kCamStack;
         off = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
@@ -348,7 +380,7 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
 template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, int32_t hint, Work* w) {
-    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount>(sc, v, r, has_range, r2, hint, w);
+    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount, Src<kSrc>::prefix>(sc, v, r, has_range, r2, hint, w);
     else if constexpr (Src<kSrc>::bvh) return occluded_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, has_range, r2, hint, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
@@ -962,6 +994,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvh4L4 * 101: RT_GEN(kSrcBvh4L4, kSrcBvh4L4); break;
         case kSrcBvhL8 * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8, kSrcBvh4L); break;
         case kSrcBvhG * 100 + kSrcBvh4G: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
+        case kSrcBvhP * 100 + kSrcBvh4P: RT_GEN(kSrcBvhP, kSrcBvh4P); break;
+        case kSrcBvhP * 100 + kSrcBvh4G: RT_GEN(kSrcBvhP, kSrcBvh4G); break;
+        case kSrcBvhG * 100 + kSrcBvh4P: RT_GEN(kSrcBvhG, kSrcBvh4P); break;
         default: RT_GEN(kSrcBvh4G, kSrcBvh4G); break;
         }
 #undef RT_GEN

@@ -105,7 +105,7 @@ int env_int(const char* name, int dflt) {
 uint32_t wf_chunk_pixels() {
     const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
     long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<uint32_t>(v) : (1u << 24);
+    return v > 0 ? static_cast<uint32_t>(v) : (1u << 25);   // 33.5 M pixels: ~17 GB of working set at depth 8
 }
 
 // The b streams need hardware queues of their own: HIP deals streams over a
@@ -136,7 +136,13 @@ int ensure_lanes(rt_ctx* c, int n) {
         rt_ctx::Lane L;
         c->lanes.push_back(L);
         rt_ctx::Lane& M = c->lanes.back();
-        HIP_TRY(c, hipStreamCreateWithFlags(&M.s, hipStreamNonBlocking));
+        // RT_WF_PRIO=1: the nearest-hit chain (the critical path) on a high-priority stream
+        int lo = 0, hi = 0;
+        if (env_int("RT_WF_PRIO", 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+            HIP_TRY(c, hipStreamCreateWithPriority(&M.s, hipStreamNonBlocking, hi));
+        } else {
+            HIP_TRY(c, hipStreamCreateWithFlags(&M.s, hipStreamNonBlocking));
+        }
         HIP_TRY(c, hipEventCreateWithFlags(&M.mark, hipEventDisableTiming));
         HIP_TRY(c, hipEventCreateWithFlags(&M.done, hipEventDisableTiming));
         M.near_done.assign(kMaxGenerations, nullptr);
@@ -568,9 +574,12 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             src = src_occ = fits_lds ? 1 : 0;
         }
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
+        // (balanced: a frame slightly over the cap becomes two halves, not a full chunk plus a
+        // sliver that pays every generation's launch latency again)
         uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
         const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
+        chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);
         const int n_lanes = std::max(1, std::min<int>(env_int("RT_WF_STREAMS", 1), static_cast<int>(n_chunks)));
         const int mark_gen = std::max(0, std::min<int>(env_int("RT_WF_STAGGER_GEN", 1), static_cast<int>(o->max_depth) + 1));
         int rc2 = ensure_lanes(c, n_lanes);

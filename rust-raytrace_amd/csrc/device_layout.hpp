@@ -139,6 +139,7 @@ struct FrameParams {
     int32_t jitter;                 // rt_jitter: 0 centre, 1 keyed random draws (path kernel)
     uint64_t seed;                  // keyed RNG seed (path kernel)
     const double* srgb;             // the 255 sRGB thresholds in HBM (path kernel stages them in LDS)
+    uint32_t path_group;            // path kernel: lanes per pixel (power of two <= 64), sharing its AA samples
 };
 
 

@@ -385,30 +385,48 @@ __global__ __launch_bounds__(kPathBlock, 4) void path_kernel(DevScene sc, FrameP
     const uint64_t npix = static_cast<uint64_t>(fp.tile_w) * fp.rows;
     uint64_t rays = 0, shadows = 0;
     const double ns = static_cast<double>(sc.cam_samples), aa = static_cast<double>(fp.spp);
-    for (uint64_t p = t; p < npix; p += st.T) {                        // main.rs:45-56
+    // G = fp.path_group lanes of one wave share a pixel: lane j of the group traces
+    // AA samples j, j + G, ..., and the group adds the sample colours in sample
+    // order through cross-lane reads, so the sum is main.rs:47-55's
+    // `res = res + raytrace(..)` sequence exactly.  G > 1 when the frame has too
+    // few pixels to fill the chip one pixel per lane (C1: 64 k pixels x 1024 samples).
+    const uint32_t G = fp.path_group;
+    const uint32_t lane = threadIdx.x & 63u, gl = lane & (G - 1u), gbase = lane - gl;
+    for (uint64_t p = t / G; p < npix; p += st.T / G) {               // main.rs:45-56
         const uint32_t lx = static_cast<uint32_t>(p % fp.tile_w);
         const uint32_t lr = fp.row0 + static_cast<uint32_t>(p / fp.tile_w);
         const uint32_t x = fp.x0 + lx;
         const uint32_t y = fp.y0 + ((lr / fp.band) * fp.band_stride + fp.band_phase) * fp.band + lr % fp.band;
         const uint64_t kp = key_pixel(fp.seed, x, y);
         Col res{0.0, 0.0, 0.0};
-        for (uint32_t a = 0; a < fp.spp; ++a) {
-            const uint64_t ka = key_child(kp, a);
-            const double jx = fp.jitter ? key_f64(ka, 0) : 0.5;       // x drawn before y (main.rs:51-52)
-            const double jy = fp.jitter ? key_f64(ka, 1) : 0.5;
-            const double px = ((static_cast<double>(x) + jx) - fp.hw) * fp.scale;
-            const double py = ((static_cast<double>(y) + jy) - fp.hh) * fp.scale;
+        for (uint32_t a0 = 0; a0 < fp.spp; a0 += G) {
+            const uint32_t a = a0 + gl;
             Col r{0.0, 0.0, 0.0};                                      // raytrace.rs:270-276
-            for (uint32_t cs = 0; cs < sc.cam_samples; ++cs) {
-                const uint64_t kc = key_child(ka, cs);
-                const Col c = trace_path<kNodes>(sc, v, fp, st, t, camera_project(sc, px, py, kc), kc, rays, shadows);
-                r = Col{r.r + c.r, r.g + c.g, r.b + c.b};
+            if (a < fp.spp) {
+                const uint64_t ka = key_child(kp, a);
+                const double jx = fp.jitter ? key_f64(ka, 0) : 0.5;   // x drawn before y (main.rs:51-52)
+                const double jy = fp.jitter ? key_f64(ka, 1) : 0.5;
+                const double px = ((static_cast<double>(x) + jx) - fp.hw) * fp.scale;
+                const double py = ((static_cast<double>(y) + jy) - fp.hh) * fp.scale;
+                for (uint32_t cs = 0; cs < sc.cam_samples; ++cs) {
+                    const uint64_t kc = key_child(ka, cs);
+                    const Col c = trace_path<kNodes>(sc, v, fp, st, t, camera_project(sc, px, py, kc), kc, rays, shadows);
+                    r = Col{r.r + c.r, r.g + c.g, r.b + c.b};
+                }
+                r = Col{r.r / ns, r.g / ns, r.b / ns};
             }
-            r = Col{r.r / ns, r.g / ns, r.b / ns};
-            res = Col{res.r + r.r, res.g + r.g, res.b + r.b};
+            if (G == 1) {
+                res = Col{res.r + r.r, res.g + r.g, res.b + r.b};
+            } else {
+                const uint32_t m = min(G, fp.spp - a0);
+                for (uint32_t j = 0; j < m; ++j) {                     // sample order
+                    const int src = static_cast<int>(gbase + j);
+                    res = Col{res.r + __shfl(r.r, src, 64), res.g + __shfl(r.g, src, 64), res.b + __shfl(r.b, src, 64)};
+                }
+            }
         }
         res = Col{res.r / aa, res.g / aa, res.b / aa};
-        write_pixel(fp, lx, lr, res, s_srgb);
+        if (gl == 0) write_pixel(fp, lx, lr, res, s_srgb);
     }
     for (int off = 32; off > 0; off >>= 1) {
         rays += __shfl_xor(rays, off, 64);
@@ -431,7 +449,7 @@ size_t path_lds_bytes(const DevScene& sc, bool staged) {
 
 hipError_t launch_path(const DevScene& sc, const FrameParams& fp, const PathStack& st, bool staged, hipStream_t stream) {
     const uint64_t npix = static_cast<uint64_t>(fp.tile_w) * fp.rows;
-    const uint64_t want = (npix + kPathBlock - 1) / kPathBlock;
+    const uint64_t want = (npix * fp.path_group + kPathBlock - 1) / kPathBlock;   // path_group lanes per pixel
     const dim3 grid(static_cast<uint32_t>(want < st.T / kPathBlock ? want : st.T / kPathBlock));
     if (grid.x == 0) return hipSuccess;
     if (staged) hipLaunchKernelGGL(path_kernel<2>, grid, dim3(kPathBlock), path_lds_bytes(sc, true), stream, sc, fp, st);

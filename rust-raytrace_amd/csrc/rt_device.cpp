@@ -675,8 +675,15 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // persistent grid: enough work-items to fill every CU; each owns one
         // recursion stack of max_depth + 1 frames (PathStack)
         const uint64_t npix = static_cast<uint64_t>(o->tile_w) * o->tile_h;
-        const uint32_t T_full = static_cast<uint32_t>(c->n_cu) * 2048u;
-        const uint32_t T = static_cast<uint32_t>(std::min<uint64_t>(T_full, (npix + 255) / 256 * 256));
+        // 1024 work-items per CU = the kernel's occupancy (128 VGPRs: 4 waves per SIMD)
+        const uint32_t T_full = static_cast<uint32_t>(c->n_cu) * 1024u;
+        // lanes per pixel: enough work-items to fill the chip, at most one per AA sample
+        uint32_t G = 1;
+        while (G < 64 && 2 * G <= spp && npix * G < T_full) G *= 2;
+        if (const int ge = env_int("RT_PATH_GROUP", 0)) G = static_cast<uint32_t>(ge);   // A/B override
+        if (G == 0 || (G & (G - 1)) || G > 64) G = 1;
+        fp.path_group = G;
+        const uint32_t T = static_cast<uint32_t>(std::min<uint64_t>(T_full, (npix * G + 255) / 256 * 256));
         PathStack ps{};
         ps.T = T;
         ps.levels = o->max_depth + 1;

@@ -11,7 +11,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 
 
 def family(name):
-    m = re.search(r"(wf_\w+<[^>]*>|wf_\w+|trace_frame_kernel<[^>]*>)", name)
+    m = re.search(r"(wf_\w+<[^>]*>|wf_\w+|trace_frame_kernel<[^>]*>|path_kernel<[^>]*>)", name)
     return m.group(1) if m else name[:40]
 
 

@@ -8,7 +8,8 @@
 // the frame (no collective: pixels are independent, main.rs:45-57).
 //
 //   raytrace [--scene FILE] [--out FILE] [--width W] [--height H] [--spp N]
-//            [--max-depth D] [--gpus N] [--band ROWS] [--algo auto|lds|global]
+//            [--max-depth D] [--gpus N] [--band ROWS] [--jitter random|center] [--seed N]
+//            [--algo auto|wavefront|path|lds|global]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +31,8 @@ struct Args {
     int gpus = 1;
     unsigned band = 16;
     int algo = RT_ALGO_AUTO;
+    int jitter = RT_JITTER_RANDOM;     // main.rs:51-52 jitters every sample; --jitter center = parity mode
+    unsigned long long seed = 1;       // keyed draws (the reference seeds from OS entropy, main.rs:43)
 };
 
 bool parse_args(int argc, char** argv, Args& a) {
@@ -45,12 +48,16 @@ bool parse_args(int argc, char** argv, Args& a) {
         else if (k == "--max-depth" && (v = val())) a.max_depth = static_cast<unsigned>(std::atol(v));
         else if (k == "--gpus" && (v = val())) a.gpus = std::atoi(v);
         else if (k == "--band" && (v = val())) a.band = static_cast<unsigned>(std::atol(v));
+        else if (k == "--seed" && (v = val())) a.seed = std::strtoull(v, nullptr, 0);
+        else if (k == "--jitter" && (v = val())) a.jitter = std::string(v) == "center" ? RT_JITTER_CENTER : RT_JITTER_RANDOM;
         else if (k == "--algo" && (v = val())) {
             std::string s = v;
-            a.algo = s == "lds" ? RT_ALGO_BRUTE_LDS : s == "global" ? RT_ALGO_BRUTE_GLOBAL : RT_ALGO_AUTO;
+            a.algo = s == "lds" ? RT_ALGO_BRUTE_LDS : s == "global" ? RT_ALGO_BRUTE_GLOBAL
+                   : s == "wavefront" ? RT_ALGO_WAVEFRONT : s == "path" ? RT_ALGO_PATH : RT_ALGO_AUTO;
         } else {
             std::fprintf(stderr, "usage: raytrace [--scene FILE] [--out FILE] [--width W] [--height H] [--spp N]\n"
-                                 "                [--max-depth D] [--gpus N] [--band ROWS] [--algo auto|lds|global]\n");
+                                 "                [--max-depth D] [--gpus N] [--band ROWS] [--jitter random|center]\n"
+                                 "                [--seed N] [--algo auto|wavefront|path|lds|global]\n");
             return false;
         }
     }
@@ -108,7 +115,7 @@ int main(int argc, char** argv) {
             std::vector<uint8_t> local(static_cast<size_t>(pitch) * my_rows);
             rt_render_opts o;
             rt_render_opts_default(&o, W, H);
-            o.max_depth = a.max_depth; o.spp = spp; o.algo = a.algo;
+            o.max_depth = a.max_depth; o.spp = spp; o.algo = a.algo; o.jitter = a.jitter; o.seed = a.seed;
             o.flags = RT_OUT_BGR_U8; o.bgr_pitch = pitch;
             o.band = band; o.band_stride = G; o.band_phase = g; o.tile_h = my_full * band;
             if (o.tile_h && (rc[g] = rt_render(ctx, &o, nullptr, local.data(), &st[g])) != RT_OK) {
@@ -118,7 +125,7 @@ int main(int argc, char** argv) {
             if (H % band && full_bands % G == static_cast<uint32_t>(g)) {
                 rt_render_opts t;
                 rt_render_opts_default(&t, W, H);
-                t.max_depth = a.max_depth; t.spp = spp; t.algo = a.algo;
+                t.max_depth = a.max_depth; t.spp = spp; t.algo = a.algo; t.jitter = a.jitter; t.seed = a.seed;
                 t.flags = RT_OUT_BGR_U8; t.bgr_pitch = pitch;
                 t.y0 = full_bands * band; t.tile_h = H % band;
                 rt_stats ts{};

@@ -188,3 +188,23 @@ def test_skybox_bit_exact(gpu_ctx, tmp_path, jitter, spp):
     gpu_ctx.upload(sc3)
     assert np.array_equal(gpu_ctx.render(o)[1], a)
     del sc2
+
+
+def test_cli_renders_the_reference_scene(tmp_path):
+    """The main.rs replacement end to end: test_scene.txt in, out.bmp out (header
+    bytes as bmp.rs writes them; pixels statistically equal to the reference's)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "rust-raytrace_amd", "raytrace")
+    out = str(tmp_path / "out.bmp")
+    r = subprocess.run([exe, "--scene", os.path.join(root, "tests", "golden", "test_scene.txt"), "--out", out,
+                        "--width", "200", "--height", "200", "--seed", "77"],
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    data = open(out, "rb").read()
+    hdr, pitch = lr.bmp_header(200, 200)
+    assert data[:122] == hdr and len(data) == 122 + pitch * 200
+    bgr = np.frombuffer(data[122:], np.uint8).reshape(200, pitch)[:, :600]
+    rms, mx = check_out_bmp_statistics(bgr)
+    print(f"CLI out.bmp: rms {rms:.3f} LSB vs the reference's out.bmp")

@@ -227,6 +227,7 @@ struct WfBufs {
     uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
     uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
     uint32_t tiles_x;               // 8x8 tiles per row of the chunk
+    uint32_t spread_below;          // queues below this many items are dealt workgroup-first regardless
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
 

@@ -75,6 +75,7 @@ struct WfStreams {
     LaunchMarks* mb[kMaxBStreams];
     bool fuse;
     int cam;            // generation 0: 0 per-ray traversal, 1 camera tiles (LDS), 2 camera tiles (HBM/L2)
+    bool lists0;        // shadow item lists from generation 0 (else from generation 1)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

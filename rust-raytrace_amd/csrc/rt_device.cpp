@@ -625,6 +625,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
+            c->lanes[l].b.spread_below = static_cast<uint32_t>(std::max(0, env_int("RT_WF_SPREAD_BELOW", 0)));
         }
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
         // per-launch timing needs one in-order stream
@@ -663,6 +664,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
             ws.cam = cam;
+            ws.lists0 = env_int("RT_WF_LISTS0", 0) != 0;
             HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, ws, L.mark, mark_gen));
         }
         for (int l = 0; l < n_lanes; ++l) {

@@ -159,19 +159,23 @@ __device__ __forceinline__ uint32_t lds_append(uint32_t* counter, bool want) {
 // CU for the kernels of the other stream).  Either way a workgroup takes at
 // most 16 chunks per round of W, i.e. at most R items.  Loop condition and
 // chunk are wave-uniform.
-__device__ __forceinline__ uint32_t wave_slot(const WfBufs& b) {
+// A queue smaller than b.spread_below items is always dealt workgroup-first
+// (its few chunks then occupy every CU instead of a few whole workgroups).
+__device__ __forceinline__ bool deal_major(const WfBufs& b, uint32_t n) { return b.wg_major && n >= b.spread_below; }
+
+__device__ __forceinline__ uint32_t wave_slot(const WfBufs& b, uint32_t n) {
     const uint32_t wave = threadIdx.x >> 6;
-    return b.wg_major ? blockIdx.x * (kWfThreads / 64) + wave : wave * b.G + blockIdx.x;
+    return deal_major(b, n) ? blockIdx.x * (kWfThreads / 64) + wave : wave * b.G + blockIdx.x;
 }
 
 // Whether this workgroup's first chunk is below n (workgroup-uniform).
 __device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n) {
-    const uint64_t first = b.wg_major ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
+    const uint64_t first = deal_major(b, n) ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
     return first * 64u < n;
 }
 
 #define RT_FOR_CHUNKS(b, n, j)                                                              \
-    for (uint32_t rt_c = wave_slot(b), rt_w = (b).G * (kWfThreads / 64);                     \
+    for (uint32_t rt_c = wave_slot(b, n), rt_w = (b).G * (kWfThreads / 64);                  \
          static_cast<uint64_t>(rt_c) * 64u < static_cast<uint64_t>(n); rt_c += rt_w)        \
         if (const uint32_t j = rt_c * 64u + (threadIdx.x & 63u); true)
 
@@ -915,11 +919,17 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
 #define RT_NEARL(S, FR) hipLaunchKernelGGL((wf_nearest<S, false, kCount, FR, true>), grid, block, \
                                            staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
     // shadow lists from generation 1 on (generation 0 feeds every (record, light) pair to the plain shadow kernel)
-    const bool lists = b.nlists != 0 && k >= 1;
+#define RT_NEARC(S, FR, L) hipLaunchKernelGGL((wf_nearest<S, true, kCount, FR, L>), grid, block, \
+                                              staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+    const bool lists = b.nlists != 0 && (k >= 1 || ws.lists0);
     if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
-        if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
+        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamL, true, true); else RT_NEARC(kSrcCamL, false, true); }
+        else if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
     } else if (k == 0 && ws.cam == 2) {
-        if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
+        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamG, true, true); else RT_NEARC(kSrcCamG, false, true); }
+        else if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
+    } else if (k == 0 && lists) {
+        if (sc.has_fresnel) RT_NEARC(kSrcN, true, true); else RT_NEARC(kSrcN, false, true);
     } else if (k == 0) {
         if (sc.has_fresnel) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, true, false);
     } else if (lists) {
@@ -927,6 +937,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     } else {
         if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
     }
+#undef RT_NEARC
 #undef RT_NEARL
 #undef RT_NEAR
     (void)lds_n;

@@ -85,6 +85,7 @@ hipError_t upload_srgb_table(const double* avg255);
 // keyed random draws, one work-item per pixel over the HBM recursion stack.
 // staged: binary BVH + spheres in LDS (path_lds_bytes(sc, true) must fit).
 size_t path_lds_bytes(const DevScene& sc, bool staged);
+int path_waves_per_simd();          // the path kernel's occupancy (its launch bounds)
 hipError_t launch_path(const DevScene& sc, const FrameParams& fp, const PathStack& st, bool staged, hipStream_t stream);
 
 }  // namespace rtamd

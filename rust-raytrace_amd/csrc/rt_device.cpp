@@ -677,8 +677,8 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // persistent grid: enough work-items to fill every CU; each owns one
         // recursion stack of max_depth + 1 frames (PathStack)
         const uint64_t npix = static_cast<uint64_t>(o->tile_w) * o->tile_h;
-        // 1024 work-items per CU = the kernel's occupancy (128 VGPRs: 4 waves per SIMD)
-        const uint32_t T_full = static_cast<uint32_t>(c->n_cu) * 1024u;
+        // work-items per CU = the kernel's occupancy (4 SIMDs x waves per SIMD x 64 lanes)
+        const uint32_t T_full = static_cast<uint32_t>(c->n_cu) * 256u * static_cast<uint32_t>(path_waves_per_simd());
         // lanes per pixel: enough work-items to fill the chip, at most one per AA sample
         uint32_t G = 1;
         while (G < 64 && 2 * G <= spp && npix * G < T_full) G *= 2;

@@ -9,10 +9,10 @@
  * It is a plain-C f64 restatement of the reference algorithm, following:
  *   main.rs:39-59        pixel mapping, AA loop and average, BGR row write
  *   camera.rs:51-80      SimplePerspectiveCamera new / look_at / project
- *   camera.rs:83-123     DepthOfFieldCamera (stochastic; statistical only)
+ *   camera.rs:83-123     DepthOfFieldCamera (stochastic: keyed draws = the device's, REF_RNG_KEYED)
  *   raytrace.rs:17-28    MIN_SIGNIFICANCE, MAX_DEPTH (a parameter here), clamps
  *   raytrace.rs:30-67    PhongMaterial::color
- *   raytrace.rs:69-121   IndirectPhongMaterial::color (stochastic)
+ *   raytrace.rs:69-121   IndirectPhongMaterial::color (stochastic; keyed or XorShift draws)
  *   raytrace.rs:123-167  FresnelMaterial::color
  *   raytrace.rs:169-226  TransparentMaterial::color
  *   raytrace.rs:228-256  SolidColorBackground, SkyboxBackground (texture.rs:46-58 sampling)

@@ -208,3 +208,47 @@ def test_cli_renders_the_reference_scene(tmp_path):
     bgr = np.frombuffer(data[122:], np.uint8).reshape(200, pitch)[:, :600]
     rms, mx = check_out_bmp_statistics(bgr)
     print(f"CLI out.bmp: rms {rms:.3f} LSB vs the reference's out.bmp")
+
+
+def _edge_scene():
+    """Reference quirks and corner cases of the stochastic / branching classes."""
+    spec = scenes.SceneSpec(width=72, height=48, antialias=2, max_depth=3, camera=dict(scenes.DEFAULT_CAMERA),
+                            background=(0.3, 0.2, 0.1))
+    # IndirectPhong with ks > 0: the specular term is pow(NaN, exp) (raytrace.rs:108,115) -> NaN pixels
+    spec.sphere((-2.0, 1.0, -6.0), 1.0, scenes.indirect_phong((0.5, 0.5, 0.5), (0.2, 0.2, 0.2), 8.0, (0.0,) * 3, 1))
+    # IndirectPhong with samples = 0: direct light only, no bounce
+    spec.sphere((0.0, 1.0, -6.0), 1.0, scenes.indirect_phong((0.4, 0.6, 0.2), (0.0,) * 3, 1.0, (0.01,) * 3, 0))
+    # dense glass: total internal reflection inside (refract None -> fresnel 1)
+    spec.sphere((2.0, 1.0, -6.0), 1.0, scenes.transparent((1.0, 1.0, 1.0), 32.0, 2.4))
+    spec.plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), scenes.phong((0.5, 0.5, 0.5), (0.3,) * 3, 16.0, (0.01,) * 3))
+    spec.area_light((-1.0, 6.0, -4.0), (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), (0.5, 0.5, 0.5))   # degenerate: a point
+    spec.area_light((2.0, 7.0, -3.0), (1.5, 0.0, 0.0), (0.0, 0.0, 1.5), (0.4, 0.4, 0.4))
+    spec.directional_light((0.0, -1.0, -0.5), (0.2, 0.2, 0.2))
+    return spec
+
+
+def test_stochastic_edge_cases_bit_exact_without_bounces(gpu_ctx):
+    spec = _edge_scene()
+    spec.objects = [o for o in spec.objects if o["material"].get("samples", 0) == 0]   # no cos/sin draws
+    for depth in (0, 3):
+        spec.max_depth = depth
+        rgb, bgr, st = render(gpu_ctx, spec, seed=31)
+        assert_exact(rgb, bgr, st, oracle(spec, seed=31))
+
+
+def test_stochastic_edge_cases_close(gpu_ctx):
+    spec = _edge_scene()
+    rgb, bgr, st = render(gpu_ctx, spec, seed=32)
+    ref = oracle(spec, seed=32)
+    assert_close(bgr, st, ref)
+    assert np.isnan(rgb).any() and np.array_equal(np.isnan(rgb), np.isnan(ref["rgb32"]))   # the NaN quirk, same pixels
+
+
+def test_dof_aperture_zero_equals_pinhole_rays(gpu_ctx):
+    """DepthOfFieldCamera with aperture 0: every lens sample starts on the image
+    plane point and aims at the focal point (camera.rs:109-122); keyed, exact."""
+    spec = scenes.config2(64, 36)
+    spec.depth_of_field(6.0, 0.0, 3)
+    rgb, bgr, st = render(gpu_ctx, spec, jitter=lr.RT_JITTER_CENTER)
+    ref = oracle(spec, jitter=0, seed=7)
+    assert_close(bgr, st, ref, min_equal=0.999)

@@ -555,7 +555,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             }
             auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
             const bool pair_ok = ok(src) && ok(src_occ) &&
-                                 ((src == src_occ && src != 8 && src != 13) || (src == 7 && src_occ == 10) ||
+                                 ((src == src_occ && src != 13) || (src == 7 && src_occ == 10) ||
                                   (src == 2 && src_occ == 11) || (src == 8 && (src_occ == 13 || src_occ == 11)) ||
                                   (src == 2 && src_occ == 13));
             const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src == 12) && !fit4) &&

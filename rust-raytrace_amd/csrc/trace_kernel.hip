@@ -1006,6 +1006,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvhL8 * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8, kSrcBvh4L); break;
         case kSrcBvhG * 100 + kSrcBvh4G: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
         case kSrcBvhP * 100 + kSrcBvh4P: RT_GEN(kSrcBvhP, kSrcBvh4P); break;
+        case kSrcBvhP * 101: RT_GEN(kSrcBvhP, kSrcBvhP); break;
         case kSrcBvhP * 100 + kSrcBvh4G: RT_GEN(kSrcBvhP, kSrcBvh4G); break;
         case kSrcBvhG * 100 + kSrcBvh4P: RT_GEN(kSrcBvhG, kSrcBvh4P); break;
         default: RT_GEN(kSrcBvh4G, kSrcBvh4G); break;

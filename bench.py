@@ -63,6 +63,9 @@ def parse():
                         "its time is what each rank of an N-GPU run spends")
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N > 1: process-group backend for the barrier and the max-over-ranks timing (nccl = RCCL; "
+                        "gloo rehearses N ranks on fewer GPUs, ranks sharing a device round-robin)")
     return p.parse_args()
 
 
@@ -112,9 +115,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":
+        local %= max(1, torch.cuda.device_count())      # rehearsal: several ranks per device
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     cfg = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
@@ -217,7 +225,7 @@ def main():
     host_ms = min(host_ms)
 
     t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms, float(wst.sphere_tests), float(wst.box_tests)],
-                     dtype=torch.float64, device=dev)
+                     dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -259,7 +267,7 @@ def main():
             "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak" if (n_split > 1 and args.scaling == "weak") else "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
                        "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth, "spp": spp,
                        "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}",

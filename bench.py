@@ -63,6 +63,9 @@ def parse():
                         "its time is what each rank of an N-GPU run spends")
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
+    p.add_argument("--inflight", type=int, default=1,
+                   help="frames in flight: F contexts (each its own working set and streams) render successive "
+                        "steps into F output buffers, so frame i+1's first generations overlap frame i's tail")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: process-group backend for the barrier and the max-over-ranks timing (nccl = RCCL; "
                         "gloo rehearses N ranks on fewer GPUs, ranks sharing a device round-robin)")
@@ -149,9 +152,12 @@ def main():
     spp = spec.antialias
     jitter = lr.RT_JITTER_RANDOM if path_cfg else lr.RT_JITTER_CENTER
     W, H = spec.width, spec.height
-    ctx = lr.Context(local)
     scene = lr.Scene.deserialize(spec.to_text())
-    ctx.upload(scene)
+    F = max(1, args.inflight)
+    ctxs = [lr.Context(local) for _ in range(F)]
+    for c in ctxs:
+        c.upload(scene)
+    ctx = ctxs[0]
     rows = shard.local_rows(H, BAND, band_world, rank)
     tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, band_world) == rank else None
     assert tail is None or len(tail) == 0, "bench frames are whole bands"
@@ -161,11 +167,13 @@ def main():
                   spp=spp, algo=algo, jitter=jitter, seed=cfg[3])
     opts = lr.render_opts(W, H, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8, **common)
     pitch = 3 * W
-    out_rgb = torch.empty((len(rows), W, 3), dtype=torch.float32, device=dev)
-    out_bgr = torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)
+    outs = [(torch.empty((len(rows), W, 3), dtype=torch.float32, device=dev),
+             torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)) for _ in range(F)]
+    out_rgb, out_bgr = outs[0]
     # a real (non-null) stream: the library launches on exactly this stream, so the
     # torch events below bracket the kernel (handle 0 would select the context's own stream)
-    stream = torch.cuda.Stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    stream = streams[0]
 
     # per-kernel-family launch durations come from K more frames that record HIP
     # events around every launch (RT_TIME_KERNELS), after the timed region: the
@@ -173,11 +181,12 @@ def main():
     timed_flags = opts.flags | lr.RT_TIME_KERNELS
     opts_timed = lr.render_opts(W, H, flags=timed_flags, **common)
 
-    def step(o=opts):
-        ctx.render_device(o, out_rgb.data_ptr(), out_bgr.data_ptr(), stream.cuda_stream)
+    def step(o=opts, i=0):
+        f = i % F
+        ctxs[f].render_device(o, outs[f][0].data_ptr(), outs[f][1].data_ptr(), streams[f].cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(max(args.warmup, F)):
+        step(i=i)
     torch.cuda.synchronize(dev)
     st = ctx.stats()                       # rays of one frame-slice (deterministic: same every step)
     local_rays = st.rays
@@ -189,9 +198,9 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
+        evs[i][0].record(streams[i % F])
+        step(i=i)
+        evs[i][1].record(streams[i % F])
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -270,7 +279,7 @@ def main():
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
                        "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth, "spp": spp,
-                       "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}",
+                       "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}", "frames_in_flight": F,
                        "algo": args.algo},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -304,7 +313,8 @@ def main():
             except Exception as e:  # the oracle is optional on a box where it was not built
                 line["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(line), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

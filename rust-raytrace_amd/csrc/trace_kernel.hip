@@ -251,8 +251,48 @@ __device__ __forceinline__ void tile_rect(const FrameParams& fp, const WfBufs& b
     ty0 = __double2float_rd(py0); ty1 = __double2float_ru(py1);
 }
 
+// Streaming accesses (queues, shade records, levels): each word is written once
+// and read once by a later launch, so they bypass L2 allocation (nontemporal)
+// and leave it to the BVH / sphere lines the traversals re-read.
+#ifndef RT_NT
+#define RT_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T ldn(const T* p) {
+#if RT_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <class T, class U>
+__device__ __forceinline__ void stn(T* p, U v) {
+#if RT_NT
+    __builtin_nontemporal_store(static_cast<T>(v), p);
+#else
+    *p = static_cast<T>(v);
+#endif
+}
+
+// RT_NT >= 2: also the shadow-list entries and the shade records' last read;
+// RT_NT >= 3: also the shadow kernels' record reads.
+template <int kLevel, class T>
+__device__ __forceinline__ T ldn_if(const T* p) {
+#if RT_NT
+    if constexpr (RT_NT >= kLevel) return __builtin_nontemporal_load(p);
+#endif
+    return *p;
+}
+template <int kLevel, class T, class U>
+__device__ __forceinline__ void stn_if(T* p, U v) {
+#if RT_NT
+    if constexpr (RT_NT >= kLevel) { __builtin_nontemporal_store(static_cast<T>(v), p); return; }
+#endif
+    *p = static_cast<T>(v);
+}
+
 __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
-    return Ray{b.qf(q, 0)[i], b.qf(q, 1)[i], b.qf(q, 2)[i], b.qf(q, 3)[i], b.qf(q, 4)[i], b.qf(q, 5)[i]};
+    return Ray{ldn(&b.qf(q, 0)[i]), ldn(&b.qf(q, 1)[i]), ldn(&b.qf(q, 2)[i]), ldn(&b.qf(q, 3)[i]), ldn(&b.qf(q, 4)[i]), ldn(&b.qf(q, 5)[i])};
 }
 
 // Sphere sources of the wavefront intersection kernels.
@@ -433,7 +473,7 @@ __device__ __forceinline__ void write_background_pixel(const FrameParams& fp, co
 }
 
 __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
-    b.term(0)[p] = c.r; b.term(1)[p] = c.g; b.term(2)[p] = c.b;
+    stn(&b.term(0)[p], c.r); stn(&b.term(1)[p], c.g); stn(&b.term(2)[p], c.b);
     b.nlev()[p] = static_cast<uint8_t>(k);
 }
 
@@ -515,31 +555,31 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
                 want = d == 2;
             }
             const uint32_t qs = lds_append(&counts[2 + l], want);
-            if (want) b.oq()[(rk + l) * b.qcap + obase + qs] = static_cast<uint32_t>(obase) + slot;
+            if (want) stn_if<2>(&b.oq()[(rk + l) * b.qcap + obase + qs], static_cast<uint32_t>(obase) + slot);
         }
         occ |= decided << kOccCount;
         const bool none = shade && decided == L;           // nothing to trace: shade directly from the list
         const uint32_t qs = lds_append(&counts[2 + L], none);
-        if (none) b.oq()[(rk + L) * b.qcap + obase + qs] = static_cast<uint32_t>(obase) + slot;
+        if (none) stn_if<2>(&b.oq()[(rk + L) * b.qcap + obase + qs], static_cast<uint32_t>(obase) + slot);
     }
     if (shade) {
         const size_t at = rbase + slot;
-        b.rf(0)[at] = ptx; b.rf(1)[at] = pty; b.rf(2)[at] = ptz;
-        b.rf(3)[at] = r.dx; b.rf(4)[at] = r.dy; b.rf(5)[at] = r.dz;
-        b.rf(6)[at] = sig;
-        b.ru(0)[at] = static_cast<uint32_t>(h.obj);
-        b.ru(1)[at] = static_cast<uint32_t>(h.prim);
-        b.ru(2)[at] = p;
-        b.ru(3)[at] = occ;
+        stn(&b.rf(0)[at], ptx); stn(&b.rf(1)[at], pty); stn(&b.rf(2)[at], ptz);
+        stn(&b.rf(3)[at], r.dx); stn(&b.rf(4)[at], r.dy); stn(&b.rf(5)[at], r.dz);
+        stn(&b.rf(6)[at], sig);
+        stn(&b.ru(0)[at], static_cast<uint32_t>(h.obj));
+        stn(&b.ru(1)[at], static_cast<uint32_t>(h.prim));
+        stn(&b.ru(2)[at], p);
+        stn(&b.ru(3)[at], occ);
     }
     const uint32_t rslot = lds_append(&counts[1], refl);
     if (refl) {
         const int qn = (k + 1) & 1;
         const size_t at = obase + rslot;
-        b.qf(qn, 0)[at] = rr.ox; b.qf(qn, 1)[at] = rr.oy; b.qf(qn, 2)[at] = rr.oz;
-        b.qf(qn, 3)[at] = rr.dx; b.qf(qn, 4)[at] = rr.dy; b.qf(qn, 5)[at] = rr.dz;
-        b.qf(qn, 6)[at] = nsig;
-        b.qpix(qn)[at] = p;
+        stn(&b.qf(qn, 0)[at], rr.ox); stn(&b.qf(qn, 1)[at], rr.oy); stn(&b.qf(qn, 2)[at], rr.oz);
+        stn(&b.qf(qn, 3)[at], rr.dx); stn(&b.qf(qn, 4)[at], rr.dy); stn(&b.qf(qn, 5)[at], rr.dz);
+        stn(&b.qf(qn, 6)[at], nsig);
+        stn(&b.qpix(qn)[at], p);
     }
 }
 
@@ -591,8 +631,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             } else {
                 const size_t at = region_entry(ql.scan, b.G, b.R, j);
                 r = load_ray(b, k & 1, at);
-                sig = b.qf(k & 1, 6)[at];
-                p = b.qpix(k & 1)[at];
+                sig = ldn(&b.qf(k & 1, 6)[at]);
+                p = ldn(&b.qpix(k & 1)[at]);
                 live = true;
             }
         }
@@ -621,15 +661,15 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
 // ends the chain with it.
 template <bool kFresnel>
 __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
-    const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
-    const double dx = b.rf(3)[at], dy = b.rf(4)[at], dz = b.rf(5)[at];
-    const double sig = b.rf(6)[at];
-    const int32_t obj = static_cast<int32_t>(b.ru(0)[at]);
-    const uint32_t p = b.ru(2)[at];
+    const double ptx = ldn_if<2>(&b.rf(0)[at]), pty = ldn_if<2>(&b.rf(1)[at]), ptz = ldn_if<2>(&b.rf(2)[at]);
+    const double dx = ldn_if<2>(&b.rf(3)[at]), dy = ldn_if<2>(&b.rf(4)[at]), dz = ldn_if<2>(&b.rf(5)[at]);
+    const double sig = ldn_if<2>(&b.rf(6)[at]);
+    const int32_t obj = static_cast<int32_t>(ldn_if<2>(&b.ru(0)[at]));
+    const uint32_t p = ldn_if<2>(&b.ru(2)[at]);
     const DevMaterial& m = sc.mats[obj];
     Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
     double nx, ny, nz;
-    hit_normal(sc, sc.spheres, static_cast<int32_t>(b.ru(1)[at]), ptx, pty, ptz, nx, ny, nz);
+    hit_normal(sc, sc.spheres, static_cast<int32_t>(ldn_if<2>(&b.ru(1)[at])), ptx, pty, ptz, nx, ny, nz);
     const double nd = nx * dx + ny * dy + nz * dz;
     const Shading sh = shading_flags<kFresnel>(m, sig, nd);
     const bool diffuse = sh.diffuse, specular = sh.specular;
@@ -643,9 +683,9 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
     }
     if (specular) {
         const size_t st = static_cast<size_t>(k) * b.capa + p;
-        b.lf(0)[st] = res.r; b.lf(1)[st] = res.g; b.lf(2)[st] = res.b;
-        b.lobj()[st] = obj;
-        if (kFresnel && m.kind == kMatFresnel) b.lf(3)[st] = sh.f;
+        stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
+        stn(&b.lobj()[st], obj);
+        if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
     } else {
         set_terminal(b, p, res, k);
     }
@@ -691,7 +731,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
         if (qi >= n) continue;
         const uint32_t l = qi / nrec, j = qi - l * nrec;
         const size_t at = rk + region_entry(ql.scan, b.G, b.R, j);
-        const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
+        const double ptx = ldn_if<3>(&b.rf(0)[at]), pty = ldn_if<3>(&b.rf(1)[at]), ptz = ldn_if<3>(&b.rf(2)[at]);
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
@@ -739,12 +779,12 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_shadow(DevSce
         const uint32_t j = qi - s_start[l];
         const uint32_t* sl = scans + l * (b.G + 1);
         if (j >= sl[b.G]) continue;                               // padding of the list's last chunk
-        const size_t at = rk + b.oq()[(static_cast<size_t>(k) * NL + l) * b.qcap + region_entry(sl, b.G, b.R, j)];
+        const size_t at = rk + ldn_if<2>(&b.oq()[(static_cast<size_t>(k) * NL + l) * b.qcap + region_entry(sl, b.G, b.R, j)]);
         if (l == L) {                                             // nothing to trace
             shade_record<kFresnel>(sc, b, k, at, b.ru(3)[at] & ((1u << kOccCount) - 1u));
             continue;
         }
-        const double ptx = b.rf(0)[at], pty = b.rf(1)[at], ptz = b.rf(2)[at];
+        const double ptx = ldn_if<3>(&b.rf(0)[at]), pty = ldn_if<3>(&b.rf(1)[at]), ptz = ldn_if<3>(&b.rf(2)[at]);
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
@@ -778,7 +818,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
     if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
-    Col acc{b.term(0)[p], b.term(1)[p], b.term(2)[p]};
+    Col acc{ldn(&b.term(0)[p]), ldn(&b.term(1)[p]), ldn(&b.term(2)[p])};
     for (int k = static_cast<int>(nlev) - 1; k >= 0; k -= 4) {
         double sr[4], sg[4], sb[4];
         int32_t ob[4];
@@ -786,8 +826,8 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
         for (int u = 0; u < 4; ++u) {
             if (k - u >= 0) {
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
-                ob[u] = b.lobj()[at];
-                sr[u] = b.lf(0)[at]; sg[u] = b.lf(1)[at]; sb[u] = b.lf(2)[at];
+                ob[u] = ldn(&b.lobj()[at]);
+                sr[u] = ldn(&b.lf(0)[at]); sg[u] = ldn(&b.lf(1)[at]); sb[u] = ldn(&b.lf(2)[at]);
             }
         }
         double kr[4], kg[4], kb[4], kf[4];
@@ -796,7 +836,7 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
             if (k - u >= 0) {
                 const DevMaterial& m = sc.mats[ob[u]];
                 kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
-                kf[u] = kFresnel && m.kind == kMatFresnel ? b.lf(3)[static_cast<size_t>(k - u) * b.capa + p] : 1.0;
+                kf[u] = kFresnel && m.kind == kMatFresnel ? ldn(&b.lf(3)[static_cast<size_t>(k - u) * b.capa + p]) : 1.0;
             }
         }
 #pragma unroll

@@ -42,3 +42,21 @@ int bvh_depth(const BvhResult& b2);
 std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]);
 
 }  // namespace rtamd
+
+namespace rtamd {
+
+// Light-view grids for point-light shadow queries (host_lightgrid.cpp,
+// DESIGN.md "Light-view grids").  Per point light: a cube map of R x R cells
+// per face around the light; cell c lists every sphere whose padded box has a
+// point whose direction from the light falls in c (a conservative superset),
+// sorted by the box's distance from the light.  `r_leaf` are the radii and
+// `spheres` the centres in leaf order (the indices the lists hold).
+struct LightGridResult {
+    std::vector<DevLightGrid> grids;    // one per light (R = 0: no grid, e.g. not a point light)
+    std::vector<uint32_t> off;          // cell offsets into ent (per face rect: w * h + 1)
+    std::vector<DevLgEntry> ent;
+};
+LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
+                                  const std::vector<DevLight>& lights, double pad, int r_override);
+
+}  // namespace rtamd

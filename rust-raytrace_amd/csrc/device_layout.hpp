@@ -95,6 +95,27 @@ struct DevTexFace {
     uint64_t off;
 };
 
+// Light-view grid of one point light (host_lightgrid.cpp): a cube map of R x R
+// cells per face centred on the light.  A direction d (from the light) maps to
+// face 2a + (d_a < 0) with a = argmax |d_i|, and to face coordinates
+// u = d_b / |d_a|, v = d_c / |d_a| (b = a+1, c = a+2 mod 3), cell
+// (floor((u+1)/2 R), floor((v+1)/2 R)).  Only the face's rectangle of non-empty
+// cells is stored: its cell offsets start at lg_off[off_base[f]].
+struct DevLightGrid {
+    double lx, ly, lz;              // the light's location
+    int32_t R;                      // cells per face side; 0 = no grid for this light
+    uint32_t always_begin, always_end;   // lg_ent entries tested for every query (spheres at the light)
+    int32_t fx0[6], fy0[6], fw[6], fh[6];
+    uint32_t off_base[6];
+};
+
+// One list entry: a sphere (leaf-order index) and a lower bound on the distance
+// from the light to its padded box (f32, rounded down).
+struct DevLgEntry {
+    int32_t sph;
+    float near;
+};
+
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -122,6 +143,9 @@ struct DevScene {
     double cam_pos[3];
     double cam_m[9];                // row-major
     double bg[3];
+    const DevLightGrid* lgrid;       // per light (null: no grids)
+    const uint32_t* lg_off;
+    const DevLgEntry* lg_ent;
 };
 
 struct FrameParams {

@@ -353,13 +353,19 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (bvh_depth(bvh) > 64) return fail(c, RT_E_UNSUPPORTED, "sphere BVH deeper than the traversal stack");
     c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
     const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
+    std::vector<double> r_leaf(spheres.size());
     {
         std::vector<DevSphere> s2(spheres.size());
         std::vector<int32_t> o2(spheres.size());
-        for (size_t k = 0; k < spheres.size(); ++k) { s2[k] = spheres[bvh.order[k]]; o2[k] = sphere_obj[bvh.order[k]]; }
+        for (size_t k = 0; k < spheres.size(); ++k) {
+            s2[k] = spheres[bvh.order[k]]; o2[k] = sphere_obj[bvh.order[k]]; r_leaf[k] = srad[bvh.order[k]];
+        }
         spheres.swap(s2);
         sphere_obj.swap(o2);
     }
+    // light-view grids of the point lights (RT_WF_LGRID=0 disables; RT_LGRID_R forces the resolution)
+    LightGridResult lg;
+    if (env_int("RT_WF_LGRID", 1) != 0) lg = build_light_grids(spheres, r_leaf, lights, pad, env_int("RT_LGRID_R", 0));
     // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights][bvh], 256-B aligned pieces.
     size_t off = 0;
     auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
@@ -373,6 +379,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
     const size_t o_cam = place(camn.size() * sizeof(DevCamNode));
     const size_t o_srgbv = place(256 * sizeof(double));
+    const size_t o_lg = place(lg.grids.size() * sizeof(DevLightGrid));
+    const size_t o_lgoff = place(lg.off.size() * sizeof(uint32_t));
+    const size_t o_lgent = place(lg.ent.size() * sizeof(DevLgEntry));
     size_t tex_bytes = 0;
     uint64_t face_off[6] = {0, 0, 0, 0, 0, 0};
     if (skybox)
@@ -391,6 +400,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
     put(o_cam, camn.data(), camn.size() * sizeof(DevCamNode));
     put(o_srgbv, srgb_values_table(), 256 * sizeof(double));
+    put(o_lg, lg.grids.data(), lg.grids.size() * sizeof(DevLightGrid));
+    put(o_lgoff, lg.off.data(), lg.off.size() * sizeof(uint32_t));
+    put(o_lgent, lg.ent.data(), lg.ent.size() * sizeof(DevLgEntry));
     if (skybox)
         for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -441,6 +453,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     for (int k = 0; k < 3; ++k) d.cam_pos[k] = s->camera.position[k];
     for (int k = 0; k < 9; ++k) d.cam_m[k] = s->camera.matrix[k];
     d.bg[0] = s->background.r; d.bg[1] = s->background.g; d.bg[2] = s->background.b;
+    d.lgrid = lg.grids.empty() ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_lg);
+    d.lg_off = reinterpret_cast<const uint32_t*>(base + o_lgoff);
+    d.lg_ent = reinterpret_cast<const DevLgEntry*>(base + o_lgent);
     c->has_scene = true;
     return RT_OK;
 }

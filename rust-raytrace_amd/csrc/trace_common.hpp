@@ -709,6 +709,68 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
     }
 }
 
+// ---- point-light shadows through the light-view grid ---------------------
+// The shadow query of occluded_bvh4 for a point light (has_range), with the
+// spheres taken from the light's grid (host_lightgrid.cpp) instead of a tree:
+// the always list, then the list of the cell that p's direction from the light
+// falls in, in increasing box distance from the light, stopping at the first
+// box farther than p (no blocker can be farther from the light than p is).
+// Every sphere that could report a blocking hit is on those lists, and each is
+// tested with the exact quadratic, so the any-hit answer is the linear scan's.
+// A degenerate direction (p at the light, non-finite) tests every sphere.
+template <bool kCount = false>
+__device__ __forceinline__ bool occluded_lgrid(const DevScene& sc, const BvhView& v, const DevLightGrid& g,
+                                               const Ray& r, double r2, double ptx, double pty, double ptz,
+                                               int32_t hint, Work* w = nullptr) {
+    bool plane_block = false;
+    for (int i = 0; i < sc.n_planes; ++i) {
+        double t;
+        if (!plane_t(sc.planes[i], r, t)) continue;
+        if (t != t) return false;                  // the NaN hit is the nearest: t*t < r2 fails (lit)
+        plane_block |= t * t < r2;
+    }
+    if (plane_block) return true;
+    if (sc.n_spheres == 0) return false;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    auto blocks = [&](int32_t k) {
+        if constexpr (kCount) ++w->spheres;
+        double t;
+        return sphere_t(v.sph[k], r, a2, a4, t) && t * t < r2;
+    };
+    if (hint >= 0 && blocks(hint)) return true;
+    for (uint32_t e = g.always_begin; e < g.always_end; ++e)
+        if (blocks(sc.lg_ent[e].sph)) return true;
+    const float dx = static_cast<float>(ptx - g.lx), dy = static_cast<float>(pty - g.ly),
+                dz = static_cast<float>(ptz - g.lz);
+    const float ax = fabsf(dx), ay = fabsf(dy), az = fabsf(dz);
+    const int fa = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    const float da = fa == 0 ? dx : fa == 1 ? dy : dz;
+    const float db = fa == 0 ? dy : fa == 1 ? dz : dx;
+    const float dc = fa == 0 ? dz : fa == 1 ? dx : dy;
+    if (!(fabsf(da) > 0.0f && fabsf(da) < 3.0e38f)) {
+        for (int32_t k = 0; k < sc.n_spheres; ++k)
+            if (blocks(k)) return true;
+        return false;
+    }
+    const int f = 2 * fa + (da < 0.0f ? 1 : 0);
+    const float inv = 1.0f / fabsf(da);
+    const float R = static_cast<float>(g.R);
+    const int ci = min(max(static_cast<int>(floorf((db * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int cj = min(max(static_cast<int>(floorf((dc * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int li = ci - g.fx0[f], lj = cj - g.fy0[f];
+    if (li < 0 || lj < 0 || li >= g.fw[f] || lj >= g.fh[f]) return false;    // no sphere in this direction
+    const uint32_t cell = g.off_base[f] + static_cast<uint32_t>(lj * g.fw[f] + li);
+    const uint32_t e0 = sc.lg_off[cell], e1 = sc.lg_off[cell + 1];
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz) * 1.00001f + 1e-5f;     // >= |p - L|
+    for (uint32_t e = e0; e < e1; ++e) {
+        const DevLgEntry en = sc.lg_ent[e];
+        if (en.near > dist) break;
+        if (blocks(en.sph)) return true;
+    }
+    return false;
+}
+
 // ---- generation 0: camera rays by 8x8 tile -----------------------------
 // Every camera ray starts at the camera, so the wave's 64 rays of one pixel
 // tile share a rectangle of image-plane coordinates [tx0, tx1] x [ty0, ty1]

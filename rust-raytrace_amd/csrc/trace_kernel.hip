@@ -291,8 +291,20 @@ __device__ __forceinline__ void stn_if(T* p, U v) {
     *p = static_cast<T>(v);
 }
 
+// the fold's loads (RT_NT_FOLD=1: nontemporal; measured 346 -> 413 us per fold at C3, so plain)
+#ifndef RT_NT_FOLD
+#define RT_NT_FOLD 0
+#endif
+constexpr int kNtFold = RT_NT_FOLD ? 1 : 99;
+// the queue loads of the nearest-hit kernel (RT_NT_QLOAD=0: plain loads)
+#ifndef RT_NT_QLOAD
+#define RT_NT_QLOAD 1
+#endif
+constexpr int kNtQ = RT_NT_QLOAD ? 1 : 99;
+
 __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
-    return Ray{ldn(&b.qf(q, 0)[i]), ldn(&b.qf(q, 1)[i]), ldn(&b.qf(q, 2)[i]), ldn(&b.qf(q, 3)[i]), ldn(&b.qf(q, 4)[i]), ldn(&b.qf(q, 5)[i])};
+    return Ray{ldn_if<kNtQ>(&b.qf(q, 0)[i]), ldn_if<kNtQ>(&b.qf(q, 1)[i]), ldn_if<kNtQ>(&b.qf(q, 2)[i]),
+               ldn_if<kNtQ>(&b.qf(q, 3)[i]), ldn_if<kNtQ>(&b.qf(q, 4)[i]), ldn_if<kNtQ>(&b.qf(q, 5)[i])};
 }
 
 // Sphere sources of the wavefront intersection kernels.
@@ -631,8 +643,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             } else {
                 const size_t at = region_entry(ql.scan, b.G, b.R, j);
                 r = load_ray(b, k & 1, at);
-                sig = ldn(&b.qf(k & 1, 6)[at]);
-                p = ldn(&b.qpix(k & 1)[at]);
+                sig = ldn_if<kNtQ>(&b.qf(k & 1, 6)[at]);
+                p = ldn_if<kNtQ>(&b.qpix(k & 1)[at]);
                 live = true;
             }
         }
@@ -737,7 +749,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
         const int32_t hint = static_cast<int32_t>(b.ru(1)[at]);
-        const bool occluded = occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
+        const bool occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
+                                  ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
+                                  : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
         occlusion_done<kShade, kFresnel>(sc, b, k, at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
@@ -788,7 +802,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_shadow(DevSce
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        const bool occluded = occluded_any<kSrc, kCount>(ss, v, sray, has_range, r2, -1, &w);
+        const bool occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
+                                  ? occluded_lgrid<kCount>(ss, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, -1, &w)
+                                  : occluded_any<kSrc, kCount>(ss, v, sray, has_range, r2, -1, &w);
         occlusion_done<true, kFresnel>(sc, b, k, at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
@@ -818,7 +834,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
     if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
-    Col acc{ldn(&b.term(0)[p]), ldn(&b.term(1)[p]), ldn(&b.term(2)[p])};
+    Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
     for (int k = static_cast<int>(nlev) - 1; k >= 0; k -= 4) {
         double sr[4], sg[4], sb[4];
         int32_t ob[4];
@@ -826,8 +842,8 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
         for (int u = 0; u < 4; ++u) {
             if (k - u >= 0) {
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
-                ob[u] = ldn(&b.lobj()[at]);
-                sr[u] = ldn(&b.lf(0)[at]); sg[u] = ldn(&b.lf(1)[at]); sb[u] = ldn(&b.lf(2)[at]);
+                ob[u] = ldn_if<kNtFold>(&b.lobj()[at]);
+                sr[u] = ldn_if<kNtFold>(&b.lf(0)[at]); sg[u] = ldn_if<kNtFold>(&b.lf(1)[at]); sb[u] = ldn_if<kNtFold>(&b.lf(2)[at]);
             }
         }
         double kr[4], kg[4], kb[4], kf[4];
@@ -836,7 +852,7 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
             if (k - u >= 0) {
                 const DevMaterial& m = sc.mats[ob[u]];
                 kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
-                kf[u] = kFresnel && m.kind == kMatFresnel ? ldn(&b.lf(3)[static_cast<size_t>(k - u) * b.capa + p]) : 1.0;
+                kf[u] = kFresnel && m.kind == kMatFresnel ? ldn_if<kNtFold>(&b.lf(3)[static_cast<size_t>(k - u) * b.capa + p]) : 1.0;
             }
         }
 #pragma unroll

@@ -297,6 +297,45 @@ def test_extreme_sphere_sizes_and_far_plane_origins(gpu_ctx, algo):
     check_parity(gpu_ctx, s, algo)
 
 
+@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
+def test_light_view_grids_adversarial_lights(gpu_ctx, algo):
+    """Point-light shadows through the light-view grids (host_lightgrid.cpp):
+    lights inside the sphere cloud (boxes straddling the light's axis planes,
+    every cube face populated), a light inside a sphere and one on a sphere's
+    surface (the always list), shade points close to a light, spheres from
+    1e-3 to 1e3, a plane through a light.  Every shadow answer must be the
+    linear scan's (the oracle)."""
+    s = scenes.SceneSpec(width=81, height=67, max_depth=6, background=(0.05, 0.05, 0.1),
+                         camera={"ctor": "new", "position": (0, 2, 12), "look": (0, -0.1, -1), "up": (0, 1, 0),
+                                 "im_dist": 1.2})
+    rng = scenes.SplitMix64(4242)
+    for k in range(400):
+        c = (rng.uniform(-6, 6), rng.uniform(-2, 6), rng.uniform(-10, 2))
+        kd = (rng.uniform(0.1, 0.9), rng.uniform(0.1, 0.9), rng.uniform(0.1, 0.9))
+        s.sphere(c, 10 ** rng.uniform(-3, -0.2), scenes.phong(kd, (0.3, 0.3, 0.3), 20.0, (0.01, 0.01, 0.01)))
+    s.sphere((3.0, 1.0, -4.0), 0.8, scenes.phong((0.8, 0.8, 0.2), (0.4, 0.4, 0.4), 10.0, (0, 0, 0)))
+    s.sphere((0.0, -1e3 - 2.5, -4.0), 1e3, scenes.phong((0.5, 0.5, 0.5), (0.2, 0.2, 0.2), 5.0, (0, 0, 0)))
+    s.plane((0.0, 0.0, -30.0), (0.0, 0.0, 1.0), scenes.phong((0.3, 0.3, 0.3), (0.0, 0.0, 0.0), 1.0, (0, 0, 0)))
+    s.point_light((0.0, 2.0, -4.0), (0.6, 0.6, 0.6))          # inside the cloud
+    s.point_light((3.0, 1.0, -4.0), (0.5, 0.2, 0.2))          # at the centre of a sphere
+    s.point_light((3.0, 1.8, -4.0), (0.2, 0.5, 0.2))          # on that sphere's surface
+    s.point_light((-5.0, 0.5, -30.0), (0.2, 0.2, 0.5))        # on the plane
+    s.directional_light((0.2, -1.0, -0.1), (0.2, 0.2, 0.2))   # no grid: the tree
+    check_parity(gpu_ctx, s, algo)
+
+
+def test_light_view_grids_off_is_bit_identical(gpu_ctx, monkeypatch):
+    """RT_WF_LGRID=0 (shadow queries through the 4-wide tree) and the default
+    grids give the same bytes, colours and ray counts on the 10k-sphere scene."""
+    spec = scenes.config4(160, 120)
+    a = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    monkeypatch.setenv("RT_WF_LGRID", "0")
+    b = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert np.array_equal(a[1], b[1])
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    assert a[2].rays == b[2].rays and a[2].shadow_rays == b[2].shadow_rays
+
+
 def test_bvh_ten_thousand_spheres(gpu_ctx):
     s = scenes.config4(96, 96)
     check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)

@@ -613,10 +613,12 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // RT_WF_SPLIT=0: every kernel on one in-order stream (A/B measurement);
         // RT_WF_DEAL: 1 workgroup-major chunk dealing (default), 0 workgroup-first
         // RT_WF_BSTREAMS: streams for the shadow + shading kernels (default 1;
-        // generations alternate over them); RT_WF_FUSE=0: separate shading kernel
+        // generations alternate over them); RT_WF_FUSE=1: shading fused into the shadow kernel
         const bool split = env_int("RT_WF_SPLIT", 1) != 0;
         const int n_b = std::max(1, std::min(kMaxBStreams, env_int("RT_WF_BSTREAMS", 1)));
-        const bool fuse = env_int("RT_WF_FUSE", 1) != 0;
+        // (fused shading measured slower once shadow queries went through the light-view
+        // grids: the shading's pow and the per-light atomics then dominate the fused kernel)
+        const bool fuse = env_int("RT_WF_FUSE", 0) != 0;
         // shadow item lists (RT_WF_LISTS=0: every (record, light) pair goes to the shadow kernel)
         const uint32_t nlists = (split && fuse && env_int("RT_WF_LISTS", 1) != 0 && c->dsc.n_lights > 0 &&
                                  c->dsc.n_lights <= 24) ? static_cast<uint32_t>(c->dsc.n_lights) + 1u : 0u;

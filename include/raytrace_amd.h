@@ -125,6 +125,18 @@ int rt_scene_get_desc(const rt_scene* scene, rt_scene_desc* out);
 void rt_scene_free(rt_scene* scene);
 /* Make the scene's background a SkyboxBackground with faces px, nx, py, ny, pz, nz (copied). */
 int rt_scene_set_skybox(rt_scene* scene, const rt_texture faces[6]);
+/* Diagnostic, host only (no device): the spheres the light-view grid of point
+ * light `light` (built as rt_scene_upload builds it) hands a
+ * shadow query from each point of `points` (n_points x 3 doubles): the same
+ * candidate list, in the same order, as the device tests after the planes and
+ * the hint.  counts[i] = its length, or -1 when the device tests every sphere
+ * (degenerate direction, or no grid for this light); ids = the candidates'
+ * object ids (file order, scene.rs:248), concatenated, at most cap in all.
+ * info[0..2] = cells per face side, stored cells, list entries.
+ * Replaces nothing in the reference (its shadow query scans every object,
+ * scene.rs:247-249); tests check the lists against that scan. */
+int rt_light_grid_candidates(const rt_scene* scene, int light, const double* points, uint32_t n_points,
+                             int32_t* counts, int32_t* ids, size_t cap, int64_t* info);
 /* Decode an image file as Texture::load does (RGB8, rows top-down).  rgb == NULL: only the size.
  * Formats: uncompressed BMP (24/32 bit) and binary PPM; others -> RT_E_UNSUPPORTED. */
 int rt_texture_load(const char* path, uint32_t* width, uint32_t* height, uint8_t* rgb, size_t cap);

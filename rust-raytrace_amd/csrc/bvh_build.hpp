@@ -58,5 +58,7 @@ struct LightGridResult {
 };
 LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
                                   const std::vector<DevLight>& lights, double pad, int r_override);
+// Host mirror of the device's candidate list (test / diagnostic).
+bool light_grid_candidates(const LightGridResult& lg, int light, const double p[3], std::vector<int32_t>& out);
 
 }  // namespace rtamd

@@ -161,4 +161,38 @@ LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const s
     return out;
 }
 
+// The device's candidate list for a shadow query from p toward light `li`
+// (occluded_lgrid, trace_common.hpp), with the same f32 arithmetic: the always
+// list, then p's cell up to the early stop.  Returns false when the device
+// would test every sphere (degenerate direction) or the light has no grid.
+bool light_grid_candidates(const LightGridResult& lg, int li, const double p[3], std::vector<int32_t>& out) {
+    out.clear();
+    if (li < 0 || li >= static_cast<int>(lg.grids.size())) return false;
+    const DevLightGrid& g = lg.grids[li];
+    if (g.R <= 0) return false;
+    for (uint32_t e = g.always_begin; e < g.always_end; ++e) out.push_back(lg.ent[e].sph);
+    const float dx = static_cast<float>(p[0] - g.lx), dy = static_cast<float>(p[1] - g.ly),
+                dz = static_cast<float>(p[2] - g.lz);
+    const float ax = std::fabs(dx), ay = std::fabs(dy), az = std::fabs(dz);
+    const int fa = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    const float da = fa == 0 ? dx : fa == 1 ? dy : dz;
+    const float db = fa == 0 ? dy : fa == 1 ? dz : dx;
+    const float dc = fa == 0 ? dz : fa == 1 ? dx : dy;
+    if (!(std::fabs(da) > 0.0f && std::fabs(da) < 3.0e38f)) return false;
+    const int f = 2 * fa + (da < 0.0f ? 1 : 0);
+    const float inv = 1.0f / std::fabs(da);
+    const float R = static_cast<float>(g.R);
+    const int ci = std::min(std::max(static_cast<int>(std::floor((db * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int cj = std::min(std::max(static_cast<int>(std::floor((dc * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int li2 = ci - g.fx0[f], lj = cj - g.fy0[f];
+    if (li2 < 0 || lj < 0 || li2 >= g.fw[f] || lj >= g.fh[f]) return true;
+    const uint32_t cell = g.off_base[f] + static_cast<uint32_t>(lj * g.fw[f] + li2);
+    const float dist = std::sqrt(dx * dx + dy * dy + dz * dz) * 1.00001f + 1e-5f;
+    for (uint32_t e = lg.off[cell]; e < lg.off[cell + 1]; ++e) {
+        if (lg.ent[e].near > dist) break;
+        out.push_back(lg.ent[e].sph);
+    }
+    return true;
+}
+
 }  // namespace rtamd

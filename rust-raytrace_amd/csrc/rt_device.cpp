@@ -271,6 +271,57 @@ void rt_ctx_destroy(rt_ctx* c) {
 
 const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : thread_error(); }
 
+int rt_light_grid_candidates(const rt_scene* s, int light, const double* points, uint32_t n_points, int32_t* counts,
+                             int32_t* ids, size_t cap, int64_t* info) {
+    if (!s || (n_points && (!points || !counts)) || (cap && !ids)) return RT_E_INVALID;
+    if (light < 0 || light >= static_cast<int>(s->lights.size())) return RT_E_INVALID;
+    try {
+        std::vector<DevSphere> spheres;
+        std::vector<double> srad;
+        std::vector<int32_t> obj;
+        double extent = 0.0;
+        for (size_t i = 0; i < s->objects.size(); ++i) {
+            const rt_object& o = s->objects[i];
+            if (o.shape != RT_SHAPE_SPHERE) continue;
+            spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
+            srad.push_back(o.geom[3]);
+            obj.push_back(static_cast<int32_t>(i));
+            const double r = std::fabs(o.geom[3]);
+            for (int k = 0; k < 3; ++k)
+                for (double v : {o.geom[k] - r, o.geom[k] + r})
+                    if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
+        }
+        std::vector<DevLight> lights;
+        for (const rt_light& l : s->lights) {
+            DevLight d{};
+            for (int k = 0; k < 9; ++k) d.v[k] = l.v[k];
+            d.kind = l.kind;
+            lights.push_back(d);
+        }
+        const LightGridResult lg = build_light_grids(spheres, srad, lights, 1e-5 * (1.0 + extent), env_int("RT_LGRID_R", 0));
+        if (info) {
+            info[0] = lg.grids[light].R;
+            int64_t cells = 0;
+            for (int f = 0; f < 6; ++f) cells += static_cast<int64_t>(lg.grids[light].fw[f]) * lg.grids[light].fh[f];
+            info[1] = cells;
+            info[2] = static_cast<int64_t>(lg.ent.size());
+        }
+        std::vector<int32_t> cand;
+        size_t used = 0;
+        for (uint32_t i = 0; i < n_points; ++i) {
+            if (!light_grid_candidates(lg, light, points + 3 * i, cand)) { counts[i] = -1; continue; }
+            counts[i] = static_cast<int32_t>(cand.size());
+            for (int32_t k : cand) {
+                if (used == cap) return fail(nullptr, RT_E_INVALID, "candidate buffer too small");
+                ids[used++] = obj[k];
+            }
+        }
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return fail(nullptr, RT_E_NOMEM, e.what());
+    }
+}
+
 int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));

@@ -116,6 +116,8 @@ def _load():
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
         "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
         "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
+        "rt_light_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, P(C.c_double), C.c_uint32, P(C.c_int32),
+                                               P(C.c_int32), C.c_size_t, P(C.c_int64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -205,6 +207,28 @@ class Scene:
         h = C.c_void_p()
         _check(lib.rt_scene_from_desc(C.byref(desc), C.byref(h)))
         return cls(h.value)
+
+    def light_grid_candidates(self, light, points, cap=1 << 22):
+        """Diagnostic (host only): for each point p, the object ids the light-view
+        grid of point light `light` hands a shadow query from p (None when the
+        device tests every sphere), and (R, stored cells, list entries)."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        n = pts.shape[0]
+        counts = np.zeros(n, np.int32)
+        ids = np.zeros(cap, np.int32)
+        info = np.zeros(3, np.int64)
+        _check(lib.rt_light_grid_candidates(self._h, light, pts.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                            counts.ctypes.data_as(C.POINTER(C.c_int32)),
+                                            ids.ctypes.data_as(C.POINTER(C.c_int32)), cap,
+                                            info.ctypes.data_as(C.POINTER(C.c_int64))))
+        out, at = [], 0
+        for c in counts:
+            if c < 0:
+                out.append(None)
+            else:
+                out.append(ids[at:at + c].copy())
+                at += c
+        return out, tuple(int(x) for x in info)
 
     def set_skybox(self, faces):
         """SkyboxBackground { px, nx, py, ny, pz, nz } from six uint8 [h, w, 3] arrays (copied)."""

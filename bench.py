@@ -4,30 +4,39 @@ One step = one full pass of the hot path over one frame of the headline
 workload (config C3): every pixel's camera ray, its Phong
 shading with shadow rays to 2 point lights, and mirror bounces to depth 8,
 f64 arithmetic, f32 RGB + sRGB BGR written to HBM.  The scene is uploaded once
-(inputs resident in HBM before timing); output stays in HBM (the PCIe copy is
-reported separately in DESIGN.md, never in `value`).
+(inputs resident in HBM before timing); output stays in HBM (the PCIe copy and
+the host gather are reported beside `value`, never in it).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
-Multi-GPU: the frame's rows are dealt in 16-row bands round-robin over ranks
-(libraytrace/shard.py); no collective touches the data path (RCCL carries the
-barrier and the max-over-ranks timing only).  Default "scaling": "weak": at N
-GPUs the same scene and view are rendered at sqrt(N) x the resolution (frame
-side 4096*sqrt(N), rounded to whole bands), so every GPU renders the N=1
-frame's 16.7 M pixels; --scaling strong splits the 4096^2 frame instead.
-value = rays of the whole frame x K / max-over-ranks wall time of the K timed
-steps.  --config c4 / c5 select the larger configs of BASELINE.json; --config
-c1 the reference's own scene (test_scene.txt: IndirectPhong Cornell box, 1024
-random AA samples, 256x256, depth 1) on the path kernel.
+Multi-GPU: run as plain `python bench.py --gpus N` the script starts N rank
+processes itself (before anything touches a GPU), one device each; under
+torchrun it uses the launcher's ranks.  The frame's rows are dealt in 16-row
+bands round-robin over the ranks (libraytrace/shard.py); no collective touches
+the data path (RCCL carries the barrier and the max-over-ranks timing only).
+Default "scaling": "strong": the same 4096^2 frame (BASELINE config 4's "image
+tiled across GPUs"), so value = rays of the whole frame x K / max-over-ranks
+time; --scaling weak renders the same view at sqrt(N) x the resolution (every
+rank the N=1 pixel count).  After the timed region every rank copies its bands
+into ONE shared page-locked host frame (the host gather of SURVEY §8(e)),
+timed and reported as `host_gather`.  --config c4 / c5 select the larger
+configs of BASELINE.json; --config c1 the reference's own scene
+(test_scene.txt: IndirectPhong Cornell box, 1024 random AA samples, 256x256,
+depth 1) on the path kernel.
 
 Rays = every Scene::intersect query the reference would issue (camera +
 reflection + shadow), counted by the kernel; identical to the oracle's count
-(tests/test_gpu_parity.py).
+(tests/test_gpu_parity.py).  The value uses the rays the device actually
+traced (rt_stats.traced_rays), which differ only for centre jitter with spp > 1.
 """
 import argparse
 import json
+import mmap
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -52,25 +61,136 @@ def parse():
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--spheres", type=int, default=0)
     p.add_argument("--depth", type=int, default=-1)
-    p.add_argument("--algo", default="auto", choices=["auto", "wavefront", "lds", "global"])
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU time of the cpu_baseline sample")
+    p.add_argument("--algo", default="auto", choices=["auto", "wavefront", "lds", "global", "path"])
+    p.add_argument("--cpu-seconds", type=float, default=20.0,
+                   help="target CPU time of the cpu_baseline samples (split between 1 thread and all threads)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                   help="N > 1: weak = the frame side grows by sqrt(N) (same scene and view, every GPU "
-                        "renders the N=1 pixel count); strong = the N=1 frame split N ways")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="N > 1: strong = the N=1 frame dealt over N ranks (default); weak = the frame side "
+                        "grows by sqrt(N) (same scene and view, every rank renders the N=1 pixel count)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="(diagnostic, one process) render only rank 0's row bands of an N-rank frame; "
                         "its time is what each rank of an N-GPU run spends")
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
+    p.add_argument("--no-gather", action="store_true", help="skip the host-gather measurement")
     p.add_argument("--inflight", type=int, default=1,
                    help="frames in flight: F contexts (each its own working set and streams) render successive "
                         "steps into F output buffers, so frame i+1's first generations overlap frame i's tail")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: process-group backend for the barrier and the max-over-ranks timing (nccl = RCCL; "
                         "gloo rehearses N ranks on fewer GPUs, ranks sharing a device round-robin)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: start the ranks, form the process group, report the "
+                        "world and the devices seen, render nothing")
     return p.parse_args()
 
+
+# ---------------------------------------------------------------- launcher
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N`: start N rank processes of this script (one per
+    device) and wait for them.  The parent never touches a GPU."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:                 # one rank failed: stop the others (their exact PIDs)
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+# ---------------------------------------------------------------- CPU baseline
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share():
+    """Host threads this process may use: the affinity mask, capped by a cgroup
+    CPU quota when one is set (a GPU box shares its host between jobs)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_sample(spec, threads, budget_s, draws):
+    """The oracle (algorithmically the reference: same recursion, same linear
+    scan, f64) on a deterministic sample of the same frame: every stride-th row,
+    a centred window of columns, grown until it takes about budget_s."""
+    from oracle import ref64
+    W, H = spec.width, spec.height
+    stride, tw = max(1, H // 4), min(W, 64)
+    for _ in range(8):
+        rows = H // stride
+        x0 = (W - tw) // 2
+        t0 = time.time()
+        r = ref64.render(spec, x0=x0, tile_w=tw, tile_h=rows, band=1, band_stride=stride, band_phase=0,
+                         threads=threads, want_rgb64=False, **draws)
+        dt = time.time() - t0
+        if dt >= 0.5 * budget_s or (stride == 1 and tw == W):
+            break
+        f = budget_s / max(dt, 1e-3)
+        if tw < W:
+            ntw = min(W, int(tw * f))
+            f = f * tw / ntw
+            tw = ntw
+        if f > 1.2 and stride > 1:
+            stride = max(1, int(stride / f))
+    rays = r["counts"]["rays"]
+    return {"value": rays / dt / 1e6, "threads": threads, "seconds": round(dt, 2), "rays": rays,
+            "sample": f"{rows} rows (every {stride}th) x {tw} px (columns {x0}..{x0 + tw - 1}) of the same frame"}
+
+
+def cpu_baseline(spec, args, **draws):
+    share = cpu_share()
+    one = cpu_sample(spec, 1, args.cpu_seconds / 2, draws)
+    allc = cpu_sample(spec, share, args.cpu_seconds / 2, draws) if share > 1 else one
+    return {"value": allc["value"], "unit": "Mrays/s", "cores": allc["threads"], "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"{allc['sample']}; {allc['rays']} rays in {allc['seconds']} s; oracle/ref64.c "
+                      f"(linear scan, f64), {allc['threads']} threads",
+            "one_thread": {"value": one["value"], "unit": "Mrays/s",
+                           "sample": f"{one['sample']}; {one['rays']} rays in {one['seconds']} s",
+                           "note": "the reference's own execution model: one thread (main.rs:45-59)"}}
+
+
+# ---------------------------------------------------------------- helpers
 
 def pmc_traffic(config_key):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), or None."""
@@ -83,49 +203,134 @@ def pmc_traffic(config_key):
         return None
 
 
-def cpu_baseline(spec, args, **draws):
-    """Oracle (algorithmically the reference: same recursion, same linear scan,
-    f64) on the host, on a deterministic row sample of the same frame.
-    draws: jitter / seed / rng of a stochastic workload (the device's keyed draws)."""
-    from oracle import ref64
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    rows, stride = 8, max(1, spec.height // 8)
-    for _ in range(5):
-        # every stride-th row of the frame (a deterministic sample of the same workload),
-        # grown until the sample takes about cpu_seconds or covers the whole frame
-        rows = spec.height // stride
-        t0 = time.time()
-        r = ref64.render(spec, tile_h=rows, band=1, band_stride=stride, band_phase=0, threads=threads,
-                         want_rgb64=False, **draws)
-        dt = time.time() - t0
-        if dt >= 0.6 * args.cpu_seconds or stride == 1:
-            break
-        want = rows * args.cpu_seconds / max(dt, 1e-3)
-        stride = max(1, min(stride - 1, int(spec.height / want)))
-    return {"value": r["counts"]["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} rows (every {stride}th) x {spec.width} px of the same frame; "
-                      f"{r['counts']['rays']} rays in {dt:.2f} s; oracle/ref64.c, f64, {threads} threads"}
+class SharedFrame:
+    """One host frame shared by every rank (a /dev/shm file mapped by each),
+    page-locked in each process, that the ranks copy their row bands into."""
 
+    def __init__(self, name, nbytes, create):
+        import numpy as np
+        self.path = "/dev/shm/" + name
+        if create:
+            with open(self.path, "wb") as f:
+                f.truncate(nbytes)
+        self.f = open(self.path, "r+b")
+        self.mm = mmap.mmap(self.f.fileno(), nbytes)
+        self.arr = np.frombuffer(self.mm, dtype=np.uint8, count=nbytes)
+        self.pinned = False
+        try:
+            import torch
+            ok = torch.cuda.cudart().cudaHostRegister(self.arr.ctypes.data, nbytes, 0)
+            self.pinned = int(ok[0] if isinstance(ok, tuple) else ok) == 0
+        except Exception:
+            self.pinned = False
+
+    def close(self, unlink):
+        try:
+            if self.pinned:
+                import torch
+                torch.cuda.cudart().cudaHostUnregister(self.arr.ctypes.data)
+        except Exception:
+            pass
+        del self.arr
+        self.mm.close()
+        self.f.close()
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
+def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
+    """Every rank copies its bands of the frame (f32 RGB and BGR) into one shared
+    page-locked host frame; returns (best ms of 3, pinned) measured between barriers."""
+    import torch
+    nb = H // BAND
+    rgb_bytes, bgr_bytes = H * W * 12, H * pitch
+    name = [f"rtbench_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}"]
+    if world > 1:
+        dist.broadcast_object_list(name, src=0)
+    fr = SharedFrame(name[0], rgb_bytes + bgr_bytes, create=True) if rank == 0 else None
+    if world > 1:
+        dist.barrier()
+    if fr is None:
+        fr = SharedFrame(name[0], rgb_bytes + bgr_bytes, create=False)
+    try:
+        host = torch.from_numpy(fr.arr)
+        rgb_h = host[:rgb_bytes].view(nb, BAND * W * 12)[rank::world]
+        bgr_h = host[rgb_bytes:].view(nb, BAND * pitch)[rank::world]
+        out_rgb, out_bgr = outs_local
+        src_rgb = out_rgb.view(torch.uint8).reshape(-1, BAND * W * 12)
+        src_bgr = out_bgr.reshape(-1, BAND * pitch)
+        best = None
+        for _ in range(3):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            rgb_h.copy_(src_rgb)
+            bgr_h.copy_(src_bgr)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            ms = (time.perf_counter() - t0) * 1e3
+            best = ms if best is None else min(best, ms)
+        pinned = fr.pinned
+        del host, rgb_h, bgr_h
+    finally:
+        if world > 1:
+            dist.barrier()
+        fr.close(unlink=(rank == 0))
+    return best, pinned
+
+
+# ---------------------------------------------------------------- main
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
-    import libraytrace as lr
-    from libraytrace import scenes, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist_backend == "gloo":
-        local %= max(1, torch.cuda.device_count())      # rehearsal: several ranks per device
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "gloo" and n_dev:
+        local %= n_dev                               # rehearsal: several ranks per device
+    elif world > 1 and not args.dry_run and local >= n_dev:
+        raise SystemExit(f"rank {rank}: local rank {local} but only {n_dev} devices (one device per rank; "
+                         f"--dist-backend gloo rehearses more ranks than devices)")
     if world > 1:
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
+        if args.dist_backend == "nccl" and not args.dry_run:
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    red_dev = "cpu" if (args.dist_backend == "gloo" or args.dry_run) else torch.device("cuda", local)
+
+    def distinct_devices():
+        """Devices the ranks render on (n_gpus counts devices, not ranks)."""
+        t = torch.zeros(max(1, n_dev), dtype=torch.float64, device=red_dev)
+        if not args.dry_run and n_dev:
+            t[local] = 1
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.sum().item())
+
+    if args.dry_run:
+        n_gpus = distinct_devices()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "ranks": world, "n_gpus": n_gpus, "devices_visible": n_dev,
+                              "scaling": args.scaling, "backend": args.dist_backend}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    import numpy as np
+    import libraytrace as lr
+    from libraytrace import scenes, shard
     dev = torch.device("cuda", local)
 
     cfg = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
@@ -133,11 +338,11 @@ def main():
     path_cfg = args.config == "c1"
     args.width = args.width or cfg[0]
     args.height = args.height or cfg[0]
-    n_split = args.shard_of if (args.shard_of > 1 and world == 1) else world
-    if n_split > 1 and args.scaling == "weak":
+    band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
+    if band_world > 1 and args.scaling == "weak":
         # weak scaling: the same view at sqrt(N) x the resolution, so each of the N ranks renders
         # (up to rounding to whole bands) the N=1 frame's pixel count
-        f = n_split ** 0.5
+        f = band_world ** 0.5
         args.width = max(BAND, int(round(args.width * f / BAND)) * BAND)
         args.height = max(BAND, int(round(args.height * f / BAND)) * BAND)
     args.spheres = args.spheres or cfg[1]
@@ -152,6 +357,7 @@ def main():
     spp = spec.antialias
     jitter = lr.RT_JITTER_RANDOM if path_cfg else lr.RT_JITTER_CENTER
     W, H = spec.width, spec.height
+    assert H % BAND == 0, "bench frames are whole bands"
     scene = lr.Scene.deserialize(spec.to_text())
     F = max(1, args.inflight)
     ctxs = [lr.Context(local) for _ in range(F)]
@@ -159,10 +365,8 @@ def main():
         c.upload(scene)
     ctx = ctxs[0]
     rows = shard.local_rows(H, BAND, band_world, rank)
-    tail = shard.tail_rows(H, BAND) if shard.tail_owner(H, BAND, band_world) == rank else None
-    assert tail is None or len(tail) == 0, "bench frames are whole bands"
     algo = {"auto": lr.RT_ALGO_AUTO, "wavefront": lr.RT_ALGO_WAVEFRONT, "lds": lr.RT_ALGO_BRUTE_LDS,
-            "global": lr.RT_ALGO_BRUTE_GLOBAL}[args.algo]
+            "global": lr.RT_ALGO_BRUTE_GLOBAL, "path": lr.RT_ALGO_PATH}[args.algo]
     common = dict(tile_h=len(rows), band=BAND, band_stride=band_world, band_phase=rank, max_depth=args.depth,
                   spp=spp, algo=algo, jitter=jitter, seed=cfg[3])
     opts = lr.render_opts(W, H, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8, **common)
@@ -171,15 +375,14 @@ def main():
              torch.empty((len(rows), pitch), dtype=torch.uint8, device=dev)) for _ in range(F)]
     out_rgb, out_bgr = outs[0]
     # a real (non-null) stream: the library launches on exactly this stream, so the
-    # torch events below bracket the kernel (handle 0 would select the context's own stream)
+    # torch events below bracket the kernels (handle 0 would select the context's own stream)
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     stream = streams[0]
 
     # per-kernel-family launch durations come from K more frames that record HIP
     # events around every launch (RT_TIME_KERNELS), after the timed region: the
     # events sit between launches on both streams and would perturb the timing
-    timed_flags = opts.flags | lr.RT_TIME_KERNELS
-    opts_timed = lr.render_opts(W, H, flags=timed_flags, **common)
+    opts_timed = lr.render_opts(W, H, flags=opts.flags | lr.RT_TIME_KERNELS, **common)
 
     def step(o=opts, i=0):
         f = i % F
@@ -189,7 +392,7 @@ def main():
         step(i=i)
     torch.cuda.synchronize(dev)
     st = ctx.stats()                       # rays of one frame-slice (deterministic: same every step)
-    local_rays = st.rays
+    local_rays, local_traced = st.rays, st.traced_rays
     ctx.kernel_times()                     # discard anything recorded before the timed region
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -224,72 +427,91 @@ def main():
     except lr.RtError:
         gen_q, gen_s = [], []
 
-    # PCIe-inclusive rate: rt_render into host buffers, D2H of f32 RGB + BGR included.
-    # Reported beside `value`, never as it.
-    host_ms = []
-    for _ in range(2):
-        t0h = time.perf_counter()
-        ctx.render(opts)
-        host_ms.append((time.perf_counter() - t0h) * 1e3)
-    host_ms = min(host_ms)
+    # host gather: every rank's bands into one shared page-locked frame
+    gather_ms, gather_pinned = None, None
+    if not args.no_gather and band_world == world:
+        gather_ms, gather_pinned = host_gather(dist, world, rank, outs[0], W, H, pitch, dev)
 
-    t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms, float(wst.sphere_tests), float(wst.box_tests)],
-                     dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    # PCIe-inclusive rate: rt_render into reused pageable host buffers, kernels + D2H.
+    # Reported beside `value`, never as it.
+    host = {}
+    if world == 1:
+        hb = np.zeros((len(rows), pitch), np.uint8)
+        hr = np.zeros((len(rows), W, 3), np.float32)
+        for name, out in (("bgr", (None, hb)), ("rgb_bgr", (hr, hb))):
+            ms = []
+            for _ in range(3):
+                t0h = time.perf_counter()
+                ctx.render(opts, out=out)
+                ms.append((time.perf_counter() - t0h) * 1e3)
+            host[name] = min(ms)
+
+    n_gpus = distinct_devices()
+    t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms, float(wst.sphere_tests), float(wst.box_tests),
+                      float(local_traced), gather_ms or 0.0], dtype=torch.float64, device=red_dev)
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, avg_kernel_ms = mx[0].item(), mx[2].item()
-        total_rays = int(sm[1].item())
+        gather_ms = mx[6].item() if gather_ms is not None else None
+        total_rays, total_traced = int(sm[1].item()), int(sm[5].item())
         sphere_tests, box_tests = int(sm[3].item()), int(sm[4].item())
     else:
-        total_rays = local_rays
+        total_rays, total_traced = local_rays, local_traced
         sphere_tests, box_tests = wst.sphere_tests, wst.box_tests
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
-        value = total_rays * args.steps / elapsed / 1e6
+        value = total_traced * args.steps / elapsed / 1e6
         pixels_local = len(rows) * W
         scene_bytes = args.spheres * (32 + 4) + args.spheres * 128 + 2 * 56
         algo_bytes = pixels_local * (12 + 3) + scene_bytes          # f32 RGB + u8 BGR writes + scene read once
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
         key = f"{args.config}_{W}x{H}_n{args.spheres}_d{args.depth}"
-        traffic = pmc_traffic(key)
+        traffic = pmc_traffic(key) if world == 1 else None
         kernels = {}
         for fam, (ms, n) in ktimes.items():
             if n:
                 kernels["wf_" + fam] = {"avg_launch_us": round(ms / n * 1e3, 2),
                                         "launches_per_frame": round(n / args.steps, 2),
                                         "ms_per_frame": round(ms / args.steps, 4)}
-        if path_cfg:        # one launch of path_kernel per frame: its duration is the render's
+        path_kernel = path_cfg or args.algo == "path"
+        if path_kernel:        # one launch of path_kernel per frame: its duration is the render's
             kernels = {"path_kernel": {"avg_launch_us": round(avg_kernel_ms * 1e3, 2), "launches_per_frame": 1.0,
                                        "ms_per_frame": round(avg_kernel_ms, 4)}}
         dominant = max(kernels, key=lambda k: kernels[k]["ms_per_frame"]) if kernels else None
         if path_cfg:
             workload = (f"C1: test_scene.txt (IndirectPhong Cornell box, no lights) at {W}x{H}, {spp} random AA "
                         f"samples per pixel (keyed draws, seed {cfg[3]}), depth {args.depth}")
+            metric = f"Mrays/sec at {W}x{H}, test_scene.txt, {spp} AA samples, depth {args.depth}"
         else:
             workload = (f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
-                        f"depth {args.depth}, 1 spp centre jitter (seed {cfg[3]})")
+                        f"depth {args.depth}, {spp} spp centre jitter (seed {cfg[3]}); camera at (0, 3, 10) "
+                        f"looking into the sphere box (at C3 71% of the camera rays miss every sphere)")
+            metric = ("Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline"
+                      if (args.config, W, H) == ("c3", 4096, 4096)
+                      else f"Mrays/sec at {W}x{H}, {args.spheres} spheres, depth {args.depth}")
         line = {
-            "metric": "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline",
-            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric,
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
                        "width": W, "height": H, "spheres": args.spheres, "max_depth": args.depth, "spp": spp,
-                       "rays_per_frame": total_rays, "band_rows": BAND, "parallelism": f"row-bands x{world}", "frames_in_flight": F,
+                       "rays_per_frame": total_rays, "traced_rays_per_frame": total_traced, "band_rows": BAND,
+                       "parallelism": f"row-bands x{world}", "ranks": world, "frames_in_flight": F,
                        "algo": args.algo},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
-                         "kernel": "path_kernel" if path_cfg else
+                         "kernel": "path_kernel" if path_kernel else
                                    "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
                                    "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "kernels": kernels or None, "dominant_kernel": dominant,
-                         "note": "VALU-bound path (f64 exact tests, f32 BVH boxes); HBM fraction reported "
+                         "note": "latency-bound traversal (f64 exact tests, f32 BVH boxes); HBM fraction reported "
                                  "because the metric asks for it; see 'compute'"},
             "compute": {"bound": "valu", "sphere_tests_per_frame": sphere_tests, "box_tests_per_frame": box_tests,
                         "f64_flops_per_sphere_test": 19, "f32_flops_per_box_test": 20,
@@ -300,12 +522,19 @@ def main():
                         "generation_queue_sizes": gen_q[:args.depth + 3] if world == 1 else None,
                         "generation_shaded": gen_s[:args.depth + 3] if world == 1 else None},
         }
-        if world == 1:
-            line["pcie_inclusive"] = {"ms_per_frame": round(host_ms, 3),
-                                      "value": round(total_rays / (host_ms * 1e-3) / 1e6, 3), "unit": "Mrays/s",
-                                      "note": f"rt_render to pageable host buffers: kernels + D2H of "
-                                              f"{W * H * 12 / 1e6:.0f} MB f32 RGB + {W * H * 3 / 1e6:.0f} MB BGR "
-                                              f"(+ host allocation)"}
+        if gather_ms is not None:
+            line["host_gather"] = {"ms": round(gather_ms, 3), "pinned": bool(gather_pinned),
+                                   "bytes": H * W * 15,
+                                   "note": "after the timed region: every rank copies its row bands (f32 RGB + "
+                                           "BGR) into one shared page-locked host frame; max over ranks"}
+        if host:
+            line["pcie_inclusive"] = {
+                "bgr_only": {"ms_per_frame": round(host["bgr"], 3),
+                             "value": round(total_traced / (host["bgr"] * 1e-3) / 1e6, 3), "unit": "Mrays/s"},
+                "rgb_and_bgr": {"ms_per_frame": round(host["rgb_bgr"], 3),
+                                "value": round(total_traced / (host["rgb_bgr"] * 1e-3) / 1e6, 3), "unit": "Mrays/s"},
+                "note": f"rt_render into reused pageable host buffers: kernels + D2H of {W * H * 3 / 1e6:.0f} MB "
+                        f"BGR (+ {W * H * 12 / 1e6:.0f} MB f32 RGB) through the pinned staging slices"}
         if world == 1 and not args.no_cpu:
             try:
                 draws = dict(jitter=1, seed=cfg[3], rng=1) if path_cfg else {}

@@ -31,6 +31,12 @@
  *   - All pointers are caller-owned; the library copies what it keeps.
  *   - One rt_ctx per device; calls on one context are not thread-safe;
  *     different contexts may be driven concurrently (one host thread per GPU).
+ *   - A context's renders are ordered: each waits (on the device, not the
+ *     host) for the context's previous render, whatever streams they were
+ *     issued on, because they share the context's working set.
+ *     rt_scene_upload waits for every render still reading the old scene.
+ *   - Nothing is read from the environment: a render's schedule depends only
+ *     on the scene, the options and the context's tuning (rt_ctx_set_tuning).
  *   - All scene arithmetic is IEEE f64 exactly as the reference (no FMA
  *     contraction); output colours are the f64 result rounded once to f32,
  *     and the u8 BGR bytes are quantised from the f64 value on the device.
@@ -46,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum rt_status {
     RT_OK = 0,
@@ -132,10 +138,11 @@ int rt_scene_set_skybox(rt_scene* scene, const rt_texture faces[6]);
  * the hint.  counts[i] = its length, or -1 when the device tests every sphere
  * (degenerate direction, or no grid for this light); ids = the candidates'
  * object ids (file order, scene.rs:248), concatenated, at most cap in all.
- * info[0..2] = cells per face side, stored cells, list entries.
+ * info[0..2] = cells per face side, stored cells, list entries.  resolution:
+ * cells per face side (0 = the upload's automatic choice, else 1..4096).
  * Replaces nothing in the reference (its shadow query scans every object,
  * scene.rs:247-249); tests check the lists against that scan. */
-int rt_light_grid_candidates(const rt_scene* scene, int light, const double* points, uint32_t n_points,
+int rt_light_grid_candidates(const rt_scene* scene, int light, int resolution, const double* points, uint32_t n_points,
                              int32_t* counts, int32_t* ids, size_t cap, int64_t* info);
 /* Decode an image file as Texture::load does (RGB8, rows top-down).  rgb == NULL: only the size.
  * Formats: uncompressed BMP (24/32 bit) and binary PPM; others -> RT_E_UNSUPPORTED. */
@@ -188,7 +195,7 @@ typedef struct {
     uint32_t y0, tile_h;      /* local row j -> global row y0 + ((j/band)*band_stride + band_phase)*band + j%band */
     uint32_t band, band_stride, band_phase;   /* 0 -> 1: contiguous rows */
     uint32_t max_depth;       /* reference MAX_DEPTH = 4 (raytrace.rs:18); <= RT_MAX_DEPTH_LIMIT */
-    uint32_t spp;             /* AA samples (Options.antialias); 0 -> scene's value */
+    uint32_t spp;             /* AA samples (Options.antialias); 0 -> the uploaded scene's value */
     int32_t jitter;           /* rt_jitter */
     uint32_t flags;           /* rt_out_flags */
     int32_t algo;             /* rt_algo */
@@ -210,11 +217,17 @@ typedef struct {
     uint64_t box_tests;       /* RT_COUNT_WORK only: BVH slab tests (2 per inner node visited) */
     uint64_t sphere_tests;    /* RT_COUNT_WORK only: exact ray-sphere quadratics evaluated */
     uint64_t shadow_box_tests, shadow_sphere_tests;   /* the shadow-query share of the two above */
+    uint64_t traced_rays;     /* queries the device actually traced: `rays` / spp when a chain schedule
+                                 renders spp identical centre-jitter samples once, else `rays` */
 } rt_stats;
 
 void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height);
 
-/* Synchronous: renders into caller-owned HOST buffers (either may be NULL). */
+/* Synchronous: renders into caller-owned HOST buffers (either may be NULL).
+ * Page-locked buffers (hipHostMalloc / hipHostRegister) receive the DMA
+ * directly; pageable ones are filled through two pinned 16 MiB slices, the
+ * copy engine writing one while host threads empty the other.  Pass only the
+ * outputs needed: BGR alone moves 3 B per pixel instead of 15. */
 int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* out_bgr, rt_stats* stats);
 /* Asynchronous on `stream` (a hipStream_t; NULL = the context's own stream):
  * renders into caller-owned DEVICE buffers.  Statistics of the most recent
@@ -240,6 +253,19 @@ enum rt_kernel_family {
     RT_KF_COUNT = 7
 };
 int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
+
+/* Schedule tuning of a context (A/B measurement; the defaults are the measured
+ * best).  Keys (rt_tuning_key(i) for i = 0, 1, ... until NULL):
+ * chunk_pixels (wavefront chunk cap), bvh_leaf, light_grids, light_grid_res
+ * (these three take effect at the next rt_scene_upload), src, src_occ,
+ * prefix_kb, prefix4_kb, lanes, stagger_gen, regions, split, bstreams, fuse,
+ * lists, cam, deal, spread_below, lists0, path_group, cu_mask, prio, verbose,
+ * grid_occ.
+ * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
+ * them (tests/test_gpu_parity.py renders under several and compares bits). */
+int rt_ctx_set_tuning(rt_ctx* ctx, const char* key, int64_t value);
+int rt_ctx_get_tuning(const rt_ctx* ctx, const char* key, int64_t* value);
+const char* rt_tuning_key(int index);
 
 #ifdef __cplusplus
 }

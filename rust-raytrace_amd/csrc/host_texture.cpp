@@ -5,6 +5,7 @@
 // PPM (P6, maxval 255).  The result is what `image::open(path).to_rgb()`
 // yields: RGB8, rows top-down.
 #include <cctype>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -18,6 +19,10 @@ namespace {
 uint32_t le16(const uint8_t* p) { return p[0] | (p[1] << 8); }
 uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | (static_cast<uint32_t>(p[3]) << 24); }
 
+// Largest side accepted (a texture is at most 2^15 x 2^15 texels = 3 GiB of
+// RGB8): every size product below then fits in 64 bits without wrapping.
+constexpr uint64_t kMaxSide = 1u << 15;
+
 int decode_bmp(const std::vector<uint8_t>& f, HostTexture& t, std::string& err) {
     if (f.size() < 54) { err = "truncated BMP header"; return RT_E_IO; }
     const uint32_t data_off = le32(&f[10]), hdr = le32(&f[14]);
@@ -28,11 +33,12 @@ int decode_bmp(const std::vector<uint8_t>& f, HostTexture& t, std::string& err) 
         err = "unsupported BMP encoding (" + std::to_string(bpp) + " bpp, compression " + std::to_string(comp) + ")";
         return RT_E_UNSUPPORTED;
     }
-    if (w <= 0 || h == 0) { err = "empty BMP"; return RT_E_IO; }
+    if (w <= 0 || h == 0 || h == INT32_MIN) { err = "empty BMP"; return RT_E_IO; }
     const bool bottom_up = h > 0;
-    const uint32_t H = static_cast<uint32_t>(bottom_up ? h : -h), W = static_cast<uint32_t>(w);
+    const uint32_t H = static_cast<uint32_t>(bottom_up ? h : -static_cast<int64_t>(h)), W = static_cast<uint32_t>(w);
+    if (W > kMaxSide || H > kMaxSide) { err = "BMP larger than 32768 x 32768"; return RT_E_UNSUPPORTED; }
     const uint64_t pitch = (static_cast<uint64_t>(W) * (bpp / 8) + 3) & ~3ull;
-    if (data_off + pitch * H > f.size()) { err = "truncated BMP pixel data"; return RT_E_IO; }
+    if (static_cast<uint64_t>(data_off) + pitch * H > f.size()) { err = "truncated BMP pixel data"; return RT_E_IO; }
     t.width = W;
     t.height = H;
     t.rgb.assign(static_cast<size_t>(W) * H * 3, 0);
@@ -68,7 +74,9 @@ int decode_ppm(const std::vector<uint8_t>& f, HostTexture& t, std::string& err) 
     if (!num(w) || !num(h) || !num(mx) || i >= f.size()) { err = "bad PPM header"; return RT_E_IO; }
     if (mx != 255) { err = "unsupported PPM maxval " + std::to_string(mx); return RT_E_UNSUPPORTED; }
     ++i;                                               // one whitespace byte ends the header
-    if (w == 0 || h == 0 || i + w * h * 3 > f.size()) { err = "truncated PPM"; return RT_E_IO; }
+    if (w == 0 || h == 0) { err = "empty PPM"; return RT_E_IO; }
+    if (w > kMaxSide || h > kMaxSide) { err = "PPM larger than 32768 x 32768"; return RT_E_UNSUPPORTED; }
+    if (w * h * 3 > f.size() - i) { err = "truncated PPM"; return RT_E_IO; }
     t.width = static_cast<uint32_t>(w);
     t.height = static_cast<uint32_t>(h);
     t.rgb.assign(f.begin() + i, f.begin() + i + w * h * 3);

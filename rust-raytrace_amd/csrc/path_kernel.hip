@@ -373,12 +373,10 @@ __global__ __launch_bounds__(kPathBlock, RT_PATH_WAVES) void path_kernel(DevScen
     for (int i = threadIdx.x; i < 255; i += kPathBlock) s_srgb[i] = fp.srgb[i];
     BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     if constexpr (kNodes == 2) {
-        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds + 2048);
-        for (int i = threadIdx.x; i < sc.n_bvh; i += kPathBlock) ln[i] = sc.bvh[i];
-        DevSphere* ls = reinterpret_cast<DevSphere*>(ln + sc.n_bvh);
+        v.lnodes = stage_node_planes<kPathBlock>(sc.bvh, sc.n_bvh, lds + 2048);
+        DevSphere* ls = reinterpret_cast<DevSphere*>(lds + 2048 + node_planes_bytes(sc.n_bvh));
         int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
         for (int i = threadIdx.x; i < sc.n_spheres; i += kPathBlock) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
-        v.lnodes = ln;
         v.nl = sc.n_bvh;
         v.sph = ls;
         v.obj = lo;
@@ -448,7 +446,7 @@ int path_waves_per_simd() { return RT_PATH_WAVES; }
 
 size_t path_lds_bytes(const DevScene& sc, bool staged) {
     size_t b = 2048;
-    if (staged) b += static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode) + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + 4);
+    if (staged) b += node_planes_bytes(sc.n_bvh) + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + 4);
     return b;
 }
 

@@ -8,7 +8,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -18,6 +20,51 @@
 #include "launch_api.hpp"
 
 using namespace rtamd;
+
+namespace {
+
+// Schedule knobs of a context (rt_ctx_set_tuning).  The defaults are the
+// measured-best settings; nothing is read from the environment,
+// so a render's schedule depends only on the scene, the options and these.
+enum TuneKey : int {
+    kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
+    kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
+    kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
+    kTuneVerbose, kTuneGridOcc, kTuneCount
+};
+struct TuneDef {
+    const char* name;
+    int64_t dflt, lo, hi;
+};
+// -1 in src / src_occ / cam: chosen per scene
+constexpr TuneDef kTune[kTuneCount] = {
+    {"chunk_pixels", 1 << 25, 64, INT32_MAX},   // wavefront chunk cap: ~17 GB of working set at depth 8
+    {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
+    {"light_grids", 1, 0, 1},                    // light-view grids for point-light shadow queries
+    {"light_grid_res", 0, 0, 4096},              // 0: from the median sphere's angular size
+    {"src", -1, -1, 13},                         // nearest-hit sphere source (trace_kernel.hip kSrc*)
+    {"src_occ", -1, -1, 13},                     // shadow sphere source
+    {"prefix_kb", 64, 1, 160},                   // LDS prefix of the binary tree (KB) for trees that do not fit
+    {"prefix4_kb", 0, 0, 160},                   // LDS prefix of the 4-wide tree (0: read through L2)
+    {"lanes", 1, 1, 8},                          // chunk lanes (each its own streams and working set)
+    {"stagger_gen", 1, 0, 64},                   // lanes: chunk c+1 starts after this generation of chunk c
+    {"regions", 0, 0, 2048},                     // regions per queue (0: 2 x CUs)
+    {"split", 1, 0, 1},                          // 0: every wavefront kernel on one in-order stream
+    {"bstreams", 2, 1, 4},                       // streams for the shadow + shading kernels
+    {"fuse", 0, 0, 1},                           // shading inside the shadow kernel
+    {"lists", 1, 0, 1},                          // shadow item lists (with fuse)
+    {"cam", -1, -1, 2},                          // generation 0: 0 per ray, 1 camera tiles in LDS, 2 from L2
+    {"deal", 1, 0, 1},                           // chunk dealing: 1 workgroup-major, 0 workgroup-first
+    {"spread_below", 0, 0, INT32_MAX},           // queues below this size are dealt workgroup-first
+    {"lists0", 0, 0, 1},                         // shadow lists from generation 0
+    {"path_group", 0, 0, 64},                    // path kernel: lanes per pixel (0: auto)
+    {"cu_mask", 1, 0, 1},                        // b streams CU-masked (own hardware queue)
+    {"prio", 0, 0, 1},                           // nearest-hit chain on a high-priority stream
+    {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
+    {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
+};
+
+}  // namespace
 
 struct rt_ctx {
     int device = 0;
@@ -29,6 +76,7 @@ struct rt_ctx {
     DevScene dsc{};
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
+    bool all_lights_gridded = false; // every light is a point light with a light-view grid
     unsigned long long* d_counters = nullptr;
     double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
     void* d_path = nullptr;           // path kernel recursion stack (PathStack)
@@ -61,7 +109,17 @@ struct rt_ctx {
     std::vector<LaunchInterval> tint;
     hipEvent_t fork = nullptr;
     bool wf_used = false;
+    uint32_t scene_spp = 1;           // the uploaded scene's Options.antialias (rt_render_opts.spp = 0)
+    hipEvent_t render_done = nullptr; // end of the last render on its stream: the next one waits for it
+    bool render_pending = false;
+    uint32_t last_spp_traced = 1;     // chain schedules trace one of spp identical centre-jitter samples
+    // rt_render: two pinned staging slices for the device -> host copy of the outputs
+    void* pin[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    int64_t tune[kTuneCount];
     std::string err;
+    rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
+    int64_t t(TuneKey k) const { return tune[k]; }
 };
 
 namespace {
@@ -82,6 +140,20 @@ int hip_fail(rt_ctx* c, hipError_t e, const char* what) {
         if (_e != hipSuccess) return hip_fail((c), _e, #expr);      \
     } while (0)
 
+// No C++ exception crosses the ABI: allocation failures become RT_E_NOMEM.
+template <class F>
+int guarded(rt_ctx* c, F&& body) {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return fail(c, RT_E_NOMEM, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(c, RT_E_INVALID, e.what());
+    } catch (...) {
+        return fail(c, RT_E_INVALID, "unexpected exception");
+    }
+}
+
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // counters: [0, 256) rays per shard (megakernel), [256, 512) shadow rays per
@@ -97,17 +169,6 @@ static_assert(kLightArea == RT_LIGHT_AREA, "DevLight::kind mirrors rt_light_kind
 // LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
 constexpr size_t kLdsBudget = 72 * 1024;
 
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
-
-uint32_t wf_chunk_pixels() {
-    const char* e = std::getenv("RT_WF_CHUNK_PIXELS");
-    long v = e ? std::atol(e) : 0;
-    return v > 0 ? static_cast<uint32_t>(v) : (1u << 25);   // 33.5 M pixels: ~17 GB of working set at depth 8
-}
-
 // The b streams need hardware queues of their own: HIP deals streams over a
 // few shared queues (GPU_MAX_HW_QUEUES), and two streams on one queue run
 // strictly in submission order.  A CU-masked stream (mask = every CU) gets a
@@ -118,7 +179,7 @@ int ensure_bstreams(rt_ctx* c, rt_ctx::Lane& M, int nb) {
     for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
     while (static_cast<int>(M.sb.size()) < nb) {
         hipStream_t s = nullptr;
-        if (env_int("RT_WF_CUMASK", 1) == 0 ||
+        if (c->t(kTuneCuMask) == 0 ||
             hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()) != hipSuccess) {
             (void)hipGetLastError();
             HIP_TRY(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -136,9 +197,9 @@ int ensure_lanes(rt_ctx* c, int n) {
         rt_ctx::Lane L;
         c->lanes.push_back(L);
         rt_ctx::Lane& M = c->lanes.back();
-        // RT_WF_PRIO=1: the nearest-hit chain (the critical path) on a high-priority stream
+        // prio: the nearest-hit chain (the critical path) on a high-priority stream
         int lo = 0, hi = 0;
-        if (env_int("RT_WF_PRIO", 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+        if (c->t(kTunePrio) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
             HIP_TRY(c, hipStreamCreateWithPriority(&M.s, hipStreamNonBlocking, hi));
         } else {
             HIP_TRY(c, hipStreamCreateWithFlags(&M.s, hipStreamNonBlocking));
@@ -231,6 +292,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->render_done, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_srgb, 255 * sizeof(double)) != hipSuccess ||
         hipMemcpy(c->d_srgb, srgb_average_table(), 255 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
@@ -243,6 +305,7 @@ int rt_ctx_create(int device, rt_ctx** out) {
 void rt_ctx_destroy(rt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->render_pending) (void)hipEventSynchronize(c->render_done);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_blob) (void)hipFree(c->d_blob);
     if (c->d_counters) (void)hipFree(c->d_counters);
@@ -262,6 +325,11 @@ void rt_ctx_destroy(rt_ctx* c) {
         for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
     }
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    if (c->render_done) (void)hipEventDestroy(c->render_done);
+    for (int i = 0; i < 2; ++i) {
+        if (c->pin[i]) (void)hipHostFree(c->pin[i]);
+        if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
+    }
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -271,10 +339,11 @@ void rt_ctx_destroy(rt_ctx* c) {
 
 const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : thread_error(); }
 
-int rt_light_grid_candidates(const rt_scene* s, int light, const double* points, uint32_t n_points, int32_t* counts,
-                             int32_t* ids, size_t cap, int64_t* info) {
+int rt_light_grid_candidates(const rt_scene* s, int light, int resolution, const double* points, uint32_t n_points,
+                             int32_t* counts, int32_t* ids, size_t cap, int64_t* info) {
     if (!s || (n_points && (!points || !counts)) || (cap && !ids)) return RT_E_INVALID;
-    if (light < 0 || light >= static_cast<int>(s->lights.size())) return RT_E_INVALID;
+    if (light < 0 || light >= static_cast<int>(s->lights.size()) || resolution < 0 || resolution > 4096)
+        return RT_E_INVALID;
     try {
         std::vector<DevSphere> spheres;
         std::vector<double> srad;
@@ -298,7 +367,7 @@ int rt_light_grid_candidates(const rt_scene* s, int light, const double* points,
             d.kind = l.kind;
             lights.push_back(d);
         }
-        const LightGridResult lg = build_light_grids(spheres, srad, lights, 1e-5 * (1.0 + extent), env_int("RT_LGRID_R", 0));
+        const LightGridResult lg = build_light_grids(spheres, srad, lights, 1e-5 * (1.0 + extent), resolution);
         if (info) {
             info[0] = lg.grids[light].R;
             int64_t cells = 0;
@@ -322,8 +391,7 @@ int rt_light_grid_candidates(const rt_scene* s, int light, const double* points,
     }
 }
 
-int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
-    if (!c || !s) return RT_E_INVALID;
+static int scene_upload(rt_ctx* c, const rt_scene* s) {
     HIP_TRY(c, hipSetDevice(c->device));
     // Every class of the reference except SkyboxBackground (textures) has a
     // device implementation: Phong / Fresnel chains on the wavefront path,
@@ -393,9 +461,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
             if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
     }
     // Leaves of 2 spheres measured fastest at C3; 4 when that tree and the
-    // spheres would not fit the traversal kernels' LDS budget (RT_BVH_LEAF overrides).
+    // spheres would not fit the traversal kernels' LDS budget (tuning "bvh_leaf" overrides).
     const double pad = 1e-5 * (1.0 + extent);
-    const int leaf_env = env_int("RT_BVH_LEAF", 0);
+    const int leaf_env = static_cast<int>(c->t(kTuneBvhLeaf));
     BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf_env > 0 ? leaf_env : 2);
     if (leaf_env <= 0 && bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
         bvh = build_sphere_bvh(sx, sy, sz, srad, pad, 4);
@@ -414,9 +482,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
         spheres.swap(s2);
         sphere_obj.swap(o2);
     }
-    // light-view grids of the point lights (RT_WF_LGRID=0 disables; RT_LGRID_R forces the resolution)
+    // light-view grids of the point lights (tuning: "light_grids" 0 disables, "light_grid_res" forces the resolution)
     LightGridResult lg;
-    if (env_int("RT_WF_LGRID", 1) != 0) lg = build_light_grids(spheres, r_leaf, lights, pad, env_int("RT_LGRID_R", 0));
+    if (c->t(kTuneLgrid) != 0) lg = build_light_grids(spheres, r_leaf, lights, pad, static_cast<int>(c->t(kTuneLgridRes)));
     // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights][bvh], 256-B aligned pieces.
     size_t off = 0;
     auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
@@ -456,6 +524,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_lgent, lg.ent.data(), lg.ent.size() * sizeof(DevLgEntry));
     if (skybox)
         for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
+    // every render still reading the old blob (on any stream) must be done before it is overwritten
+    if (c->render_pending) HIP_TRY(c, hipEventSynchronize(c->render_done));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_blob && c->blob_bytes < total) { (void)hipFree(c->d_blob); c->d_blob = nullptr; c->blob_bytes = 0; }
     if (!c->d_blob) {
@@ -507,8 +577,16 @@ int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
     d.lgrid = lg.grids.empty() ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_lg);
     d.lg_off = reinterpret_cast<const uint32_t*>(base + o_lgoff);
     d.lg_ent = reinterpret_cast<const DevLgEntry*>(base + o_lgent);
+    c->all_lights_gridded = !lights.empty() && lg.grids.size() == lights.size();
+    for (const DevLightGrid& g : lg.grids) c->all_lights_gridded = c->all_lights_gridded && g.R > 0;
+    c->scene_spp = s->antialias;
     c->has_scene = true;
     return RT_OK;
+}
+
+int rt_scene_upload(rt_ctx* c, const rt_scene* s) {
+    if (!c || !s) return RT_E_INVALID;
+    return guarded(c, [&] { return scene_upload(c, s); });
 }
 
 static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_t& band, uint32_t& stride, uint32_t& pitch) {
@@ -525,22 +603,24 @@ static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_
         uint64_t last = o->y0 + ((j / band) * stride + o->band_phase) * band + j % band;
         if (last >= o->height) return fail(c, RT_E_INVALID, "tile exceeds frame height");
     }
-    spp = o->spp;
-    if (spp == 0) return fail(c, RT_E_INVALID, "spp must be set (the scene's antialias value for reference behaviour)");
+    spp = o->spp ? o->spp : c->scene_spp;                     // 0: the scene's Options.antialias
+    if (spp == 0) return fail(c, RT_E_INVALID, "spp is 0 and the scene's antialias is 0");
     pitch = o->bgr_pitch ? o->bgr_pitch : 3 * o->tile_w;
     if (pitch < 3 * o->tile_w) return fail(c, RT_E_INVALID, "bgr_pitch < 3*tile_w");
     if (o->algo < RT_ALGO_AUTO || o->algo > RT_ALGO_PATH) return fail(c, RT_E_INVALID, "bad algo");
     return RT_OK;
 }
 
-int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
-    if (!c) return RT_E_INVALID;
+static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
     if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
     uint32_t spp, band, stride, pitch;
     int rc = check_opts(c, o, spp, band, stride, pitch);
     if (rc != RT_OK) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    // The context's working sets (counters, wavefront buffers, path stacks) are
+    // shared by its renders: a render on another stream waits for the previous one.
+    if (c->render_pending) HIP_TRY(c, hipStreamWaitEvent(st, c->render_done, 0));
     FrameParams fp{};
     fp.hw = static_cast<double>(o->width) / 2.0;              // main.rs:39-41
     fp.hh = static_cast<double>(o->height) / 2.0;
@@ -594,7 +674,13 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
     c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
     c->last_stream = st;
-    if (o->tile_w == 0 || o->tile_h == 0) { c->last_timed = false; return RT_OK; }
+    c->last_spp_traced = 1;
+    if (o->tile_w == 0 || o->tile_h == 0) {
+        c->last_timed = false;
+        HIP_TRY(c, hipEventRecord(c->render_done, st));
+        c->render_pending = true;
+        return RT_OK;
+    }
     if (mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) {
         // LDS per traversal workgroup (1024 threads, two resident per CU): the
         // whole BVH + sphere list when they fit, else the top of the tree.
@@ -604,7 +690,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // (nearest, occlusion) sphere sources, see launch_api.hpp.  Default: the
         // binary tree for the nearest-hit query and the 4-wide tree for the
         // shadow query, each staged whole in LDS with the spheres when it fits
-        // (measured best at C3); RT_WF_SRC = "n" or "n,o" overrides.
+        // (measured best at C3); tuning "src" / "src_occ" override.
         int src, src_occ;
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool fit2 = node_bytes + sph_bytes <= kLdsBudget;
@@ -614,10 +700,9 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             src_occ = fit4 ? 10 : 13;
             if (!fit2 || !fit4) { src = 8; src_occ = 13; }
             if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;  // the 4-wide stack could overflow
-            if (const char* force = std::getenv("RT_WF_SRC")) {
-                int n = -1, oc = -1;
-                const int got = std::sscanf(force, "%d,%d", &n, &oc);
-                if (got >= 1) { src = n; src_occ = got == 2 ? oc : n; }
+            if (c->t(kTuneSrc) >= 0) {
+                src = static_cast<int>(c->t(kTuneSrc));
+                src_occ = c->t(kTuneSrcOcc) >= 0 ? static_cast<int>(c->t(kTuneSrcOcc)) : src;
             }
             auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
             const bool pair_ok = ok(src) && ok(src_occ) &&
@@ -628,11 +713,10 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
                               !((src_occ == 10 || src_occ == 12) && !fit4);
             if (!pair_ok || !fits) { src = 2; src_occ = 11; }
             if (c->deep_bvh4 && src_occ >= 10) src_occ = src = 2;
-            // LDS prefix sizes (RT_WF_PREFIX_KB = "nearest,shadow" overrides): measured at C4,
-            // 64 KB of binary nodes for the nearest-hit kernels; the 4-wide shadow tree stays in
-            // HBM/L2 by default (src 11), a prefix there costs more in co-residency than it saves
-            int kb2 = 64, kb4 = 0;
-            if (const char* pk = std::getenv("RT_WF_PREFIX_KB")) std::sscanf(pk, "%d,%d", &kb2, &kb4);
+            // LDS prefix sizes (tuning "prefix_kb", "prefix4_kb"): measured at C4, 64 KB of binary
+            // nodes for the nearest-hit kernels; the 4-wide shadow tree stays in HBM/L2 by default
+            // (src 11), a prefix there costs more in co-residency than it saves
+            const int kb2 = static_cast<int>(c->t(kTunePrefixKb2)), kb4 = static_cast<int>(c->t(kTunePrefixKb4));
             c->dsc.pfx2 = static_cast<int32_t>(static_cast<size_t>(std::max(kb2, 1)) * 1024 / sizeof(DevBvhNode));
             c->dsc.pfx4 = static_cast<int32_t>(static_cast<size_t>(std::max(kb4, 1)) * 1024 / (kBvh4Planes * sizeof(DevBvh4Plane)));
             if (src_occ == 13 && kb4 <= 0) src_occ = 11;
@@ -642,12 +726,12 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         // (balanced: a frame slightly over the cap becomes two halves, not a full chunk plus a
         // sliver that pays every generation's launch latency again)
-        uint32_t chunk_rows = std::max<uint32_t>(8, (wf_chunk_pixels() / o->tile_w) / 8 * 8);
+        uint32_t chunk_rows = std::max<uint32_t>(8, (static_cast<uint32_t>(c->t(kTuneChunkPixels)) / o->tile_w) / 8 * 8);
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
         const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
         chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);
-        const int n_lanes = std::max(1, std::min<int>(env_int("RT_WF_STREAMS", 1), static_cast<int>(n_chunks)));
-        const int mark_gen = std::max(0, std::min<int>(env_int("RT_WF_STAGGER_GEN", 1), static_cast<int>(o->max_depth) + 1));
+        const int n_lanes = std::max(1, std::min<int>(static_cast<int>(c->t(kTuneLanes)), static_cast<int>(n_chunks)));
+        const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));
         int rc2 = ensure_lanes(c, n_lanes);
         if (rc2 != RT_OK) return rc2;
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
@@ -657,36 +741,36 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // workgroup resident at once (1024 threads with the LDS-staged BVH),
         // so the wave-chunk dealing spreads even a small tail queue over the
         // whole chip in one round; fewer for small chunks; R covers every slot.
-        const int g_env = env_int("RT_WF_REGIONS", 0);
+        const int g_env = static_cast<int>(c->t(kTuneRegions));
         uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
         G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
         const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
-        // RT_WF_SPLIT=0: every kernel on one in-order stream (A/B measurement);
-        // RT_WF_DEAL: 1 workgroup-major chunk dealing (default), 0 workgroup-first
-        // RT_WF_BSTREAMS: streams for the shadow + shading kernels (default 2;
-        // generations alternate over them); RT_WF_FUSE=1: shading fused into the shadow kernel
-        const bool split = env_int("RT_WF_SPLIT", 1) != 0;
+        // tuning "split" 0: every kernel on one in-order stream (A/B measurement);
+        // "deal": 1 workgroup-major chunk dealing (default), 0 workgroup-first;
+        // "bstreams": streams for the shadow + shading kernels (default 2;
+        // generations alternate over them); "fuse" 1: shading fused into the shadow kernel
+        const bool split = c->t(kTuneSplit) != 0;
         // two b streams (consecutive generations' shadows and shading overlap): measured
         // 3.87 -> 3.78 ms at C3 once the shading runs in its own kernel; three are slower
-        const int n_b = std::max(1, std::min(kMaxBStreams, env_int("RT_WF_BSTREAMS", 2)));
+        const int n_b = std::max(1, std::min(kMaxBStreams, static_cast<int>(c->t(kTuneBStreams))));
         // (fused shading measured slower once shadow queries went through the light-view
         // grids: the shading's pow and the per-light atomics then dominate the fused kernel)
-        const bool fuse = env_int("RT_WF_FUSE", 0) != 0;
-        // shadow item lists (RT_WF_LISTS=0: every (record, light) pair goes to the shadow kernel)
-        const uint32_t nlists = (split && fuse && env_int("RT_WF_LISTS", 1) != 0 && c->dsc.n_lights > 0 &&
+        const bool fuse = c->t(kTuneFuse) != 0;
+        // shadow item lists ("lists" 0: every (record, light) pair goes to the shadow kernel)
+        const uint32_t nlists = (split && fuse && c->t(kTuneLists) != 0 && c->dsc.n_lights > 0 &&
                                  c->dsc.n_lights <= 24) ? static_cast<uint32_t>(c->dsc.n_lights) + 1u : 0u;
-        // generation 0 by camera tile (RT_WF_CAM=0: per-ray like the other generations);
+        // generation 0 by camera tile ("cam" 0: per-ray like the other generations);
         // only with the binary-tree sources, whose node order the camera view shares
         int cam = 0;
         if (src == 2 || src == 4 || src == 7 || src == 8) {
             const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
             cam = cam_lds <= kLdsBudget ? 1 : 2;
-            const int ce = env_int("RT_WF_CAM", -1);
+            const int ce = static_cast<int>(c->t(kTuneCam));
             if (ce == 0) cam = 0;
             else if (ce == 2) cam = 2;
         }
-        const uint32_t wg_major = env_int("RT_WF_DEAL", 1) != 0 ? 1u : 0u;
-        if (env_int("RT_WF_VERBOSE", 0))
+        const uint32_t wg_major = c->t(kTuneDeal) != 0 ? 1u : 0u;
+        if (c->t(kTuneVerbose))
             std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d pfx %d/%d\n", src, src_occ, cam,
                          nlists, c->deep_bvh4 ? 1 : 0, c->dsc.pfx2, c->dsc.pfx4);
         for (int l = 0; l < n_lanes; ++l) {
@@ -695,7 +779,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             if (rc2 != RT_OK) return rc2;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
-            c->lanes[l].b.spread_below = static_cast<uint32_t>(std::max(0, env_int("RT_WF_SPREAD_BELOW", 0)));
+            c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
         }
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
         // per-launch timing needs one in-order stream
@@ -734,7 +818,12 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
             ws.cam = cam;
-            ws.lists0 = env_int("RT_WF_LISTS0", 0) != 0;
+            ws.lists0 = c->t(kTuneLists0) != 0;
+            // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
+            // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
+            ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
+                              ? (static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere) <= 64 * 1024 ? 1 : 2)
+                              : 0;
             HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, ws, L.mark, mark_gen));
         }
         for (int l = 0; l < n_lanes; ++l) {
@@ -752,7 +841,7 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         // lanes per pixel: enough work-items to fill the chip, at most one per AA sample
         uint32_t G = 1;
         while (G < 64 && 2 * G <= spp && npix * G < T_full) G *= 2;
-        if (const int ge = env_int("RT_PATH_GROUP", 0)) G = static_cast<uint32_t>(ge);   // A/B override
+        if (const int64_t ge = c->t(kTunePathGroup)) G = static_cast<uint32_t>(ge);   // A/B override
         if (G == 0 || (G & (G - 1)) || G > 64) G = 1;
         fp.path_group = G;
         const uint32_t T = static_cast<uint32_t>(std::min<uint64_t>(T_full, (npix * G + 255) / 256 * 256));
@@ -778,8 +867,18 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
         HIP_TRY(c, hipEventRecord(c->ev1, st));
     }
+    // the chain schedules (wavefront, megakernel) trace one camera ray tree per
+    // pixel and count it spp times: the spp centre-jitter samples are identical
+    if (mode != RT_ALGO_PATH) c->last_spp_traced = spp;
+    HIP_TRY(c, hipEventRecord(c->render_done, st));
+    c->render_pending = true;
     c->last_timed = true;
     return RT_OK;
+}
+
+int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
+    if (!c) return RT_E_INVALID;
+    return guarded(c, [&] { return render_device(c, o, d_rgb, d_bgr, stream); });
 }
 
 int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
@@ -798,6 +897,7 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     s->shadow_box_tests = h[kTotals + 4];
     s->shadow_sphere_tests = h[kTotals + 5];
     s->pixels = c->last_pixels;
+    s->traced_rays = c->last_spp_traced > 1 ? s->rays / c->last_spp_traced : s->rays;
     if (c->last_timed) {
         float ms = 0.f;
         HIP_TRY(c, hipEventSynchronize(c->ev1));
@@ -837,8 +937,55 @@ int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
     return RT_OK;
 }
 
-int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
-    if (!c || !o) return RT_E_INVALID;
+// Device -> caller-owned host memory.  A page-locked destination gets the DMA
+// directly; pageable memory goes through two pinned slices, the copy engine
+// filling one while host threads move the other out.
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return RT_OK;
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, dst) == hipSuccess && attr.type == hipMemoryTypeHost) {
+        HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return RT_OK;
+    }
+    (void)hipGetLastError();                       // a pageable pointer is not an error
+    constexpr size_t kSlice = 16u << 20;
+    for (int i = 0; i < 2; ++i) {
+        if (!c->pin[i]) HIP_TRY(c, hipHostMalloc(&c->pin[i], kSlice, hipHostMallocDefault));
+        if (!c->pin_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
+    }
+    auto drain = [&](size_t slice) {               // host copy of slice `slice` out of its pinned buffer
+        const size_t off = slice * kSlice, len = std::min(kSlice, bytes - off);
+        const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+        const size_t parts = std::max<size_t>(1, std::min<size_t>(hw, len >> 21));   // >= 2 MiB per thread
+        const size_t step = (len + parts - 1) / parts;
+        const auto* from = static_cast<const uint8_t*>(c->pin[slice & 1]);
+        auto* to = static_cast<uint8_t*>(dst) + off;
+        std::vector<std::thread> th;
+        for (size_t p = 1; p < parts; ++p) {
+            const size_t a = p * step, b = std::min(len, a + step);
+            if (a < b) th.emplace_back([=] { std::memcpy(to + a, from + a, b - a); });
+        }
+        std::memcpy(to, from, std::min(len, step));
+        for (std::thread& t : th) t.join();
+    };
+    const size_t n = (bytes + kSlice - 1) / kSlice;
+    for (size_t i = 0; i <= n; ++i) {
+        if (i < n) {                                // slot i & 1 was drained in iteration i - 1
+            const size_t off = i * kSlice, len = std::min(kSlice, bytes - off);
+            HIP_TRY(c, hipMemcpyAsync(c->pin[i & 1], static_cast<const uint8_t*>(src) + off, len,
+                                      hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipEventRecord(c->pin_ev[i & 1], c->stream));
+        }
+        if (i >= 1) {
+            HIP_TRY(c, hipEventSynchronize(c->pin_ev[(i - 1) & 1]));
+            drain(i - 1);
+        }
+    }
+    return RT_OK;
+}
+
+static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
     uint32_t spp, band, stride, pitch;
     int rc = check_opts(c, o, spp, band, stride, pitch);
     if (rc != RT_OK) return rc;
@@ -847,6 +994,8 @@ int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_b
     oo.flags = (o->flags & ~(RT_OUT_RGB_F32 | RT_OUT_BGR_U8)) | (out_rgb ? RT_OUT_RGB_F32 : 0) | (out_bgr ? RT_OUT_BGR_U8 : 0);
     const size_t rgb_bytes = static_cast<size_t>(o->tile_w) * o->tile_h * 3 * sizeof(float);
     const size_t bgr_bytes = static_cast<size_t>(pitch) * o->tile_h;
+    if (c->render_pending && ((out_rgb && rgb_bytes > c->rgb_cap) || (out_bgr && bgr_bytes > c->bgr_cap)))
+        HIP_TRY(c, hipEventSynchronize(c->render_done));     // an earlier render may still write the old buffers
     if (out_rgb && rgb_bytes > c->rgb_cap) {
         if (c->d_rgb) (void)hipFree(c->d_rgb);
         c->d_rgb = nullptr; c->rgb_cap = 0;
@@ -859,13 +1008,39 @@ int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_b
         HIP_TRY(c, hipMalloc(&c->d_bgr, bgr_bytes));
         c->bgr_cap = bgr_bytes;
     }
-    rc = rt_render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
+    rc = render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
     if (rc != RT_OK) return rc;
-    if (out_rgb && rgb_bytes) HIP_TRY(c, hipMemcpyAsync(out_rgb, c->d_rgb, rgb_bytes, hipMemcpyDeviceToHost, c->stream));
-    if (out_bgr && bgr_bytes) HIP_TRY(c, hipMemcpyAsync(out_bgr, c->d_bgr, bgr_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, bgr_bytes)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, rgb_bytes)) != RT_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (stats) return rt_ctx_stats(c, stats);
     return RT_OK;
 }
+
+int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
+    if (!c || !o) return RT_E_INVALID;
+    return guarded(c, [&] { return render_host(c, o, out_rgb, out_bgr, stats); });
+}
+
+int rt_ctx_set_tuning(rt_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return RT_E_INVALID;
+    for (int i = 0; i < kTuneCount; ++i) {
+        if (std::strcmp(key, kTune[i].name) != 0) continue;
+        if (value < kTune[i].lo || value > kTune[i].hi)
+            return fail(c, RT_E_INVALID, std::string("tuning ") + key + " out of range");
+        c->tune[i] = value;
+        return RT_OK;
+    }
+    return fail(c, RT_E_INVALID, std::string("unknown tuning key ") + key);
+}
+
+int rt_ctx_get_tuning(const rt_ctx* c, const char* key, int64_t* value) {
+    if (!c || !key || !value) return RT_E_INVALID;
+    for (int i = 0; i < kTuneCount; ++i)
+        if (std::strcmp(key, kTune[i].name) == 0) { *value = c->tune[i]; return RT_OK; }
+    return RT_E_INVALID;
+}
+
+const char* rt_tuning_key(int index) { return index >= 0 && index < kTuneCount ? kTune[index].name : nullptr; }
 
 }  // extern "C"

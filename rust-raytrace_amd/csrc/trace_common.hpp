@@ -297,7 +297,7 @@ __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) 
 // order, i.e. the top of the tree) from an LDS copy, the rest from HBM/L2;
 // spheres and their object ids from LDS when the whole list fits, else HBM.
 struct BvhView {
-    const DevBvhNode* lnodes;
+    const float4* lnodes;        // LDS nodes, plane-major (stage_node_planes): 3 box planes then the child pairs
     int32_t nl;
     const DevBvhNode* gnodes;
     const DevSphere* sph;
@@ -310,13 +310,47 @@ struct BvhView {
     int32_t* stk;                // this wave's LDS traversal stack (camera sources)
 };
 
+// LDS copy of binary nodes [0, n), PLANE-MAJOR: box plane q (dwords 4q..4q+3
+// of DevBvhNode: lo0 hi0.x | hi0.yz lo1.xy | lo1.z hi1) of node i at
+// P[q * n + i], the child pair at ((int2*)(P + 3n))[i]; 56 B per node.  A
+// wave's lanes fetch 16-B plane q of up to 64 different nodes: in the array-of-
+// nodes layout (64-B stride) a ds_read_b128 lane group of 16 spreads over only
+// 4 of the 16 16-B bank slots, plane-major over all 16 (MI355X_MICROARCH.md,
+// LDS banking), so random node fetches conflict about 3x less.
+__host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 56u + 15u) / 16u * 16u; }
+
+template <int kThreads>
+__device__ __forceinline__ const float4* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
+    float4* P = reinterpret_cast<float4*>(lds);
+    int2* C = reinterpret_cast<int2*>(P + 3 * n);
+    for (int i = threadIdx.x; i < n; i += kThreads) {
+        const float4* q = reinterpret_cast<const float4*>(src + i);
+        P[i] = q[0];
+        P[n + i] = q[1];
+        P[2 * n + i] = q[2];
+        C[i] = make_int2(src[i].c0, src[i].c1);
+    }
+    return P;
+}
+
+__device__ __forceinline__ DevBvhNode lds_node(const float4* P, int32_t n, int32_t i) {
+    const float4 a = P[i], b = P[n + i], c = P[2 * n + i];
+    const int2 cc = reinterpret_cast<const int2*>(P + 3 * n)[i];
+    DevBvhNode nd;
+    nd.lo0[0] = a.x; nd.lo0[1] = a.y; nd.lo0[2] = a.z; nd.hi0[0] = a.w;
+    nd.hi0[1] = b.x; nd.hi0[2] = b.y; nd.lo1[0] = b.z; nd.lo1[1] = b.w;
+    nd.lo1[2] = c.x; nd.hi1[0] = c.y; nd.hi1[1] = c.z; nd.hi1[2] = c.w;
+    nd.c0 = cc.x; nd.c1 = cc.y;
+    return nd;
+}
+
 // kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS
 template <int kNodes>
 __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
     if constexpr (kNodes == 2) {
-        return v.lnodes[i];
+        return lds_node(v.lnodes, v.nl, i);
     } else if constexpr (kNodes == 1) {
-        if (i < v.nl) return v.lnodes[i];
+        if (i < v.nl) return lds_node(v.lnodes, v.nl, i);
         return v.gnodes[i];
     } else {
         return v.gnodes[i];

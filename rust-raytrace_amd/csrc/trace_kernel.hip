@@ -325,16 +325,22 @@ constexpr int kSrcBvh4P = 13;       // 4-wide BVH, LDS prefix
 // binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
 constexpr int kSrcCamL = 20;        // camera nodes + spheres in LDS
 constexpr int kSrcCamG = 21;        // camera nodes + spheres from HBM/L2
+// Shadow kernel when every light is a point light with a light-view grid: no
+// tree walk at all (so no traversal stack in scratch and no register spills),
+// spheres from LDS or HBM/L2.
+constexpr int kSrcGridL = 14;
+constexpr int kSrcGridG = 15;
 
 template <int kSrc>
 struct Src {
     static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
-    static constexpr bool bvh = kSrc >= kSrcBvhG;
+    static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
+    static constexpr bool bvh = kSrc >= kSrcBvhG && !grid;
     static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P;
     static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
                                     kSrc == kSrcCamL;
-    static constexpr bool sph_lds = kSrc == kSrcLds || all_lds;
+    static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL;
     static constexpr int nodes = all_lds ? 2 : prefix ? 1 : 0;
     static constexpr int waves = kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 ? 8 : 4;   // min waves per SIMD
 };
@@ -354,15 +360,15 @@ __host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
 template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
-    if (kSrc == kSrcLds) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
-    if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
+    if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if (kSrc == kSrcBvhP) bytes = node_planes_bytes(prefix_nodes<kSrc>(sc));
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
     if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
     if (Src<kSrc>::nodes > 0)
         bytes += Src<kSrc>::cam    ? static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode)
                  : Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
-                                   : static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
+                                   : node_planes_bytes(sc.n_bvh);
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     return (bytes + 15) / 16 * 16;
 }
@@ -375,10 +381,8 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     size_t off = 0;
     if constexpr (kSrc == kSrcBvhP) {
-        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
         const int32_t nl = prefix_nodes<kSrc>(sc);
-        for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh[i];
-        v.lnodes = ln;
+        v.lnodes = stage_node_planes<T>(sc.bvh, nl, lds);
         v.nl = nl;
         return v;
     } else if constexpr (kSrc == kSrcBvh4P) {
@@ -398,7 +402,7 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
             v.cn = lc;
             off += static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode);
         }
-    } else if constexpr (kSrc == kSrcLds) {
+    } else if constexpr (kSrc == kSrcLds || kSrc == kSrcGridL) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
@@ -410,11 +414,9 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.p4 = lp;
         off = static_cast<size_t>(n) * sizeof(DevBvh4Plane);
     } else if constexpr (Src<kSrc>::nodes > 0) {
-        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
-        for (int i = threadIdx.x; i < sc.n_bvh; i += T) ln[i] = sc.bvh[i];
-        v.lnodes = ln;
+        v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
         v.nl = sc.n_bvh;
-        off = static_cast<size_t>(sc.n_bvh) * sizeof(DevBvhNode);
+        off = node_planes_bytes(sc.n_bvh);
     }
     if constexpr (Src<kSrc>::bvh && Src<kSrc>::sph_lds) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds + off);
@@ -751,9 +753,13 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
         const int32_t hint = static_cast<int32_t>(b.ru(1)[at]);
-        const bool occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
-                                  ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
-                                  : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
+        bool occluded;
+        if constexpr (Src<kSrc>::grid)          // the host checked: every light has a grid
+            occluded = occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w);
+        else
+            occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
+                           ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
+                           : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
         occlusion_done<kShade, kFresnel>(sc, b, k, at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
@@ -1024,7 +1030,9 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
 #define RT_OCC(S, SH, FR) hipLaunchKernelGGL((wf_occlusion<S, kCount, SH, FR>), grid, block, \
                                                staged_bytes<S>(sc) + queue_lds_bytes(b.G), sb, sc, fp, b, k)
-        if (!fused) RT_OCC(kSrcO, false, false);
+        if (!fused && ws.grid_occ == 1) RT_OCC(kSrcGridL, false, false);
+        else if (!fused && ws.grid_occ == 2) RT_OCC(kSrcGridG, false, false);
+        else if (!fused) RT_OCC(kSrcO, false, false);
         else if (sc.has_fresnel) RT_OCC(kSrcO, true, true);
         else RT_OCC(kSrcO, true, false);
 #undef RT_OCC

@@ -83,7 +83,7 @@ class rt_render_opts(C.Structure):
 class rt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64),
                 ("kernel_ms", C.c_double), ("box_tests", C.c_uint64), ("sphere_tests", C.c_uint64),
-                ("shadow_box_tests", C.c_uint64), ("shadow_sphere_tests", C.c_uint64)]
+                ("shadow_box_tests", C.c_uint64), ("shadow_sphere_tests", C.c_uint64), ("traced_rays", C.c_uint64)]
 
 
 def _load():
@@ -116,8 +116,11 @@ def _load():
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
         "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
         "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
-        "rt_light_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, P(C.c_double), C.c_uint32, P(C.c_int32),
-                                               P(C.c_int32), C.c_size_t, P(C.c_int64)]),
+        "rt_light_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(C.c_double), C.c_uint32,
+                                               P(C.c_int32), P(C.c_int32), C.c_size_t, P(C.c_int64)]),
+        "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
+        "rt_ctx_get_tuning": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
+        "rt_tuning_key": (C.c_char_p, [C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -208,16 +211,17 @@ class Scene:
         _check(lib.rt_scene_from_desc(C.byref(desc), C.byref(h)))
         return cls(h.value)
 
-    def light_grid_candidates(self, light, points, cap=1 << 22):
+    def light_grid_candidates(self, light, points, cap=1 << 22, resolution=0):
         """Diagnostic (host only): for each point p, the object ids the light-view
         grid of point light `light` hands a shadow query from p (None when the
-        device tests every sphere), and (R, stored cells, list entries)."""
+        device tests every sphere), and (R, stored cells, list entries).
+        resolution: cells per face side (0 = the upload's automatic choice)."""
         pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
         n = pts.shape[0]
         counts = np.zeros(n, np.int32)
         ids = np.zeros(cap, np.int32)
         info = np.zeros(3, np.int64)
-        _check(lib.rt_light_grid_candidates(self._h, light, pts.ctypes.data_as(C.POINTER(C.c_double)), n,
+        _check(lib.rt_light_grid_candidates(self._h, light, int(resolution), pts.ctypes.data_as(C.POINTER(C.c_double)), n,
                                             counts.ctypes.data_as(C.POINTER(C.c_int32)),
                                             ids.ctypes.data_as(C.POINTER(C.c_int32)), cap,
                                             info.ctypes.data_as(C.POINTER(C.c_int64))))
@@ -278,24 +282,64 @@ def render_opts(width, height, **kw):
     return o
 
 
-class Context:
-    """One device (rt_ctx).  Mirrors the reference's main.rs render step."""
+def tuning_keys():
+    keys, i = [], 0
+    while True:
+        k = lib.rt_tuning_key(i)
+        if not k:
+            return keys
+        keys.append(k.decode())
+        i += 1
 
-    def __init__(self, device=0):
+
+def env_tuning():
+    """Tuning from RT_TUNE="key=value,key=value" (a convenience of this binding
+    for A/B tools; the library itself never reads the environment)."""
+    out = {}
+    for item in filter(None, os.environ.get("RT_TUNE", "").split(",")):
+        k, v = item.split("=")
+        out[k.strip()] = int(v)
+    return out
+
+
+class Context:
+    """One device (rt_ctx).  Mirrors the reference's main.rs render step.
+    tuning: {key: value} schedule knobs (rt_ctx_set_tuning); None = RT_TUNE."""
+
+    def __init__(self, device=0, tuning=None):
         h = C.c_void_p()
         _check(lib.rt_ctx_create(device, C.byref(h)))
         self._h = h
         self.device = device
+        for k, v in (env_tuning() if tuning is None else tuning).items():
+            self.set_tuning(k, v)
+
+    def set_tuning(self, key, value):
+        _check(lib.rt_ctx_set_tuning(self._h, key.encode(), int(value)), self._h)
+
+    def get_tuning(self, key):
+        v = C.c_int64()
+        _check(lib.rt_ctx_get_tuning(self._h, key.encode(), C.byref(v)), self._h)
+        return v.value
 
     def upload(self, scene):
         _check(lib.rt_scene_upload(self._h, scene.handle), self._h)
 
-    def render(self, opts, rgb=True, bgr=True):
+    def render(self, opts, rgb=True, bgr=True, out=None):
         """Synchronous render of opts' tile into host numpy arrays.
-        Returns (rgb float32 [tile_h, tile_w, 3] or None, bgr uint8 [tile_h, pitch] or None, stats)."""
+        Returns (rgb float32 [tile_h, tile_w, 3] or None, bgr uint8 [tile_h, pitch] or None, stats).
+        out: (rgb, bgr) arrays to reuse (either None to skip that output)."""
         pitch = opts.bgr_pitch or 3 * opts.tile_w
-        out_rgb = np.zeros((opts.tile_h, opts.tile_w, 3), np.float32) if rgb else None
-        out_bgr = np.full((opts.tile_h, pitch), 0xCD, np.uint8) if bgr else None
+        if out is not None:
+            out_rgb, out_bgr = out
+            rgb, bgr = out_rgb is not None, out_bgr is not None
+            assert not rgb or (out_rgb.dtype == np.float32 and out_rgb.size >= opts.tile_h * opts.tile_w * 3
+                               and out_rgb.flags.c_contiguous)
+            assert not bgr or (out_bgr.dtype == np.uint8 and out_bgr.size >= opts.tile_h * pitch
+                               and out_bgr.flags.c_contiguous)
+        else:
+            out_rgb = np.zeros((opts.tile_h, opts.tile_w, 3), np.float32) if rgb else None
+            out_bgr = np.full((opts.tile_h, pitch), 0xCD, np.uint8) if bgr else None
         st = rt_stats()
         rc = lib.rt_render(self._h, C.byref(opts),
                            out_rgb.ctypes.data_as(C.POINTER(C.c_float)) if rgb else None,

@@ -1,0 +1,36 @@
+"""bench.py's multi-GPU launcher on CPU: `python bench.py --gpus 2` starts two
+rank processes itself (no torchrun), forms the process group, and reports
+n_gpus as the number of distinct devices rendered on (0 here: no GPU), not
+the number of ranks.  The GPU side of the same code path runs on the box
+(`python bench.py --gpus N`)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_gpus_two_spawns_two_ranks(backend):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", backend,
+                          "--dry-run"], capture_output=True, text=True, timeout=180, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout          # rank 0 prints the one line
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2
+    assert d["n_gpus"] == d["devices_visible"] == 0
+    assert d["scaling"] == "strong"
+
+
+def test_cpu_baseline_sample_is_bounded():
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
+    import bench
+    from libraytrace import scenes
+    r = bench.cpu_sample(scenes.config3(256, 256), threads=2, budget_s=1.0, draws={})
+    assert r["rays"] > 0 and r["value"] > 0 and r["seconds"] < 10
+    assert bench.cpu_share() >= 1 and bench.cpu_model()

@@ -252,7 +252,7 @@ def test_render_without_scene_and_bad_opts():
             ctx.render(lr.render_opts(8, 8, spp=1))
         assert e.value.code == lr.RT_E_NOSCENE
         ctx.upload(lr.Scene.deserialize(scenes.config2(8, 8).to_text()))
-        for bad in (dict(max_depth=lr.RT_MAX_DEPTH_LIMIT + 1, spp=1), dict(spp=0), dict(spp=1, x0=5),
+        for bad in (dict(max_depth=lr.RT_MAX_DEPTH_LIMIT + 1, spp=1), dict(spp=1, x0=5),
                     dict(spp=1, band_stride=2, band_phase=2), dict(spp=1, bgr_pitch=3)):
             with pytest.raises(lr.RtError) as e:
                 ctx.render(lr.render_opts(8, 8, **bad))
@@ -324,13 +324,16 @@ def test_light_view_grids_adversarial_lights(gpu_ctx, algo):
     check_parity(gpu_ctx, s, algo)
 
 
-def test_light_view_grids_off_is_bit_identical(gpu_ctx, monkeypatch):
-    """RT_WF_LGRID=0 (shadow queries through the 4-wide tree) and the default
+def test_light_view_grids_off_is_bit_identical(gpu_ctx):
+    """Tuning light_grids=0 (shadow queries through the 4-wide tree) and the default
     grids give the same bytes, colours and ray counts on the 10k-sphere scene."""
     spec = scenes.config4(160, 120)
     a = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
-    monkeypatch.setenv("RT_WF_LGRID", "0")
-    b = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    gpu_ctx.set_tuning("light_grids", 0)
+    try:
+        b = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    finally:
+        gpu_ctx.set_tuning("light_grids", 1)
     assert np.array_equal(a[1], b[1])
     assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
     assert a[2].rays == b[2].rays and a[2].shadow_rays == b[2].shadow_rays
@@ -391,8 +394,136 @@ def test_kernel_times(gpu_ctx):
     # shadow queries of the lit generations 0..max_depth (none past the cut-off): the
     # plain kernel for every (record, light) pair, or the item lists from generation 1 on
     assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
-    # shading runs inside the shadow kernels (fused) unless RT_WF_FUSE=0
+    # shading runs in its own kernel unless the context is tuned fuse=1 (then inside the shadow kernels)
     assert kt["shade"][1] in (0, 2 * (gens - 1))
     assert kt["fold"][1] == 2 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
     assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested
+
+
+def _with_tuning(ctx, **kv):
+    """Context manager: set tuning keys, restore the previous values after."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def cm():
+        old = {k: ctx.get_tuning(k) for k in kv}
+        try:
+            for k, v in kv.items():
+                ctx.set_tuning(k, v)
+            yield
+        finally:
+            for k, v in old.items():
+                ctx.set_tuning(k, v)
+    return cm()
+
+
+def test_config5_workload_downscaled(gpu_ctx):
+    """BASELINE config 5's workload (100k spheres, depth 16, 2 point lights) at
+    128x96: a tree far larger than LDS (the LDS-prefix sources), the linear-scan
+    semantics of scene.rs:247-249 over 100k objects, and the raytrace.rs:33
+    cut-off after 17 levels.  Rendered as one chunk and as three chunks of 32
+    rows (tuning chunk_pixels), both against the oracle bit for bit."""
+    spec = scenes.config5(128, 96)
+    ref = ref64.render(spec, threads=min(16, os.cpu_count() or 1))
+    rgb, bgr, st = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert np.array_equal(bgr, ref["bgr"]), f"{(bgr != ref['bgr']).sum()} BGR bytes differ"
+    check_close(rgb, ref["rgb64"])
+    assert st.rays == ref["counts"]["rays"] and st.shadow_rays == ref["counts"]["shadow_rays"]
+    with _with_tuning(gpu_ctx, chunk_pixels=128 * 32):
+        rgb2, bgr2, st2 = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert np.array_equal(bgr2, bgr) and np.array_equal(rgb2.view(np.uint32), rgb.view(np.uint32))
+    assert st2.rays == st.rays and st2.shadow_rays == st.shadow_rays
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_multi_chunk_schedule_matches_oracle(gpu_ctx, lanes):
+    """The wavefront schedule over many chunks (row0 > 0), on one or two chunk
+    lanes, for a plain tile and for a banded tile (band_stride > 1, band_phase
+    > 0): bit-identical to the one-chunk render and to the oracle."""
+    spec = scenes.config3(256, 256)
+    sc = lr.Scene.deserialize(spec.to_text())
+    gpu_ctx.upload(sc)
+    layouts = [dict(tile_h=256), dict(y0=0, tile_h=80, band=8, band_stride=3, band_phase=1)]
+    for lay in layouts:
+        o = lr.render_opts(256, 256, max_depth=spec.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT, **lay)
+        one = gpu_ctx.render(o)
+        with _with_tuning(gpu_ctx, chunk_pixels=256 * 16, lanes=lanes):
+            many = gpu_ctx.render(o)
+        assert np.array_equal(many[1], one[1])
+        assert np.array_equal(many[0].view(np.uint32), one[0].view(np.uint32))
+        assert many[2].rays == one[2].rays and many[2].shadow_rays == one[2].shadow_rays
+        kw = {k: v for k, v in lay.items()}
+        ref = ref64.render(spec, **kw)
+        assert np.array_equal(many[1], ref["bgr"])
+        check_close(many[0], ref["rgb64"])
+        assert many[2].rays == ref["counts"]["rays"]
+
+
+def test_tuning_knobs_do_not_change_results(gpu_ctx):
+    """Schedule knobs (one stream, no camera tiles, workgroup-first dealing,
+    fused shading with shadow lists, other region counts) leave every bit of a
+    C3-workload frame unchanged."""
+    spec = scenes.config3(192, 160)
+    base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(regions=96),
+               dict(bstreams=1), dict(src=2, src_occ=11)]:
+        with _with_tuning(gpu_ctx, **kv):
+            got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+        assert np.array_equal(got[1], base[1]), kv
+        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), kv
+        assert got[2].rays == base[2].rays, kv
+
+
+def test_default_spp_is_the_scenes_antialias(gpu_ctx):
+    """rt_render_opts.spp = 0 (the default options) renders with the uploaded
+    scene's Options.antialias (scene.rs:191-198)."""
+    spec = scenes.config2(40, 24)
+    spec.antialias = 3
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    o = lr.render_opts(40, 24, max_depth=spec.max_depth)
+    assert o.spp == 0
+    rgb, bgr, st = gpu_ctx.render(o)
+    ref = ref64.render(spec)
+    assert np.array_equal(bgr, ref["bgr"])
+    assert st.rays == ref["counts"]["rays"]
+    assert st.traced_rays * 3 == st.rays        # centre jitter: one traced sample counted 3 times
+
+
+_TWO_STREAMS = r"""
+import sys
+sys.path[:0] = sys.argv[1:3]
+import numpy as np
+import torch                      # first: the process then uses torch's HIP runtime for both
+import libraytrace as lr
+from libraytrace import scenes
+from oracle import ref64
+spec = scenes.config3(128, 128)
+dev = torch.device("cuda", 0)
+outs = [(torch.empty((128, 128, 3), dtype=torch.float32, device=dev),
+         torch.empty((128, 384), dtype=torch.uint8, device=dev)) for _ in range(2)]
+streams = [torch.cuda.Stream(dev) for _ in range(2)]
+with lr.Context(0) as ctx:
+    ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    o = lr.render_opts(128, 128, max_depth=spec.max_depth, spp=1)
+    for _ in range(3):
+        for (a, b), s in zip(outs, streams):
+            ctx.render_device(o, a.data_ptr(), b.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+ref = ref64.render(spec)
+for a, b in outs:
+    assert np.array_equal(b.cpu().numpy(), ref["bgr"])
+print("ordered ok")
+"""
+
+
+def test_renders_on_two_streams_are_ordered():
+    """Two asynchronous renders of one context on different (torch) streams share
+    its working set; the second waits for the first on the device.
+    In a child process: torch must initialise HIP before the library does."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _TWO_STREAMS, root, os.path.join(root, "rust-raytrace_amd")],
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and "ordered ok" in out.stdout, out.stderr[-3000:]

@@ -222,6 +222,29 @@ def test_texture_load_ppm_and_bmp(tmp_path):
     assert e.value.code == lr.RT_E_UNSUPPORTED
 
 
+def test_texture_load_rejects_crafted_sizes(tmp_path):
+    """Headers whose sizes would wrap 64-bit products or overflow int32
+    are rejected before any allocation."""
+    import struct
+    cases = {
+        "huge.ppm": b"P6\n40000000000 40000000000\n255\n" + bytes(16),
+        "wide.ppm": b"P6\n4000000000 1\n255\n" + bytes(16),
+        "short.ppm": b"P6\n4 4\n255\n" + bytes(47),
+    }
+    hdr = bytearray(54)
+    hdr[0:2] = b"BM"
+    struct.pack_into("<IIiiHHI", hdr, 10, 54, 40, 4, -2 ** 31, 1, 24, 0)
+    cases["intmin.bmp"] = bytes(hdr) + bytes(64)
+    struct.pack_into("<IIiiHHI", hdr, 10, 54, 40, 2 ** 31 - 1, 2 ** 31 - 1, 1, 24, 0)
+    cases["huge.bmp"] = bytes(hdr) + bytes(64)
+    for name, data in cases.items():
+        f = tmp_path / name
+        f.write_bytes(data)
+        with pytest.raises(lr.RtError) as e:
+            lr.texture_load(str(f))
+        assert e.value.code in (lr.RT_E_IO, lr.RT_E_UNSUPPORTED), name
+
+
 def test_parse_skybox_background(tmp_path):
     faces = scenes.skybox_faces(size=6)
     paths = [str(tmp_path / f"f{k}.ppm") for k in range(6)]
@@ -239,3 +262,52 @@ def test_parse_skybox_background(tmp_path):
     sc2 = lr.Scene.deserialize(scenes.config2(8, 8).to_text())
     sc2.set_skybox(faces)
     assert sc2.desc().background_kind == lr.RT_BG_SKYBOX
+
+
+def test_parser_survives_mutated_scene_text():
+    """Random byte edits of the reference's own scene file (tests/golden/
+    test_scene.txt) never crash the parser: every result is RT_OK or RT_E_PARSE /
+    RT_E_UNSUPPORTED with a message (serialize.rs:427 returns Result).  Run under
+    ASan/UBSan by tools/san_check.sh."""
+    import random
+    text = open(os.path.join(os.path.dirname(__file__), "golden", "test_scene.txt"), "rb").read()
+    rnd = random.Random(1234)
+    alphabet = b"{}()[]:,.-+eE0123456789 \n\t/*\"abcxyzPhongSphere\x00\xff"
+    ok = bad = 0
+    for _ in range(400):
+        b = bytearray(text)
+        for _ in range(rnd.randint(1, 6)):
+            op = rnd.random()
+            i = rnd.randrange(len(b)) if b else 0
+            if op < 0.4 and b:
+                b[i] = rnd.choice(alphabet)
+            elif op < 0.7 and b:
+                del b[i:i + rnd.randint(1, 40)]
+            else:
+                b[i:i] = bytes(rnd.choice(alphabet) for _ in range(rnd.randint(1, 8)))
+        try:
+            lr.Scene.deserialize(bytes(b)).close()
+            ok += 1
+        except lr.RtError as e:
+            assert e.code in (lr.RT_E_PARSE, lr.RT_E_UNSUPPORTED, lr.RT_E_INVALID), e
+            bad += 1
+    assert ok + bad == 400 and bad > 0
+
+
+def test_light_grid_builder_extreme_spheres():
+    """The light-grid builder on spheres that are huge, tiny, non-finite, at the
+    light or enclosing it: builds, and every list query returns (ASan/UBSan run)."""
+    s = scenes.SceneSpec(width=8, height=8, max_depth=2, background=(0, 0, 0),
+                         camera={"ctor": "new", "position": (0, 0, 0), "look": (0, 0, -1), "up": (0, 1, 0),
+                                 "im_dist": 1.0})
+    m = scenes.phong((0.5, 0.5, 0.5), (0.2, 0.2, 0.2), 8.0, (0, 0, 0))
+    for c, r in [((0, 0, -5), 1.0), ((1e30, 0, 0), 1e29), ((0, 0, 0), 1e-12), ((3, 3, 3), 100.0),
+                 ((2, 2, 2), 0.5), ((-1e-300, 0, 1), 1e-300), ((5, 5, 5), 0.0)]:
+        s.sphere(c, r, m)
+    s.point_light((2, 2, 2), (1, 1, 1))
+    s.point_light((1e6, -1e6, 3), (1, 1, 1))
+    sc = lr.Scene.deserialize(s.to_text())
+    pts = np.array([[0, 0, -4], [2, 2, 2], [1e30, 0, 0], [np.inf, 0, 0], [np.nan, 1, 1], [0, 0, 0]], np.float64)
+    for li in range(2):
+        cands, info = sc.light_grid_candidates(li, pts)
+        assert len(cands) == len(pts) and info[0] > 0

@@ -53,7 +53,7 @@ def _shade_points(c, r, rng, n):
     return np.vstack([on, free])
 
 
-def _check(spec, n_points=1500, seed=0):
+def _check(spec, n_points=1500, seed=0, resolution=0):
     sc = lr.Scene.deserialize(spec.to_text())
     c, r, ids = _spheres(spec)
     rng = np.random.default_rng(seed)
@@ -66,7 +66,7 @@ def _check(spec, n_points=1500, seed=0):
         # also points right next to the light
         near = Lp + rng.normal(size=(50, 3)) * 1e-3
         allp = np.vstack([pts, near])
-        cands, info = sc.light_grid_candidates(li, allp)
+        cands, info = sc.light_grid_candidates(li, allp, resolution=resolution)
         assert info[0] > 0
         for p, cand in zip(allp, cands):
             if cand is None:            # the device tests every sphere
@@ -106,10 +106,9 @@ def test_grid_lists_every_blocker_ten_thousand_spheres():
 
 
 @pytest.mark.parametrize("R", [16, 40, 512])
-def test_grid_resolution_does_not_matter(monkeypatch, R):
-    """Any forced resolution (RT_LGRID_R) keeps every blocker listed."""
-    monkeypatch.setenv("RT_LGRID_R", str(R))
-    assert _check(scenes.config3(32, 32), n_points=600, seed=3) > 500
+def test_grid_resolution_does_not_matter(R):
+    """Any forced resolution (tuning "light_grid_res") keeps every blocker listed."""
+    assert _check(scenes.config3(32, 32), n_points=600, seed=3, resolution=R) > 500
 
 
 def test_grid_sizes_config3():

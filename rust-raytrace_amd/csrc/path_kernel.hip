@@ -312,7 +312,9 @@ __device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParam
     int L = 0;
     for (;;) {
         Col c;
-        const Hit h = nearest_bvh<false, kNodes, 0>(sc, v, ray);
+        Hit h;
+        if constexpr (kNodes == 2 && RT_TRAIL) h = nearest_bvh_trail<false>(sc, v, ray);
+        else h = nearest_bvh<false, kNodes, 0>(sc, v, ray);
         ++rays;
         Frame F;
         Ray cr;
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(kPathBlock, RT_PATH_WAVES) void path_kernel(DevScen
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     double* s_srgb = reinterpret_cast<double*>(lds);
     for (int i = threadIdx.x; i < 255; i += kPathBlock) s_srgb[i] = fp.srgb[i];
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
+    BvhView v{nullptr, 0, nullptr, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     if constexpr (kNodes == 2) {
         v.lnodes = stage_node_planes<kPathBlock>(sc.bvh, sc.n_bvh, lds + 2048);
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds + 2048 + node_planes_bytes(sc.n_bvh));

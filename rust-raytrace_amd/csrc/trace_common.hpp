@@ -210,6 +210,11 @@ constexpr int kBvhStack = 64;      // host builder bounds the depth (median spli
 #ifndef RT_PUSH_BRANCHLESS
 #define RT_PUSH_BRANCHLESS 0
 #endif
+// RT_TRAIL=1: nearest-hit queries over a tree staged whole in LDS walk it
+// without a stack (nearest_bvh_trail); 0: the scratch-stack walk (A/B builds)
+#ifndef RT_TRAIL
+#define RT_TRAIL 0
+#endif
 constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst case (bvh4_stack_need) against it
 
 // f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
@@ -299,6 +304,7 @@ __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) 
 struct BvhView {
     const float4* lnodes;        // LDS nodes, plane-major (stage_node_planes): 3 box planes then the child pairs
     int32_t nl;
+    const DevBvhNode* pnodes;    // prefix sources: nodes [0, nl) in LDS as DevBvhNode (array of nodes)
     const DevBvhNode* gnodes;
     const DevSphere* sph;
     const int32_t* obj;
@@ -312,23 +318,31 @@ struct BvhView {
 
 // LDS copy of binary nodes [0, n), PLANE-MAJOR: box plane q (dwords 4q..4q+3
 // of DevBvhNode: lo0 hi0.x | hi0.yz lo1.xy | lo1.z hi1) of node i at
-// P[q * n + i], the child pair at ((int2*)(P + 3n))[i]; 56 B per node.  A
-// wave's lanes fetch 16-B plane q of up to 64 different nodes: in the array-of-
-// nodes layout (64-B stride) a ds_read_b128 lane group of 16 spreads over only
-// 4 of the 16 16-B bank slots, plane-major over all 16 (MI355X_MICROARCH.md,
-// LDS banking), so random node fetches conflict about 3x less.
-__host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 56u + 15u) / 16u * 16u; }
+// P[q * n + i], the child pair at ((int2*)(P + 3n))[i], the parent at
+// ((int*)(C + n))[i] (-1 for the root and for nodes whose parent is outside
+// [0, n)); 60 B per node.  A wave's lanes fetch 16-B plane q of up to 64
+// different nodes: in the array-of-nodes layout (64-B stride) a ds_read_b128
+// lane group of 16 spreads over only 4 of the 16 16-B bank slots, plane-major
+// over all 16 (MI355X_MICROARCH.md, LDS banking), so random node fetches
+// conflict about 3x less.
+__host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 60u + 15u) / 16u * 16u; }
 
 template <int kThreads>
 __device__ __forceinline__ const float4* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
     float4* P = reinterpret_cast<float4*>(lds);
     int2* C = reinterpret_cast<int2*>(P + 3 * n);
+    int32_t* U = reinterpret_cast<int32_t*>(C + n);
+    for (int i = threadIdx.x; i < n; i += kThreads) U[i] = -1;
+    __syncthreads();
     for (int i = threadIdx.x; i < n; i += kThreads) {
         const float4* q = reinterpret_cast<const float4*>(src + i);
         P[i] = q[0];
         P[n + i] = q[1];
         P[2 * n + i] = q[2];
-        C[i] = make_int2(src[i].c0, src[i].c1);
+        const int32_t c0 = src[i].c0, c1 = src[i].c1;
+        C[i] = make_int2(c0, c1);
+        if (c0 >= 0 && c0 < n) U[c0] = i;          // every node has one parent: no write conflicts
+        if (c1 >= 0 && c1 < n) U[c1] = i;
     }
     return P;
 }
@@ -350,8 +364,9 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
     if constexpr (kNodes == 2) {
         return lds_node(v.lnodes, v.nl, i);
     } else if constexpr (kNodes == 1) {
-        if (i < v.nl) return lds_node(v.lnodes, v.nl, i);
-        return v.gnodes[i];
+        // one flat load from LDS or HBM/L2: the same layout on both sides, so no
+        // divergent branch (a plane-major prefix measured C4 70.8 -> 79.0 ms)
+        return *(i < v.nl ? v.pnodes + i : v.gnodes + i);
     } else {
         return v.gnodes[i];
     }
@@ -445,6 +460,90 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
             const uint64_t e = stk_pop();
             cur = stk_node(e);
             if (stk_t(e) <= tlim) break;
+        }
+    }
+}
+
+// nearest_bvh over a tree staged WHOLE in LDS, without a traversal stack.
+// The stack version keeps its deferred far children in scratch: every push is
+// a vector-memory store and every pop a load whose s_waitcnt also drains the
+// stores before it (vmcnt counts both on gfx9), a few hundred cycles per pop
+// on the traversal's critical path.  Here the state is two bits per tree
+// level in registers: `pend` bit = that level's far child is still to be
+// visited, `near1` bit = child 1 was taken first (so the far one is child 0);
+// the lowest bits belong to the deepest level, the node `up` whose child is
+// being visited.  Backtracking walks up through the LDS parent links
+// (stage_node_planes) and re-tests a pending far child's box against the
+// current tlim: the same f32 interval as when it was deferred (deterministic)
+// compared with the same bound, i.e. exactly the stack version's
+// `stk_t(e) <= tlim` cut.  Visiting order, culling and result are those of
+// nearest_bvh; the tree depth (host-bounded, kBvhStack) fits the 64 bits.
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_bvh_trail(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    const float4* P = v.lnodes;
+    const int32_t n = v.nl;
+    const int2* C = reinterpret_cast<const int2*>(P + 3 * n);
+    const int32_t* U = reinterpret_cast<const int32_t*>(C + n);
+    uint64_t pend = 0, near1 = 0;
+    int32_t up = -1;
+    int32_t cur = sc.bvh_root;
+    for (;;) {
+        if (cur >= 0) {
+            const DevBvhNode nd = lds_node(P, n, cur);
+            if constexpr (kCount) w->boxes += 2;
+            float t0, t1;
+            const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
+            const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
+            if (h0 || h1) {
+                const bool both = h0 && h1;
+                const bool go1 = both ? !(t0 <= t1) : h1;
+                pend = (pend << 1) | (both ? 1u : 0u);
+                near1 = (near1 << 1) | (go1 ? 1u : 0u);
+                up = cur;
+                cur = go1 ? nd.c1 : nd.c0;
+                continue;
+            }
+        } else {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            if constexpr (kCount) w->spheres += cnt;
+            for (int k = first; k < first + cnt; ++k) {
+                double t;
+                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                    const int32_t obj = v.obj[k];
+                    if (t < h.t || (t == h.t && obj < h.obj)) {
+                        h.t = t; h.obj = obj; h.prim = k;
+                        tlim = t_limit(t);
+                    }
+                }
+            }
+        }
+        // the subtree of up's current child is done: the deepest pending far child next
+        for (;;) {
+            if (up < 0) return h;
+            if (pend & 1u) {
+                pend ^= 1u;
+                const bool far1 = (near1 & 1u) == 0u;
+                const float4 m = P[n + up];                         // hi0.yz lo1.xy
+                const float4 e = P[(far1 ? 2 * n : 0) + up];        // far1: lo1.z hi1.xyz, else lo0.xyz hi0.x
+                const float lo[3] = {far1 ? m.z : e.x, far1 ? m.w : e.y, far1 ? e.x : e.z};
+                const float hi[3] = {far1 ? e.y : e.w, far1 ? e.z : m.x, far1 ? e.w : m.y};
+                if constexpr (kCount) ++w->boxes;
+                float tn;
+                if (box_hit(lo, hi, rb, tlim, tn)) {
+                    const int2 cc = C[up];
+                    cur = far1 ? cc.y : cc.x;
+                    break;
+                }
+            }
+            pend >>= 1;
+            near1 >>= 1;
+            up = U[up];
         }
     }
 }

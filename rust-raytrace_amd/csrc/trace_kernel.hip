@@ -34,6 +34,26 @@ namespace rtamd {
 
 __constant__ double c_srgb_avg[255];
 
+// RT_STAMP=1 (diagnostic builds only, tools/stamp_probe.py): per generation,
+// wf_nearest's wave-cycles by phase from s_memtime stamps taken after a full
+// wait, [k][0] setup (region scan + LDS staging), [1] ray load + region entry,
+// [2] traversal, [3] finish (records, rays, terminals), [4] chunks, [5] waves;
+// the counting kernels add [6] the slowest lane's and [7] all lanes' node
+// visits per chunk (divergence).  Read with rt_debug_stamps (this build only).
+#ifndef RT_STAMP
+#define RT_STAMP 0
+#endif
+#if RT_STAMP
+__device__ unsigned long long g_stamp[kMaxGenerations][8];
+#define RT_STAMP_AT(v)                                                            \
+    do {                                                                          \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
+        v = __builtin_amdgcn_s_memtime();                                         \
+    } while (0)
+#else
+#define RT_STAMP_AT(v) ((void)0)
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;                 // 4 waves
@@ -361,7 +381,7 @@ template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
-    if (kSrc == kSrcBvhP) bytes = node_planes_bytes(prefix_nodes<kSrc>(sc));
+    if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
     if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
@@ -378,11 +398,13 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
 template <int kSrc>
 __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
-    BvhView v{nullptr, 0, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
+    BvhView v{nullptr, 0, nullptr, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     size_t off = 0;
     if constexpr (kSrc == kSrcBvhP) {
+        DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
         const int32_t nl = prefix_nodes<kSrc>(sc);
-        v.lnodes = stage_node_planes<T>(sc.bvh, nl, lds);
+        for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh[i];
+        v.pnodes = ln;
         v.nl = nl;
         return v;
     } else if constexpr (kSrc == kSrcBvh4P) {
@@ -433,6 +455,8 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
+    // the whole tree in LDS: the stackless walk (no scratch stack, RT_TRAIL=0 restores the stack)
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_TRAIL) return nearest_bvh_trail<kCount>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
@@ -610,6 +634,8 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
 template <int kSrc, bool kCam, bool kCount, bool kFresnel, bool kLists>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    [[maybe_unused]] unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, acc[6] = {0, 0, 0, 0, 0, 0};
+    RT_STAMP_AT(st0);
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
     if (threadIdx.x < kQueueCounters) ql.count[threadIdx.x] = 0;
     uint32_t n;
@@ -626,10 +652,14 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     }
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();                                       // publishes the LDS staging and counters
+    RT_STAMP_AT(st1);
+    acc[0] = st1 - st0;
     Work w;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
     const size_t rbase = static_cast<size_t>(k) * b.qcap + obase;
     RT_FOR_CHUNKS(b, n, j) {
+        RT_STAMP_AT(st0);
+        [[maybe_unused]] const uint32_t visits0 = w.boxes;
         Ray r{};
         double sig = 0.0;
         uint32_t p = 0;
@@ -652,6 +682,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
                 live = true;
             }
         }
+        RT_STAMP_AT(st1);
         if constexpr (Src<kSrc>::cam) {                 // whole wave: one pixel tile
             float tx0, ty0, tx1, ty1;
             tile_rect(fp, b, j >> 6, tx0, ty0, tx1, ty1);
@@ -660,8 +691,27 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         if (live) {
             if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         }
+        RT_STAMP_AT(st2);
         finish_nearest<kCam, kFresnel, kLists>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
+        RT_STAMP_AT(st3);
+#if RT_STAMP
+        acc[1] += st1 - st0; acc[2] += st2 - st1; acc[3] += st3 - st2; acc[4] += 1;
+        if constexpr (kCount) {
+            unsigned long long mx = (w.boxes - visits0) / 2, sm = mx;
+            for (int off = 32; off > 0; off >>= 1) {
+                mx = max(mx, static_cast<unsigned long long>(__shfl_xor(mx, off, 64)));
+                sm += __shfl_xor(sm, off, 64);
+            }
+            if ((threadIdx.x & 63) == 0) { atomicAdd(&g_stamp[k][6], mx); atomicAdd(&g_stamp[k][7], sm); }
+        }
+#endif
     }
+#if RT_STAMP
+    if ((threadIdx.x & 63) == 0) {
+        for (int q = 0; q < 5; ++q) atomicAdd(&g_stamp[k][q], acc[q]);
+        atomicAdd(&g_stamp[k][5], 1ull);
+    }
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         b.rs()[k * b.G + blockIdx.x] = ql.count[0];
@@ -1108,6 +1158,21 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     if (ws.ma && (e = ws.ma->mark(s, kKfTally)) != hipSuccess) return e;
     return hipGetLastError();
 }
+
+#if RT_STAMP
+}  // namespace rtamd
+extern "C" int rt_debug_stamps(unsigned long long* out, int n, int reset) {
+    const size_t bytes = sizeof(unsigned long long) * static_cast<size_t>(n < 8 * rtamd::kMaxGenerations ? n : 8 * rtamd::kMaxGenerations);
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_stamp), bytes) != hipSuccess) return -3;
+    if (reset) {
+        static unsigned long long zero[rtamd::kMaxGenerations][8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamp), zero, sizeof zero) != hipSuccess) return -3;
+    }
+    return 0;
+}
+namespace rtamd {
+#endif
 
 hipError_t upload_srgb_table(const double* avg255) {
     return hipMemcpyToSymbol(HIP_SYMBOL(c_srgb_avg), avg255, 255 * sizeof(double));

@@ -312,9 +312,7 @@ __device__ Col trace_path(const DevScene& sc, const BvhView& v, const FrameParam
     int L = 0;
     for (;;) {
         Col c;
-        Hit h;
-        if constexpr (kNodes == 2 && RT_TRAIL) h = nearest_bvh_trail<false>(sc, v, ray);
-        else h = nearest_bvh<false, kNodes, 0>(sc, v, ray);
+        const Hit h = nearest_bvh<false, kNodes, 0>(sc, v, ray);
         ++rays;
         Frame F;
         Ray cr;

@@ -122,7 +122,19 @@ __device__ __forceinline__ bool plane_t(const DevPlane& p, const Ray& r, double&
 // spheres = exact quadratic tests.
 struct Work {
     uint32_t boxes = 0, spheres = 0;
+#if RT_STAMP
+    unsigned long long cyc[3] = {0, 0, 0};     // RT_STAMP builds: nearest_bvh_bl's descend / leaf / pop loops
+#endif
 };
+#if RT_STAMP
+#define RT_WSTAMP(v)                                                              \
+    do {                                                                          \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
+        v = __builtin_amdgcn_s_memtime();                                         \
+    } while (0)
+#else
+#define RT_WSTAMP(v) ((void)0)
+#endif
 
 template <bool kCount = false, class SpherePtr>
 __device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, const Ray& r, Work* w = nullptr) {
@@ -210,11 +222,6 @@ constexpr int kBvhStack = 64;      // host builder bounds the depth (median spli
 #ifndef RT_PUSH_BRANCHLESS
 #define RT_PUSH_BRANCHLESS 0
 #endif
-// RT_TRAIL=1: nearest-hit queries over a tree staged whole in LDS walk it
-// without a stack (nearest_bvh_trail); 0: the scratch-stack walk (A/B builds)
-#ifndef RT_TRAIL
-#define RT_TRAIL 0
-#endif
 constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst case (bvh4_stack_need) against it
 
 // f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
@@ -268,6 +275,13 @@ __device__ __forceinline__ bool box_hit(const float* lo, const float* hi, const 
     tn = widen_lo(tn);
     tf = widen_hi(tf);
     tnear = tn;
+    // tn <= tf && tf >= 0 && tn <= tlim, as one compare: every caller's tlim is
+    // >= 0 (+inf or t_limit of a positive t), so max(tn, 0) <= min(tf, tlim)
+    // states exactly the same three conditions (fewer compares and mask ANDs)
+#ifndef RT_BOXFOLD
+#define RT_BOXFOLD 1
+#endif
+    if (RT_BOXFOLD) return fmaxf(tn, 0.0f) <= fminf(tf, tlim);
     return tn <= tf && tf >= 0.0f && tn <= tlim;
 }
 
@@ -318,31 +332,23 @@ struct BvhView {
 
 // LDS copy of binary nodes [0, n), PLANE-MAJOR: box plane q (dwords 4q..4q+3
 // of DevBvhNode: lo0 hi0.x | hi0.yz lo1.xy | lo1.z hi1) of node i at
-// P[q * n + i], the child pair at ((int2*)(P + 3n))[i], the parent at
-// ((int*)(C + n))[i] (-1 for the root and for nodes whose parent is outside
-// [0, n)); 60 B per node.  A wave's lanes fetch 16-B plane q of up to 64
-// different nodes: in the array-of-nodes layout (64-B stride) a ds_read_b128
-// lane group of 16 spreads over only 4 of the 16 16-B bank slots, plane-major
-// over all 16 (MI355X_MICROARCH.md, LDS banking), so random node fetches
-// conflict about 3x less.
-__host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 60u + 15u) / 16u * 16u; }
+// P[q * n + i], the child pair at ((int2*)(P + 3n))[i]; 56 B per node.  A
+// wave's lanes fetch 16-B plane q of up to 64 different nodes: in the array-of-
+// nodes layout (64-B stride) a ds_read_b128 lane group of 16 spreads over only
+// 4 of the 16 16-B bank slots, plane-major over all 16 (MI355X_MICROARCH.md,
+// LDS banking), so random node fetches conflict about 3x less.
+__host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 56u + 15u) / 16u * 16u; }
 
 template <int kThreads>
 __device__ __forceinline__ const float4* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
     float4* P = reinterpret_cast<float4*>(lds);
     int2* C = reinterpret_cast<int2*>(P + 3 * n);
-    int32_t* U = reinterpret_cast<int32_t*>(C + n);
-    for (int i = threadIdx.x; i < n; i += kThreads) U[i] = -1;
-    __syncthreads();
     for (int i = threadIdx.x; i < n; i += kThreads) {
         const float4* q = reinterpret_cast<const float4*>(src + i);
         P[i] = q[0];
         P[n + i] = q[1];
         P[2 * n + i] = q[2];
-        const int32_t c0 = src[i].c0, c1 = src[i].c1;
-        C[i] = make_int2(c0, c1);
-        if (c0 >= 0 && c0 < n) U[c0] = i;          // every node has one parent: no write conflicts
-        if (c1 >= 0 && c1 < n) U[c1] = i;
+        C[i] = make_int2(src[i].c0, src[i].c1);
     }
     return P;
 }
@@ -464,52 +470,41 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     }
 }
 
-// nearest_bvh over a tree staged WHOLE in LDS, without a traversal stack.
-// The stack version keeps its deferred far children in scratch: every push is
-// a vector-memory store and every pop a load whose s_waitcnt also drains the
-// stores before it (vmcnt counts both on gfx9), a few hundred cycles per pop
-// on the traversal's critical path.  Here the state is two bits per tree
-// level in registers: `pend` bit = that level's far child is still to be
-// visited, `near1` bit = child 1 was taken first (so the far one is child 0);
-// the lowest bits belong to the deepest level, the node `up` whose child is
-// being visited.  Backtracking walks up through the LDS parent links
-// (stage_node_planes) and re-tests a pending far child's box against the
-// current tlim: the same f32 interval as when it was deferred (deterministic)
-// compared with the same bound, i.e. exactly the stack version's
-// `stk_t(e) <= tlim` cut.  Visiting order, culling and result are those of
-// nearest_bvh; the tree depth (host-bounded, kBvhStack) fits the 64 bits.
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_bvh_trail(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+// nearest_bvh with the inner-node step written branch-light (RT_NEAR_BL=1):
+// a wave descends inner nodes in one tight loop whose only divergent
+// statement is the masked push of the far child, then tests its leaf, then
+// pops past the entries the current best rules out.  Same visiting order,
+// culling and result as nearest_bvh.
+#ifndef RT_NEAR_BL
+#define RT_NEAR_BL 1
+#endif
+template <bool kCount = false, int kNodes = 0>
+__device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const double a2 = 2.0 * a, a4 = 4.0 * a;
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    const float4* P = v.lnodes;
-    const int32_t n = v.nl;
-    const int2* C = reinterpret_cast<const int2*>(P + 3 * n);
-    const int32_t* U = reinterpret_cast<const int32_t*>(C + n);
-    uint64_t pend = 0, near1 = 0;
-    int32_t up = -1;
+    constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
+    uint64_t stk[kBvhStack];
+    int sp = 0;
     int32_t cur = sc.bvh_root;
+    [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     for (;;) {
-        if (cur >= 0) {
-            const DevBvhNode nd = lds_node(P, n, cur);
+        RT_WSTAMP(q0);
+        while (cur >= 0) {
+            const DevBvhNode nd = fetch_node<kNodes>(v, cur);
             if constexpr (kCount) w->boxes += 2;
             float t0, t1;
             const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
             const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
-            if (h0 || h1) {
-                const bool both = h0 && h1;
-                const bool go1 = both ? !(t0 <= t1) : h1;
-                pend = (pend << 1) | (both ? 1u : 0u);
-                near1 = (near1 << 1) | (go1 ? 1u : 0u);
-                up = cur;
-                cur = go1 ? nd.c1 : nd.c0;
-                continue;
-            }
-        } else {
+            const bool first0 = t0 <= t1;
+            if (h0 && h1) stk[sp++] = stk_entry(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
+            cur = (h0 && (!h1 || first0)) ? nd.c0 : (h1 ? nd.c1 : kNone);
+        }
+        RT_WSTAMP(q1);
+        if (cur != kNone) {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
@@ -523,28 +518,17 @@ __device__ __forceinline__ Hit nearest_bvh_trail(const DevScene& sc, const BvhVi
                 }
             }
         }
-        // the subtree of up's current child is done: the deepest pending far child next
-        for (;;) {
-            if (up < 0) return h;
-            if (pend & 1u) {
-                pend ^= 1u;
-                const bool far1 = (near1 & 1u) == 0u;
-                const float4 m = P[n + up];                         // hi0.yz lo1.xy
-                const float4 e = P[(far1 ? 2 * n : 0) + up];        // far1: lo1.z hi1.xyz, else lo0.xyz hi0.x
-                const float lo[3] = {far1 ? m.z : e.x, far1 ? m.w : e.y, far1 ? e.x : e.z};
-                const float hi[3] = {far1 ? e.y : e.w, far1 ? e.z : m.x, far1 ? e.w : m.y};
-                if constexpr (kCount) ++w->boxes;
-                float tn;
-                if (box_hit(lo, hi, rb, tlim, tn)) {
-                    const int2 cc = C[up];
-                    cur = far1 ? cc.y : cc.x;
-                    break;
-                }
-            }
-            pend >>= 1;
-            near1 >>= 1;
-            up = U[up];
+        RT_WSTAMP(q2);
+        cur = kNone;
+        while (sp > 0) {
+            const uint64_t e = stk[--sp];
+            if (stk_t(e) <= tlim) { cur = stk_node(e); break; }
         }
+        RT_WSTAMP(q3);
+#if RT_STAMP
+        w->cyc[0] += q1 - q0; w->cyc[1] += q2 - q1; w->cyc[2] += q3 - q2;
+#endif
+        if (cur == kNone) return h;
     }
 }
 

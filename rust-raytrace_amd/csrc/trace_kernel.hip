@@ -44,7 +44,7 @@ __constant__ double c_srgb_avg[255];
 #define RT_STAMP 0
 #endif
 #if RT_STAMP
-__device__ unsigned long long g_stamp[kMaxGenerations][8];
+__device__ unsigned long long g_stamp[kMaxGenerations][12];
 #define RT_STAMP_AT(v)                                                            \
     do {                                                                          \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
@@ -455,8 +455,7 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
-    // the whole tree in LDS: the stackless walk (no scratch stack, RT_TRAIL=0 restores the stack)
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_TRAIL) return nearest_bvh_trail<kCount>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL) return nearest_bvh_bl<kCount, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
@@ -534,6 +533,8 @@ __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
 }
 
 __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + kQueueCounters) * 4u; }
+
+
 
 // What follows a nearest hit (all 64 lanes call it; `live` lanes carry a
 // query): a miss or a cut-off ends the chain at once (terminal colour; a
@@ -707,9 +708,13 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
 #endif
     }
 #if RT_STAMP
+    for (int q = 0; q < 3; ++q)               // the wave's time in each loop = its longest-running lane's
+        for (int off = 32; off > 0; off >>= 1)
+            w.cyc[q] = max(w.cyc[q], static_cast<unsigned long long>(__shfl_xor(w.cyc[q], off, 64)));
     if ((threadIdx.x & 63) == 0) {
         for (int q = 0; q < 5; ++q) atomicAdd(&g_stamp[k][q], acc[q]);
         atomicAdd(&g_stamp[k][5], 1ull);
+        for (int q = 0; q < 3; ++q) atomicAdd(&g_stamp[k][8 + q], w.cyc[q]);
     }
 #endif
     __syncthreads();
@@ -1162,11 +1167,11 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
 #if RT_STAMP
 }  // namespace rtamd
 extern "C" int rt_debug_stamps(unsigned long long* out, int n, int reset) {
-    const size_t bytes = sizeof(unsigned long long) * static_cast<size_t>(n < 8 * rtamd::kMaxGenerations ? n : 8 * rtamd::kMaxGenerations);
+    const size_t bytes = sizeof(unsigned long long) * static_cast<size_t>(n < 12 * rtamd::kMaxGenerations ? n : 12 * rtamd::kMaxGenerations);
     if (hipDeviceSynchronize() != hipSuccess) return -3;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_stamp), bytes) != hipSuccess) return -3;
     if (reset) {
-        static unsigned long long zero[rtamd::kMaxGenerations][8];
+        static unsigned long long zero[rtamd::kMaxGenerations][12];
         if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamp), zero, sizeof zero) != hipSuccess) return -3;
     }
     return 0;

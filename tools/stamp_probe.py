@@ -28,7 +28,7 @@ def main():
     lib = lr.lib
     lib.rt_debug_stamps.restype = C.c_int
     lib.rt_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-    G, F = 34, 8
+    G, F = 34, 12
     buf = (C.c_ulonglong * (G * F))()
 
     def read(reset):
@@ -57,15 +57,15 @@ def main():
     torch.cuda.synchronize()
     counted = read(True)
     print(f"{a.config} {tune or ''}: cycles per chunk (64 rays) by phase; setup per wave; node visits per chunk")
-    print(" gen  chunks   waves  setup/wave  load/chunk  trav/chunk  fin/chunk   maxlane  meanlane  div")
+    print(" gen  chunks   waves  setup/wave  load/chunk  trav/chunk  fin/chunk   maxlane  meanlane  div   desc/ch   leaf/ch    pop/ch")
     for g in range(G):
-        st, ld, tr, fi, ch, wv, _, _ = plain[g]
+        st, ld, tr, fi, ch, wv, _, _, de, le, po, _ = plain[g]
         mx, sm = counted[g][6], counted[g][7]
         if ch == 0:
             continue
         cc = counted[g][4] or 1
         print(f"{g:4d} {ch:7d} {wv:7d} {st / max(wv, 1):11.0f} {ld / ch:11.0f} {tr / ch:11.0f} {fi / ch:10.0f} "
-              f"{mx / cc:9.1f} {sm / cc / 64:9.1f} {mx / max(sm / 64, 1):5.2f}")
+              f"{mx / cc:9.1f} {sm / cc / 64:9.1f} {mx / max(sm / 64, 1):5.2f} {de / ch:9.0f} {le / ch:9.0f} {po / ch:9.0f}")
     ctx.close()
 
 

@@ -316,7 +316,7 @@ __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) 
 // order, i.e. the top of the tree) from an LDS copy, the rest from HBM/L2;
 // spheres and their object ids from LDS when the whole list fits, else HBM.
 struct BvhView {
-    const float4* lnodes;        // LDS nodes, plane-major (stage_node_planes): 3 box planes then the child pairs
+    const float2* lnodes;        // LDS nodes, axis-pair-major (stage_node_planes): 6 bound-pair arrays then the child pairs
     int32_t nl;
     const DevBvhNode* pnodes;    // prefix sources: nodes [0, nl) in LDS as DevBvhNode (array of nodes)
     const DevBvhNode* gnodes;
@@ -330,36 +330,40 @@ struct BvhView {
     int32_t* stk;                // this wave's LDS traversal stack (camera sources)
 };
 
-// LDS copy of binary nodes [0, n), PLANE-MAJOR: box plane q (dwords 4q..4q+3
-// of DevBvhNode: lo0 hi0.x | hi0.yz lo1.xy | lo1.z hi1) of node i at
-// P[q * n + i], the child pair at ((int2*)(P + 3n))[i]; 56 B per node.  A
-// wave's lanes fetch 16-B plane q of up to 64 different nodes: in the array-of-
-// nodes layout (64-B stride) a ds_read_b128 lane group of 16 spreads over only
-// 4 of the 16 16-B bank slots, plane-major over all 16 (MI355X_MICROARCH.md,
-// LDS banking), so random node fetches conflict about 3x less.
+// LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
+// bounds of the two children of node i as one pair at L[(2a) * n + i] and
+// the hi_a bounds at L[(2a + 1) * n + i] (float2), the child pair at
+// ((int2*)(L + 6n))[i]; 56 B per node.  A ray reads only the pairs its slab
+// test needs: per axis the NEAR pair (lo when 1/d_a >= 0, else hi) and the
+// FAR pair, both children at once (nearest_bvh_bl), and every 8-B read of a
+// wave spreads over all 32 8-B bank slots (the pair arrays have an 8-B stride).
 __host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 56u + 15u) / 16u * 16u; }
 
 template <int kThreads>
-__device__ __forceinline__ const float4* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
-    float4* P = reinterpret_cast<float4*>(lds);
-    int2* C = reinterpret_cast<int2*>(P + 3 * n);
+__device__ __forceinline__ const float2* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
+    float2* L = reinterpret_cast<float2*>(lds);
+    int2* C = reinterpret_cast<int2*>(L + 6 * n);
     for (int i = threadIdx.x; i < n; i += kThreads) {
-        const float4* q = reinterpret_cast<const float4*>(src + i);
-        P[i] = q[0];
-        P[n + i] = q[1];
-        P[2 * n + i] = q[2];
-        C[i] = make_int2(src[i].c0, src[i].c1);
+        const DevBvhNode nd = src[i];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            L[(2 * a) * n + i] = make_float2(nd.lo0[a], nd.lo1[a]);
+            L[(2 * a + 1) * n + i] = make_float2(nd.hi0[a], nd.hi1[a]);
+        }
+        C[i] = make_int2(nd.c0, nd.c1);
     }
-    return P;
+    return L;
 }
 
-__device__ __forceinline__ DevBvhNode lds_node(const float4* P, int32_t n, int32_t i) {
-    const float4 a = P[i], b = P[n + i], c = P[2 * n + i];
-    const int2 cc = reinterpret_cast<const int2*>(P + 3 * n)[i];
+__device__ __forceinline__ DevBvhNode lds_node(const float2* L, int32_t n, int32_t i) {
     DevBvhNode nd;
-    nd.lo0[0] = a.x; nd.lo0[1] = a.y; nd.lo0[2] = a.z; nd.hi0[0] = a.w;
-    nd.hi0[1] = b.x; nd.hi0[2] = b.y; nd.lo1[0] = b.z; nd.lo1[1] = b.w;
-    nd.lo1[2] = c.x; nd.hi1[0] = c.y; nd.hi1[1] = c.z; nd.hi1[2] = c.w;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float2 lo = L[(2 * a) * n + i], hi = L[(2 * a + 1) * n + i];
+        nd.lo0[a] = lo.x; nd.lo1[a] = lo.y;
+        nd.hi0[a] = hi.x; nd.hi1[a] = hi.y;
+    }
+    const int2 cc = reinterpret_cast<const int2*>(L + 6 * n)[i];
     nd.c0 = cc.x; nd.c1 = cc.y;
     return nd;
 }
@@ -491,17 +495,49 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     int sp = 0;
     int32_t cur = sc.bvh_root;
     [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    // whole tree in LDS: per axis the array of NEAR bound pairs (lo when 1/d >= 0,
+    // else hi) and of FAR pairs.  fma(v, 1/d, -o/d) is monotone in v for a fixed
+    // ray (1/d != 0), so fma(near) = min(fma(lo), fma(hi)) exactly: box_hit's
+    // interval, without its six min/max per child.
+    [[maybe_unused]] const float2 *nxa = nullptr, *fxa = nullptr, *nya = nullptr, *fya = nullptr, *nza = nullptr,
+                                  *fza = nullptr;
+    [[maybe_unused]] const int2* ca = nullptr;
+    if constexpr (kNodes == 2) {
+        const float2* L = v.lnodes;
+        const int32_t n = v.nl;
+        nxa = L + (rb.ix >= 0.0f ? 0 : n); fxa = L + (rb.ix >= 0.0f ? n : 0);
+        nya = L + 2 * n + (rb.iy >= 0.0f ? 0 : n); fya = L + 2 * n + (rb.iy >= 0.0f ? n : 0);
+        nza = L + 4 * n + (rb.iz >= 0.0f ? 0 : n); fza = L + 4 * n + (rb.iz >= 0.0f ? n : 0);
+        ca = reinterpret_cast<const int2*>(L + 6 * n);
+    }
     for (;;) {
         RT_WSTAMP(q0);
         while (cur >= 0) {
-            const DevBvhNode nd = fetch_node<kNodes>(v, cur);
-            if constexpr (kCount) w->boxes += 2;
             float t0, t1;
-            const bool h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
-            const bool h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
+            bool h0, h1;
+            int32_t c0, c1;
+            if constexpr (kNodes == 2) {
+                const float2 nx = nxa[cur], fx = fxa[cur], ny = nya[cur], fy = fya[cur], nz = nza[cur], fz = fza[cur];
+                const int2 cc = ca[cur];
+                t0 = widen_lo(fmaxf(fmaxf(slab_t(nx.x, rb.ix, rb.nox), slab_t(ny.x, rb.iy, rb.noy)), slab_t(nz.x, rb.iz, rb.noz)));
+                t1 = widen_lo(fmaxf(fmaxf(slab_t(nx.y, rb.ix, rb.nox), slab_t(ny.y, rb.iy, rb.noy)), slab_t(nz.y, rb.iz, rb.noz)));
+                const float f0 = widen_hi(fminf(fminf(slab_t(fx.x, rb.ix, rb.nox), slab_t(fy.x, rb.iy, rb.noy)), slab_t(fz.x, rb.iz, rb.noz)));
+                const float f1 = widen_hi(fminf(fminf(slab_t(fx.y, rb.ix, rb.nox), slab_t(fy.y, rb.iy, rb.noy)), slab_t(fz.y, rb.iz, rb.noz)));
+                h0 = fmaxf(t0, 0.0f) <= fminf(f0, tlim);           // box_hit's folded test
+                h1 = fmaxf(t1, 0.0f) <= fminf(f1, tlim);
+                c0 = cc.x;
+                c1 = cc.y;
+            } else {
+                const DevBvhNode nd = fetch_node<kNodes>(v, cur);
+                h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);
+                h1 = box_hit(nd.lo1, nd.hi1, rb, tlim, t1);
+                c0 = nd.c0;
+                c1 = nd.c1;
+            }
+            if constexpr (kCount) w->boxes += 2;
             const bool first0 = t0 <= t1;
-            if (h0 && h1) stk[sp++] = stk_entry(first0 ? nd.c1 : nd.c0, first0 ? t1 : t0);
-            cur = (h0 && (!h1 || first0)) ? nd.c0 : (h1 ? nd.c1 : kNone);
+            if (h0 && h1) stk[sp++] = stk_entry(first0 ? c1 : c0, first0 ? t1 : t0);
+            cur = (h0 && (!h1 || first0)) ? c0 : (h1 ? c1 : kNone);
         }
         RT_WSTAMP(q1);
         if (cur != kNone) {

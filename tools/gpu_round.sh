@@ -30,4 +30,10 @@ fatal $? bench_c1; tail -1 $O/bench_c1.log | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c1 -o run --output-format csv -- \
     python3 bench.py --config c1 --no-cpu > $O/prof_c1.log 2>&1
 fatal $? rocprof_c1
+timeout -k 10 400 python bench.py --config c4 > $O/bench_c4.log 2>&1
+fatal $? bench_c4; tail -1 $O/bench_c4.log | cut -c1-200
+timeout -k 10 600 python bench.py --config c5 --steps 3 --warmup 1 > $O/bench_c5.log 2>&1
+fatal $? bench_c5; tail -1 $O/bench_c5.log | cut -c1-200
+VARIANTS="single:RT_TUNE=split=0" bash tools/gpu_timeline.sh > $O/tl.log 2>&1
+fatal $? timeline_single; cp gpurun_out/tl_single.txt $O/frame_timeline_single.txt
 echo done

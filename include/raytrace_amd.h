@@ -256,7 +256,7 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 
 /* Schedule tuning of a context (A/B measurement; the defaults are the measured
  * best).  Keys (rt_tuning_key(i) for i = 0, 1, ... until NULL):
- * chunk_pixels (wavefront chunk cap), bvh_leaf, light_grids, light_grid_res
+ * chunk_pixels (wavefront chunk cap, 0: an 80 GB working set), bvh_leaf, light_grids, light_grid_res
  * (these three take effect at the next rt_scene_upload), src, src_occ,
  * prefix_kb, prefix4_kb, lanes, stagger_gen, regions, split, bstreams, fuse,
  * lists, cam, deal, spread_below, lists0, path_group, cu_mask, prio, verbose,

@@ -38,7 +38,7 @@ struct TuneDef {
 };
 // -1 in src / src_occ / cam: chosen per scene
 constexpr TuneDef kTune[kTuneCount] = {
-    {"chunk_pixels", 1 << 25, 64, INT32_MAX},   // wavefront chunk cap: ~17 GB of working set at depth 8
+    {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what kWfBudget of working set holds at the depth)
     {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
     {"light_grids", 1, 0, 1},                    // light-view grids for point-light shadow queries
     {"light_grid_res", 0, 0, 4096},              // 0: from the median sphere's angular size
@@ -58,7 +58,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"spread_below", 0, 0, INT32_MAX},           // queues below this size are dealt workgroup-first
     {"lists0", 0, 0, 1},                         // shadow lists from generation 0
     {"path_group", 0, 0, 64},                    // path kernel: lanes per pixel (0: auto)
-    {"cu_mask", 1, 0, 1},                        // b streams CU-masked (own hardware queue)
+    {"cu_mask", 1, 0, 4},                        // b streams CU-masked (own hardware queue): 1 every CU, 2/3/4 only 3/4, 1/2, 1/4 of them
     {"prio", 0, 0, 1},                           // nearest-hit chain on a high-priority stream
     {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
@@ -168,6 +168,7 @@ static_assert(kMatPhong == RT_MAT_PHONG && kMatFresnel == RT_MAT_FRESNEL && kMat
 static_assert(kLightArea == RT_LIGHT_AREA, "DevLight::kind mirrors rt_light_kind");
 // LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
 constexpr size_t kLdsBudget = 72 * 1024;
+constexpr uint64_t kWfBudget = 80ull << 30;     // default wavefront working set per lane (of 288 GB HBM)
 
 // The b streams need hardware queues of their own: HIP deals streams over a
 // few shared queues (GPU_MAX_HW_QUEUES), and two streams on one queue run
@@ -176,7 +177,9 @@ constexpr size_t kLdsBudget = 72 * 1024;
 // firmware scheduler, measurably slowing the others.
 int ensure_bstreams(rt_ctx* c, rt_ctx::Lane& M, int nb) {
     std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
-    for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    const int keep = 5 - static_cast<int>(std::max<int64_t>(1, c->t(kTuneCuMask)));   // of every 4 CUs
+    for (int cu = 0; cu < c->n_cu; ++cu)
+        if (cu % 4 < keep) mask[cu / 32] |= 1u << (cu % 32);
     while (static_cast<int>(M.sb.size()) < nb) {
         hipStream_t s = nullptr;
         if (c->t(kTuneCuMask) == 0 ||
@@ -726,7 +729,16 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
         // (balanced: a frame slightly over the cap becomes two halves, not a full chunk plus a
         // sliver that pays every generation's launch latency again)
-        uint32_t chunk_rows = std::max<uint32_t>(8, (static_cast<uint32_t>(c->t(kTuneChunkPixels)) / o->tile_w) / 8 * 8);
+        // default chunk cap: the pixels whose working set (ensure_wf: queues, one shade-record
+        // array and one level array per lit generation, terminals) fits kWfBudget, e.g. 69 M px
+        // at depth 8 (C4's 8192^2 frame in one chunk: 62.8 vs 63.9 ms as two) and 39 M px at depth 16
+        uint64_t cap_px = static_cast<uint64_t>(c->t(kTuneChunkPixels));
+        if (cap_px == 0) {
+            const uint64_t levels = o->max_depth + 1ull;
+            const uint64_t per_px = 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * 4;
+            cap_px = std::max<uint64_t>(1ull << 20, kWfBudget / per_px);
+        }
+        uint32_t chunk_rows = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(cap_px / o->tile_w, UINT32_MAX) / 8 * 8));
         chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
         const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
         chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);

@@ -7,8 +7,16 @@ f64 arithmetic, f32 RGB + sRGB BGR written to HBM.  The scene is uploaded once
 (inputs resident in HBM before timing); output stays in HBM (the PCIe copy and
 the host gather are reported beside `value`, never in it).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--steps K] [--warmup W]            (headline: C3, one GPU)
+    python bench.py --gpus N [--steps K] [--warmup W]   (scaling curve: C4 tiled over N GPUs)
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+Configs (BASELINE.json): without --gpus the line is the headline, C3 (4096²,
+1000 spheres, depth 8) on one GPU.  With --gpus N (any N, 1 included) the
+default is BASELINE config 4, the scaling-curve configuration: 8192², 10k
+spheres, depth 8, ONE image tiled across the N GPUs (strong scaling), so
+the N = 1, 2, 4, 8 lines of a scaling run measure the same workload.
+--config overrides either (--config c3 --gpus N: C3's strong-scaling curve).
 
 Multi-GPU: run as plain `python bench.py --gpus N` the script starts N rank
 processes itself (before anything touches a GPU), one device each; under
@@ -50,10 +58,11 @@ BAND = 16
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (one rank each); given, the default config is c4, BASELINE's scaling curve")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", default="c3", choices=["c1", "c3", "c4", "c5"],
+    p.add_argument("--config", default=None, choices=["c1", "c3", "c4", "c5"],
                    help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16; "
                         "c1 test_scene.txt 256^2, 1024 random AA samples, depth 1 (path kernel)")
     p.add_argument("--spp", type=int, default=0, help="c1: AA samples (default: the scene's 1024)")
@@ -83,7 +92,11 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: start the ranks, form the process group, report the "
                         "world and the devices seen, render nothing")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.config is None:
+        a.config = "c4" if a.gpus is not None else "c3"
+    a.gpus = a.gpus if a.gpus is not None else 1
+    return a
 
 
 # ---------------------------------------------------------------- launcher
@@ -323,7 +336,8 @@ def main():
         n_gpus = distinct_devices()
         if rank == 0:
             print(json.dumps({"dry_run": True, "ranks": world, "n_gpus": n_gpus, "devices_visible": n_dev,
-                              "scaling": args.scaling, "backend": args.dist_backend}), flush=True)
+                              "scaling": args.scaling, "backend": args.dist_backend, "config": args.config}),
+                  flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -489,7 +503,9 @@ def main():
         else:
             workload = (f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
                         f"depth {args.depth}, {spp} spp centre jitter (seed {cfg[3]}); camera at (0, 3, 10) "
-                        f"looking into the sphere box (at C3 71% of the camera rays miss every sphere)")
+                        f"looking into the sphere box" +
+                        (" (71% of the camera rays miss every sphere)" if args.config == "c3" else "") +
+                        (f"; one image tiled across {world} GPUs" if args.scaling == "strong" and world > 1 else ""))
             metric = ("Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline"
                       if (args.config, W, H) == ("c3", 4096, 4096)
                       else f"Mrays/sec at {W}x{H}, {args.spheres} spheres, depth {args.depth}")

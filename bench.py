@@ -7,16 +7,12 @@ f64 arithmetic, f32 RGB + sRGB BGR written to HBM.  The scene is uploaded once
 (inputs resident in HBM before timing); output stays in HBM (the PCIe copy and
 the host gather are reported beside `value`, never in it).
 
-    python bench.py [--steps K] [--warmup W]            (headline: C3, one GPU)
-    python bench.py --gpus N [--steps K] [--warmup W]   (scaling curve: C4 tiled over N GPUs)
+    python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
-Configs (BASELINE.json): without --gpus the line is the headline, C3 (4096²,
-1000 spheres, depth 8) on one GPU.  With --gpus N (any N, 1 included) the
-default is BASELINE config 4, the scaling-curve configuration: 8192², 10k
-spheres, depth 8, ONE image tiled across the N GPUs (strong scaling), so
-the N = 1, 2, 4, 8 lines of a scaling run measure the same workload.
---config overrides either (--config c3 --gpus N: C3's strong-scaling curve).
+Every N measures the headline config C3 (the N = 1 line is the headline
+number); --config c4 --gpus N gives BASELINE config 4's curve (8192², 10k
+spheres, depth 8, one image tiled across the N GPUs).
 
 Multi-GPU: run as plain `python bench.py --gpus N` the script starts N rank
 processes itself (before anything touches a GPU), one device each; under
@@ -58,11 +54,10 @@ BAND = 16
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=None,
-                   help="GPUs (one rank each); given, the default config is c4, BASELINE's scaling curve")
+    p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--config", default=None, choices=["c1", "c3", "c4", "c5"],
+    p.add_argument("--config", default="c3", choices=["c1", "c3", "c4", "c5"],
                    help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16; "
                         "c1 test_scene.txt 256^2, 1024 random AA samples, depth 1 (path kernel)")
     p.add_argument("--spp", type=int, default=0, help="c1: AA samples (default: the scene's 1024)")
@@ -92,11 +87,7 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: start the ranks, form the process group, report the "
                         "world and the devices seen, render nothing")
-    a = p.parse_args()
-    if a.config is None:
-        a.config = "c4" if a.gpus is not None else "c3"
-    a.gpus = a.gpus if a.gpus is not None else 1
-    return a
+    return p.parse_args()
 
 
 # ---------------------------------------------------------------- launcher

@@ -26,3 +26,24 @@ def test_gpus_two_spawns_two_ranks(backend):
     assert d["n_gpus"] == d["devices_visible"] == 0
     assert d["scaling"] == "strong"
     assert d["config"] == "c3"                  # every N measures the headline config
+
+
+def test_config_defaults(monkeypatch):
+    """Every N measures the headline config C3 (the driver's bench line is
+    `--gpus 1`); --config selects BASELINE's other configs."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
+    import bench
+    for argv, cfg, gpus in ((["bench.py"], "c3", 1), (["bench.py", "--gpus", "1"], "c3", 1),
+                            (["bench.py", "--gpus", "8"], "c3", 8), (["bench.py", "--gpus", "4", "--config", "c4"], "c4", 4)):
+        monkeypatch.setattr(sys, "argv", argv)
+        a = bench.parse()
+        assert (a.config, a.gpus) == (cfg, gpus)
+
+
+def test_cpu_baseline_sample_is_bounded():
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
+    import bench
+    from libraytrace import scenes
+    r = bench.cpu_sample(scenes.config3(256, 256), threads=2, budget_s=1.0, draws={})
+    assert r["rays"] > 0 and r["value"] > 0 and r["seconds"] < 10
+    assert bench.cpu_share() >= 1 and bench.cpu_model()

@@ -635,6 +635,12 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
 template <int kSrc, bool kCam, bool kCount, bool kFresnel, bool kLists>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+#ifndef RT_NEAR_PRIO
+#define RT_NEAR_PRIO 2
+#endif
+    // the nearest-hit chain is the frame's critical path: its waves win issue
+    // arbitration over the shadow / shading waves sharing a SIMD
+    if (RT_NEAR_PRIO) __builtin_amdgcn_s_setprio(RT_NEAR_PRIO);
     [[maybe_unused]] unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, acc[6] = {0, 0, 0, 0, 0, 0};
     RT_STAMP_AT(st0);
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);

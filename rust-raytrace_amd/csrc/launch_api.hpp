@@ -76,6 +76,7 @@ struct WfStreams {
     bool fuse;
     int cam;            // generation 0: 0 per-ray traversal, 1 camera tiles (LDS), 2 camera tiles (HBM/L2)
     bool lists0;        // shadow item lists from generation 0 (else from generation 1)
+    int fuse_from;      // generations >= fuse_from shade inside the shadow kernel (one B launch instead of two)
     int grid_occ;       // every light has a light-view grid: shadow kernel without a tree walk,
                         // spheres from LDS (1) or HBM/L2 (2); 0: the general shadow kernel
 };

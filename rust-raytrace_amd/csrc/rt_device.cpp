@@ -30,7 +30,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -62,6 +62,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"prio", 0, 0, 1},                           // nearest-hit chain on a high-priority stream
     {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
+    {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)
 };
 
 }  // namespace
@@ -833,6 +834,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             ws.lists0 = c->t(kTuneLists0) != 0;
             // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
             // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
+            ws.fuse_from = static_cast<int>(c->t(kTuneFuseFrom));
             ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
                               ? (static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere) <= 64 * 1024 ? 1 : 2)
                               : 0;

@@ -1085,7 +1085,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         else hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, false>), grid, block, lds_s, sb, sc, fp, b, k);
         return mb ? mb->mark(sb, kKfShadow) : hipSuccess;
     }
-    const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && ws.fuse;
+    const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && (ws.fuse || k >= ws.fuse_from);
     if (sc.n_lights > 0) {
         const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
         if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
@@ -1094,6 +1094,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         if (!fused && ws.grid_occ == 1) RT_OCC(kSrcGridL, false, false);
         else if (!fused && ws.grid_occ == 2) RT_OCC(kSrcGridG, false, false);
         else if (!fused) RT_OCC(kSrcO, false, false);
+        else if (ws.grid_occ == 1) { if (sc.has_fresnel) RT_OCC(kSrcGridL, true, true); else RT_OCC(kSrcGridL, true, false); }
+        else if (ws.grid_occ == 2) { if (sc.has_fresnel) RT_OCC(kSrcGridG, true, true); else RT_OCC(kSrcGridG, true, false); }
         else if (sc.has_fresnel) RT_OCC(kSrcO, true, true);
         else RT_OCC(kSrcO, true, false);
 #undef RT_OCC

@@ -466,7 +466,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
     C3-workload frame unchanged."""
     spec = scenes.config3(192, 160)
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
-    for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(regions=96),
+    for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(fuse_from=3), dict(fuse_from=0), dict(regions=96),
                dict(bstreams=1), dict(src=2, src_occ=11)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)

@@ -482,7 +482,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 #ifndef RT_NEAR_BL
 #define RT_NEAR_BL 1
 #endif
-template <bool kCount = false, int kNodes = 0>
+template <bool kCount = false, int kNodes = 0, int kReg = 0>
 __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
@@ -491,8 +491,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
-    uint64_t stk[kBvhStack];
-    int sp = 0;
+    RT_STACK_DECL(kReg, uint64_t);     // kReg newest entries in registers (the LDS-prefix source), the rest in scratch
     int32_t cur = sc.bvh_root;
     [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     // whole tree in LDS: per axis the array of NEAR bound pairs (lo when 1/d >= 0,
@@ -536,7 +535,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             }
             if constexpr (kCount) w->boxes += 2;
             const bool first0 = t0 <= t1;
-            if (h0 && h1) stk[sp++] = stk_entry(first0 ? c1 : c0, first0 ? t1 : t0);
+            if (h0 && h1) stk_push(stk_entry(first0 ? c1 : c0, first0 ? t1 : t0));
             cur = (h0 && (!h1 || first0)) ? c0 : (h1 ? c1 : kNone);
         }
         RT_WSTAMP(q1);
@@ -556,8 +555,8 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
         }
         RT_WSTAMP(q2);
         cur = kNone;
-        while (sp > 0) {
-            const uint64_t e = stk[--sp];
+        while (stk_n > 0) {
+            const uint64_t e = stk_pop();
             if (stk_t(e) <= tlim) { cur = stk_node(e); break; }
         }
         RT_WSTAMP(q3);

@@ -456,6 +456,10 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL) return nearest_bvh_bl<kCount, 2>(sc, v, r, w);
+#ifndef RT_BL_PREFIX
+#define RT_BL_PREFIX 1
+#endif
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix && RT_BL_PREFIX) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Same-box A/B of the current build against the round-1 tree (old_r1/, built
-# separately, gitignored): C4 and C3, alternating, plus tuning variants.
+# Same-box A/B of the current build against an older tree in old_r1/
+# (gitignored; e.g. `git worktree add /tmp/r1 <commit>`, build it there, copy it
+# without .git to old_r1/): C4 and C3, alternating, plus tuning variants.
 set -u
 cd "$(dirname "$0")/.."
 O=gpurun_out/abr1

@@ -37,6 +37,14 @@ int bvh4_stack_need(const Bvh4Result& b4);
 // Depth of a binary tree (its traversal pushes at most one entry per level).
 int bvh_depth(const BvhResult& b2);
 
+// The binary tree's nodes with binary16 bounds rounded outward (DevBvhNodeH);
+// empty when some bound is not finite or lies outside the half range.
+std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2);
+// binary16 helpers (exact decode; the largest half <= v / smallest half >= v)
+float half_to_float(uint16_t h);
+bool half_round_down(float v, uint16_t& out);
+bool half_round_up(float v, uint16_t& out);
+
 // Camera view of every node of a binary BVH (DevCamNode) for a camera at
 // `pos` with direction matrix `m` (row-major, camera.rs:57-61).
 std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]);

@@ -59,6 +59,17 @@ struct alignas(16) DevBvhNode {
 };
 static_assert(sizeof(DevBvhNode) == 64, "BVH node is one 64-B line");
 
+// The same node with IEEE binary16 bounds (host_bvh.cpp half_nodes): each f32
+// bound rounded OUTWARD to a half (lo down, hi up), so every half box contains
+// the f32 box and the culling argument of DESIGN.md §4 carries over.  32 B:
+// twice the nodes of an LDS prefix and half the bytes per L2 fetch below it.
+// Built only when every bound is finite and within the half range (+-65504).
+struct alignas(16) DevBvhNodeH {
+    uint16_t b[12];                 // lo0 xyz, hi0 xyz, lo1 xyz, hi1 xyz (binary16 bits)
+    int32_t c0, c1;
+};
+static_assert(sizeof(DevBvhNodeH) == 32, "half BVH node is 32 B");
+
 // Camera view of one binary BVH node, for the generation-0 tile traversal:
 // every camera ray starts at the camera position, so a child box maps to a
 // conservative rectangle of image-plane coordinates (px, py) -- the (px, py)
@@ -129,6 +140,7 @@ struct DevScene {
     const DevBvh4Plane* bvh4;       // the same tree collapsed 4-wide (DevBvh4Plane)
     int32_t bvh4_root, n_bvh4;
     const DevCamNode* cam_nodes;    // camera view of the binary BVH (null: generation 0 traverses per ray)
+    const DevBvhNodeH* bvh_h;       // the binary BVH with binary16 bounds (null: not representable)
     int32_t has_fresnel;            // some object uses FresnelMaterial
     int32_t pfx2, pfx4;             // prefix sources: nodes of the binary / 4-wide tree staged in LDS (set per render)
     int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,

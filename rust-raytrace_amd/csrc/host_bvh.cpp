@@ -14,6 +14,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <limits>
 #include <vector>
 
 #include "bvh_build.hpp"
@@ -347,6 +348,58 @@ int bvh4_stack_need(const Bvh4Result& b4) {
             if (ch.i[k] != kBvh4Empty && ch.i[k] >= 0) todo.push_back({ch.i[k], here});
     }
     return worst + 1;
+}
+
+float half_to_float(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const float sign = (h & 0x8000) ? -1.0f : 1.0f;
+    if (e == 31) return m ? std::numeric_limits<float>::quiet_NaN() : sign * std::numeric_limits<float>::infinity();
+    // both forms are exact in f32 (11 significant bits)
+    return sign * (e == 0 ? std::ldexp(static_cast<float>(m), -24) : std::ldexp(static_cast<float>(1024 + m), e - 25));
+}
+
+namespace {
+// Finite halves in value order: key k in [-0x7BFF, 0x7BFF] <-> bits (k >= 0 ? k : 0x8000 | -k).
+uint16_t half_of_key(int k) { return static_cast<uint16_t>(k >= 0 ? k : (0x8000 | -k)); }
+constexpr int kHalfMaxKey = 0x7BFF;   // 65504
+}  // namespace
+
+bool half_round_down(float v, uint16_t& out) {
+    if (!(std::fabs(v) <= 65504.0f)) return false;          // NaN, inf or outside the finite range
+    int lo = -kHalfMaxKey, hi = kHalfMaxKey;                 // largest key with value <= v (value(lo) <= v)
+    while (lo < hi) {
+        const int mid = lo + (hi - lo + 1) / 2;
+        if (half_to_float(half_of_key(mid)) <= v) lo = mid; else hi = mid - 1;
+    }
+    out = half_of_key(lo);
+    return true;
+}
+
+bool half_round_up(float v, uint16_t& out) {
+    if (!(std::fabs(v) <= 65504.0f)) return false;
+    int lo = -kHalfMaxKey, hi = kHalfMaxKey;                 // smallest key with value >= v
+    while (lo < hi) {
+        const int mid = lo + (hi - lo) / 2;
+        if (half_to_float(half_of_key(mid)) >= v) hi = mid; else lo = mid + 1;
+    }
+    out = half_of_key(lo);
+    return true;
+}
+
+std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2) {
+    std::vector<DevBvhNodeH> out(b2.nodes.size());
+    for (size_t k = 0; k < b2.nodes.size(); ++k) {
+        const DevBvhNode& n = b2.nodes[k];
+        DevBvhNodeH& h = out[k];
+        for (int a = 0; a < 3; ++a) {
+            if (!half_round_down(n.lo0[a], h.b[a]) || !half_round_up(n.hi0[a], h.b[3 + a]) ||
+                !half_round_down(n.lo1[a], h.b[6 + a]) || !half_round_up(n.hi1[a], h.b[9 + a]))
+                return {};
+        }
+        h.c0 = n.c0;
+        h.c1 = n.c1;
+    }
+    return out;
 }
 
 int bvh_depth(const BvhResult& b2) {

@@ -30,7 +30,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -63,6 +63,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
     {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)
+    {"compact_stack", 1, 0, 1},                  // small trees: 32-bit nearest-hit stack entries, 32 of them (src 9)
+    {"half_nodes", 1, 0, 1},                     // trees beyond LDS: binary16 node bounds for the prefix source (src 5)
 };
 
 }  // namespace
@@ -77,6 +79,7 @@ struct rt_ctx {
     DevScene dsc{};
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
+    bool short_stack = false;        // binary tree fits the compact nearest-hit stack (16-bit codes, depth <= 32)
     bool all_lights_gridded = false; // every light is a point light with a light-view grid
     unsigned long long* d_counters = nullptr;
     double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
@@ -475,7 +478,14 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     // traversal stacks hold 64 entries (trace_common.hpp kBvhStack / kBvh4Stack)
     if (bvh_depth(bvh) > 64) return fail(c, RT_E_UNSUPPORTED, "sphere BVH deeper than the traversal stack");
     c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
+    // compact stack (trace_common.hpp kShortStack, stk_entry16): the stack never holds more
+    // entries than the deepest inner node's depth; node indices and leaf codes
+    // (first << 3 | count - 1) must fit a signed 16-bit field
+    c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 32768 && spheres.size() <= 4096;
     const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
+    // binary16 nodes only for trees that do not fit LDS whole (the prefix source reads them)
+    const bool big_tree = bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget;
+    const std::vector<DevBvhNodeH> hnodes = big_tree ? half_nodes(bvh) : std::vector<DevBvhNodeH>{};
     std::vector<double> r_leaf(spheres.size());
     {
         std::vector<DevSphere> s2(spheres.size());
@@ -501,6 +511,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
     const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
     const size_t o_cam = place(camn.size() * sizeof(DevCamNode));
+    const size_t o_bvhh = place(hnodes.size() * sizeof(DevBvhNodeH));
     const size_t o_srgbv = place(256 * sizeof(double));
     const size_t o_lg = place(lg.grids.size() * sizeof(DevLightGrid));
     const size_t o_lgoff = place(lg.off.size() * sizeof(uint32_t));
@@ -522,6 +533,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
     put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
     put(o_cam, camn.data(), camn.size() * sizeof(DevCamNode));
+    put(o_bvhh, hnodes.data(), hnodes.size() * sizeof(DevBvhNodeH));
     put(o_srgbv, srgb_values_table(), 256 * sizeof(double));
     put(o_lg, lg.grids.data(), lg.grids.size() * sizeof(DevLightGrid));
     put(o_lgoff, lg.off.data(), lg.off.size() * sizeof(uint32_t));
@@ -556,6 +568,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.bvh4_root = bvh4.root;
     d.n_bvh4 = bvh4.n_nodes;
     d.cam_nodes = reinterpret_cast<const DevCamNode*>(base + o_cam);
+    d.bvh_h = hnodes.empty() ? nullptr : reinterpret_cast<const DevBvhNodeH*>(base + o_bvhh);
     d.has_fresnel = 0;
     for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
     d.needs_path = needs_path ? 1 : 0;
@@ -704,16 +717,21 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             src_occ = fit4 ? 10 : 13;
             if (!fit2 || !fit4) { src = 8; src_occ = 13; }
             if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;  // the 4-wide stack could overflow
+            if (src == 7 && src_occ == 10 && c->short_stack && c->t(kTuneCompact) != 0) src = 9;
+            if (src == 8 && c->dsc.bvh_h && c->t(kTuneHalf) != 0) src = 5;
             if (c->t(kTuneSrc) >= 0) {
                 src = static_cast<int>(c->t(kTuneSrc));
                 src_occ = c->t(kTuneSrcOcc) >= 0 ? static_cast<int>(c->t(kTuneSrcOcc)) : src;
             }
             auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
-            const bool pair_ok = ok(src) && ok(src_occ) &&
-                                 ((src == src_occ && src != 13) || (src == 7 && src_occ == 10) ||
+            const bool pair_ok = ((src == 9 && src_occ == 10 && c->short_stack) ||
+                                  (src == 5 && (src_occ == 13 || src_occ == 11) && c->dsc.bvh_h) ||
+                                  (ok(src) && ok(src_occ))) &&
+                                 ((src == src_occ && src != 13) || ((src == 7 || src == 9) && src_occ == 10) ||
+                                  ((src == 5 || src == 8) && (src_occ == 13 || src_occ == 11)) ||
                                   (src == 2 && src_occ == 11) || (src == 8 && (src_occ == 13 || src_occ == 11)) ||
                                   (src == 2 && src_occ == 13));
-            const bool fits = !((src == 4 || src == 7) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
+            const bool fits = !((src == 4 || src == 7 || src == 9) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
                               !((src_occ == 10 || src_occ == 12) && !fit4);
             if (!pair_ok || !fits) { src = 2; src_occ = 11; }
             if (c->deep_bvh4 && src_occ >= 10) src_occ = src = 2;
@@ -775,7 +793,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // generation 0 by camera tile ("cam" 0: per-ray like the other generations);
         // only with the binary-tree sources, whose node order the camera view shares
         int cam = 0;
-        if (src == 2 || src == 4 || src == 7 || src == 8) {
+        if (src == 2 || src == 4 || src == 5 || src == 7 || src == 8 || src == 9) {
             const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
             cam = cam_lds <= kLdsBudget ? 1 : 2;
             const int ce = static_cast<int>(c->t(kTuneCam));

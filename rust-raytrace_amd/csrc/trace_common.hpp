@@ -328,6 +328,8 @@ struct BvhView {
     int32_t nl4;
     const DevCamNode* cn;        // camera view of the binary tree (LDS or HBM)
     int32_t* stk;                // this wave's LDS traversal stack (camera sources)
+    const DevBvhNodeH* hpnodes;  // half-node prefix source: nodes [0, nl) in LDS (binary16 bounds)
+    const DevBvhNodeH* hgnodes;  // ... and the whole half-node tree in HBM/L2
 };
 
 // LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
@@ -368,10 +370,26 @@ __device__ __forceinline__ DevBvhNode lds_node(const float2* L, int32_t n, int32
     return nd;
 }
 
-// kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS
+__device__ __forceinline__ float half_bits_f(uint16_t h) {
+    return static_cast<float>(__builtin_bit_cast(_Float16, h));     // exact (v_cvt_f32_f16)
+}
+
+// kNodes: 0 = every node from HBM/L2, 1 = LDS prefix + HBM, 2 = every node in LDS,
+// 3 = LDS prefix + HBM of binary16 nodes (DevBvhNodeH, bounds rounded outward:
+// decoded exactly, each box contains the f32 node's box)
 template <int kNodes>
 __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
-    if constexpr (kNodes == 2) {
+    if constexpr (kNodes == 3) {
+        const DevBvhNodeH h = *(i < v.nl ? v.hpnodes + i : v.hgnodes + i);
+        DevBvhNode nd;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            nd.lo0[a] = half_bits_f(h.b[a]); nd.hi0[a] = half_bits_f(h.b[3 + a]);
+            nd.lo1[a] = half_bits_f(h.b[6 + a]); nd.hi1[a] = half_bits_f(h.b[9 + a]);
+        }
+        nd.c0 = h.c0; nd.c1 = h.c1;
+        return nd;
+    } else if constexpr (kNodes == 2) {
         return lds_node(v.lnodes, v.nl, i);
     } else if constexpr (kNodes == 1) {
         // one flat load from LDS or HBM/L2: the same layout on both sides, so no
@@ -382,6 +400,14 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
     }
 }
 
+// The private stack array must stay in scratch: an array small enough for the
+// compiler to promote to registers is indexed per lane with divergent indices,
+// which compiles to a waterfall loop over the wave's distinct indices (the
+// 128-B compact stack measured 130x slower that way).  Passing its address to
+// an empty asm statement makes it escape, so it is never promoted.
+template <class T>
+__device__ __forceinline__ void rt_keep_in_scratch(T* p) { asm volatile("" : : "v"(p)); }
+
 // Traversal stacks, declared as plain locals so the compiler keeps the stack
 // pointer (and the register part) in registers.  The top kReg entries live in
 // registers, shifted with v_mov on push/pop (constant indices after
@@ -391,8 +417,9 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
 // kReg = 0 every pop waits for its scratch load.  The nearest query packs
 // (node, entry t) into one 64-bit entry: one scratch access per push / pop.
 // The host bounds the tree depth, so kBvhStack entries always suffice.
-#define RT_STACK_DECL(kReg, E)                                                         \
-    E stk_m[kBvhStack];                                                                \
+#define RT_STACK_DECL(kReg, E) RT_STACK_DECL_N(kReg, E, kBvhStack)
+#define RT_STACK_DECL_N(kReg, E, kN)                                                   \
+    E stk_m[kN];                                                                       \
     E stk_r[(kReg) > 0 ? (kReg) : 1];                                                  \
     int stk_n = 0;                                                                     \
     auto stk_push = [&](E v) {                                                         \
@@ -422,6 +449,20 @@ __device__ __forceinline__ uint64_t stk_entry(int32_t node, float t) {
 }
 __device__ __forceinline__ int32_t stk_node(uint64_t e) { return static_cast<int32_t>(static_cast<uint32_t>(e)); }
 __device__ __forceinline__ float stk_t(uint64_t e) { return __uint_as_float(static_cast<uint32_t>(e >> 32)); }
+
+// Compact 32-bit entries for small trees (host: every node index and leaf code
+// fits 16 bits, depth <= kShortStack): the low half is the node / leaf code
+// (sign-extended from 16 bits), the high half the entry t's top 16 bits.
+// Dropping the low mantissa bits moves t toward zero: a non-negative t can only
+// get smaller and a negative one stays negative, so `t <= tlim` (tlim > 0)
+// culls a subset of what the exact t would: the same leaves that can hold the
+// winner are visited, and the (t, object) winner does not depend on order.
+constexpr int kShortStack = 32;
+__device__ __forceinline__ uint32_t stk_entry16(int32_t node, float t) {
+    return (__float_as_uint(t) & 0xFFFF0000u) | (static_cast<uint32_t>(node) & 0xFFFFu);
+}
+__device__ __forceinline__ int32_t stk_node(uint32_t e) { return static_cast<int32_t>(static_cast<int16_t>(e & 0xFFFFu)); }
+__device__ __forceinline__ float stk_t(uint32_t e) { return __uint_as_float(e & 0xFFFF0000u); }
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
@@ -482,7 +523,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 #ifndef RT_NEAR_BL
 #define RT_NEAR_BL 1
 #endif
-template <bool kCount = false, int kNodes = 0, int kReg = 0>
+template <bool kCount = false, int kNodes = 0, int kReg = 0, bool kCompact = false>
 __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
@@ -491,7 +532,14 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
-    RT_STACK_DECL(kReg, uint64_t);     // kReg newest entries in registers (the LDS-prefix source), the rest in scratch
+    // kReg newest entries in registers (the LDS-prefix source), the rest in scratch;
+    // kCompact: 32-bit entries, kShortStack of them (128 B of scratch per lane)
+    using StkE = std::conditional_t<kCompact, uint32_t, uint64_t>;
+    RT_STACK_DECL_N(kReg, StkE, (kCompact ? kShortStack : kBvhStack));
+    if constexpr (kCompact) rt_keep_in_scratch(stk_m);
+    auto mk_entry = [](int32_t node, float t) -> StkE {
+        if constexpr (kCompact) return stk_entry16(node, t); else return stk_entry(node, t);
+    };
     int32_t cur = sc.bvh_root;
     [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     // whole tree in LDS: per axis the array of NEAR bound pairs (lo when 1/d >= 0,
@@ -535,7 +583,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             }
             if constexpr (kCount) w->boxes += 2;
             const bool first0 = t0 <= t1;
-            if (h0 && h1) stk_push(stk_entry(first0 ? c1 : c0, first0 ? t1 : t0));
+            if (h0 && h1) stk_push(mk_entry(first0 ? c1 : c0, first0 ? t1 : t0));
             cur = (h0 && (!h1 || first0)) ? c0 : (h1 ? c1 : kNone);
         }
         RT_WSTAMP(q1);
@@ -556,7 +604,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
         RT_WSTAMP(q2);
         cur = kNone;
         while (stk_n > 0) {
-            const uint64_t e = stk_pop();
+            const StkE e = stk_pop();
             if (stk_t(e) <= tlim) { cur = stk_node(e); break; }
         }
         RT_WSTAMP(q3);

@@ -333,6 +333,7 @@ constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS pe
 constexpr int kSrcBvhG = 2;         // binary BVH from HBM/L2
 constexpr int kSrcBvhL = 4;         // binary BVH + spheres in LDS
 constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
+constexpr int kSrcBvhL8C = 9;       // kSrcBvhL8 with compact 32-bit stack entries (small trees, depth <= kShortStack)
 constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
 constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
 constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
@@ -340,6 +341,7 @@ constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup p
 // pfx4 nodes, chosen by the host) in LDS, the rest and the spheres from HBM/L2
 // (64 VGPRs).
 constexpr int kSrcBvhP = 8;         // binary BVH, LDS prefix
+constexpr int kSrcBvhPH = 5;        // binary BVH with binary16 bounds (DevBvhNodeH), LDS prefix of twice the nodes
 constexpr int kSrcBvh4P = 13;       // 4-wide BVH, LDS prefix
 // Generation 0 only: camera rays by 8x8 tile, a wave-uniform traversal of the
 // binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
@@ -357,12 +359,14 @@ struct Src {
     static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
     static constexpr bool bvh = kSrc >= kSrcBvhG && !grid;
     static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P;
-    static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P;
-    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
+    static constexpr bool half = kSrc == kSrcBvhPH;
+    static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P || half;
+    static constexpr bool compact = kSrc == kSrcBvhL8C;
+    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
                                     kSrc == kSrcCamL;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL;
-    static constexpr int nodes = all_lds ? 2 : prefix ? 1 : 0;
-    static constexpr int waves = kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 ? 8 : 4;   // min waves per SIMD
+    static constexpr int nodes = all_lds ? 2 : half ? 3 : prefix ? 1 : 0;
+    static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4) || half ? 8 : 4;   // min waves per SIMD
 };
 
 // Per-wave traversal stack of the camera sources (wave-uniform entries).
@@ -372,6 +376,7 @@ constexpr int kCamStack = 64;
 template <int kSrc>
 __host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
     if (kSrc == kSrcBvhP) return min(sc.n_bvh, sc.pfx2);
+    if (kSrc == kSrcBvhPH) return min(sc.n_bvh, 2 * sc.pfx2);     // same LDS bytes, 32-B nodes
     if (kSrc == kSrcBvh4P) return min(sc.n_bvh4, sc.pfx4);
     return 0;
 }
@@ -382,6 +387,7 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
     if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
+    if (kSrc == kSrcBvhPH) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNodeH);
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
     if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
@@ -405,6 +411,14 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         const int32_t nl = prefix_nodes<kSrc>(sc);
         for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh[i];
         v.pnodes = ln;
+        v.nl = nl;
+        return v;
+    } else if constexpr (kSrc == kSrcBvhPH) {
+        DevBvhNodeH* ln = reinterpret_cast<DevBvhNodeH*>(lds);
+        const int32_t nl = prefix_nodes<kSrc>(sc);
+        for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh_h[i];
+        v.hpnodes = ln;
+        v.hgnodes = sc.bvh_h;
         v.nl = nl;
         return v;
     } else if constexpr (kSrc == kSrcBvh4P) {
@@ -455,10 +469,12 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL) return nearest_bvh_bl<kCount, 2>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL)
+        return nearest_bvh_bl<kCount, 2, 0, Src<kSrc>::compact>(sc, v, r, w);
 #ifndef RT_BL_PREFIX
 #define RT_BL_PREFIX 1
 #endif
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix && RT_BL_PREFIX) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
@@ -1137,8 +1153,11 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvh4L * 101: RT_GEN(kSrcBvh4L, kSrcBvh4L); break;
         case kSrcBvh4L4 * 101: RT_GEN(kSrcBvh4L4, kSrcBvh4L4); break;
         case kSrcBvhL8 * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8, kSrcBvh4L); break;
+        case kSrcBvhL8C * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8C, kSrcBvh4L); break;
         case kSrcBvhG * 100 + kSrcBvh4G: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
         case kSrcBvhP * 100 + kSrcBvh4P: RT_GEN(kSrcBvhP, kSrcBvh4P); break;
+        case kSrcBvhPH * 100 + kSrcBvh4P: RT_GEN(kSrcBvhPH, kSrcBvh4P); break;
+        case kSrcBvhPH * 100 + kSrcBvh4G: RT_GEN(kSrcBvhPH, kSrcBvh4G); break;
         case kSrcBvhP * 101: RT_GEN(kSrcBvhP, kSrcBvhP); break;
         case kSrcBvhP * 100 + kSrcBvh4G: RT_GEN(kSrcBvhP, kSrcBvh4G); break;
         case kSrcBvhG * 100 + kSrcBvh4P: RT_GEN(kSrcBvhG, kSrcBvh4P); break;

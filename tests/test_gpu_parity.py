@@ -344,6 +344,24 @@ def test_bvh_ten_thousand_spheres(gpu_ctx):
     check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
+def test_half_node_prefix_source_is_bit_identical(gpu_ctx):
+    """C4's workload (10k spheres: the tree exceeds LDS): the nearest-hit walk over
+    binary16 nodes (bounds rounded outward, twice the nodes in the LDS prefix;
+    the default) and over f32 nodes give the same bytes, colours and rays, equal
+    to the oracle's; also with a 1 KB prefix, so most nodes come from HBM/L2."""
+    spec = scenes.config4(128, 96)
+    ref = ref64.render(spec, threads=min(16, os.cpu_count() or 1))
+    base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert np.array_equal(base[1], ref["bgr"])
+    assert base[2].rays == ref["counts"]["rays"]
+    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1)]:
+        with _with_tuning(gpu_ctx, **kv):
+            got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+        assert np.array_equal(got[1], base[1]), kv
+        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), kv
+        assert got[2].rays == base[2].rays and got[2].shadow_rays == base[2].shadow_rays, kv
+
+
 def test_bvh_matches_brute_force_bit_for_bit_full_frame(gpu_ctx):
     """Headline scene, full 4096x4096: BVH and linear scan agree on every byte
     and every ray (a size-independent property of conservative culling)."""
@@ -467,7 +485,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
     spec = scenes.config3(192, 160)
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
     for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(fuse_from=3), dict(fuse_from=0), dict(regions=96),
-               dict(bstreams=1), dict(src=2, src_occ=11)]:
+               dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

@@ -12,12 +12,10 @@ the host gather are reported beside `value`, never in it).
 
 Every N measures the headline config C3 (the N = 1 line is the headline
 number); --config c4 --gpus N gives BASELINE config 4's curve (8192², 10k
-spheres, depth 8, one image tiled across the N GPUs).  At C3 four frames are
-in flight (--inflight): successive steps render through four contexts into
-four output buffers, so one frame's short tail generations overlap the next
-frame's first ones; every step is still one whole frame, and the K frames are
-all finished inside the timed region.  The roofline's per-render duration
-comes from K further renders issued one at a time.
+spheres, depth 8, one image tiled across the N GPUs).  --inflight F renders
+successive steps through F contexts into F output buffers (every step still
+one whole frame, all K finished inside the timed region); the roofline's
+per-render duration then comes from K further renders issued one at a time.
 
 Multi-GPU: run as plain `python bench.py --gpus N` the script starts N rank
 processes itself (before anything touches a GPU), one device each; under
@@ -55,10 +53,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TFLOPS = 78.6   # spec, FMA counted; the kernel issues no FMA (parity), so ~39.3 is its ceiling
 BAND = 16
-# Frames in flight at C3 (measured, one MI355X, 16 hardware queues, ms per frame: F = 1 3.27-3.29,
-# 2 3.31, 3 3.21, 4 3.17-3.20, 6 3.25-4.08; a 1/8 row-band share (each rank of N = 8):
-# F = 1 0.91, 4 0.75)
-INFLIGHT_DEFAULT = 4
+# Frames in flight (--inflight F) are opt-in: measured at the driver's K = 20 / W = 5 on one MI355X
+# (tools/gpu_s5.sh), F = 4 with 16 hardware queues gave 3.23-3.28 vs 3.19-3.28 ms per C3 frame and
+# 0.87-1.04 vs 0.91-0.93 ms for one rank's share of N = 8; an earlier sweep's 3.17 / 0.75 did not repeat.
 
 
 def parse():
@@ -87,10 +84,10 @@ def parse():
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
     p.add_argument("--no-gather", action="store_true", help="skip the host-gather measurement")
-    p.add_argument("--inflight", type=int, default=0,
+    p.add_argument("--inflight", type=int, default=1,
                    help="frames in flight: F contexts (each its own working set and streams) render successive "
                         "steps into F output buffers, so frame i+1's first generations overlap frame i's tail "
-                        "(0: 4 at c3; 1 at c4/c5, whose working sets fill the memory budget, and at c1, one launch per frame)")
+                        "(c4/c5: each context's working set is sized to an 80 GB budget, so keep F = 1 there)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: process-group backend for the barrier and the max-over-ranks timing (nccl = RCCL; "
                         "gloo rehearses N ranks on fewer GPUs, ranks sharing a device round-robin)")
@@ -302,13 +299,14 @@ def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
 
 def main():
     args = parse()
-    if args.inflight <= 0:
-        args.inflight = INFLIGHT_DEFAULT if args.config == "c3" else 1
+    args.inflight = max(1, args.inflight)
     if args.inflight > 1:
         # F contexts x 3 streams each (nearest-hit chain + two shadow/shading streams): with HIP's
         # default of 4 hardware queues they alias and the frames serialise; 16 gives each stream
-        # its own queue (set before anything initialises HIP, in this process and the ranks it starts)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+        # its own queue (set before anything initialises HIP, in this process and the ranks it starts;
+        # the GPU boxes export the default 4, so a lower value is raised, not kept)
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+            os.environ["GPU_MAX_HW_QUEUES"] = "16"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     import torch

@@ -36,7 +36,7 @@ struct TuneDef {
     const char* name;
     int64_t dflt, lo, hi;
 };
-// -1 in src / src_occ / cam: chosen per scene
+// -1 in src / src_occ / cam / split: chosen per scene
 constexpr TuneDef kTune[kTuneCount] = {
     {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what kWfBudget of working set holds at the depth)
     {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
@@ -49,7 +49,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"lanes", 1, 1, 8},                          // chunk lanes (each its own streams and working set)
     {"stagger_gen", 1, 0, 64},                   // lanes: chunk c+1 starts after this generation of chunk c
     {"regions", 0, 0, 2048},                     // regions per queue (0: 2 x CUs)
-    {"split", 1, 0, 1},                          // 0: every wavefront kernel on one in-order stream
+    {"split", -1, -1, 1},                        // 0: every wavefront kernel on one in-order stream (-1: per tree)
     {"bstreams", 2, 1, 4},                       // streams for the shadow + shading kernels
     {"fuse", 0, 0, 1},                           // shading inside the shadow kernel
     {"lists", 1, 0, 1},                          // shadow item lists (with fuse)
@@ -780,7 +780,12 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // "deal": 1 workgroup-major chunk dealing (default), 0 workgroup-first;
         // "bstreams": streams for the shadow + shading kernels (default 2;
         // generations alternate over them); "fuse" 1: shading fused into the shadow kernel
-        const bool split = c->t(kTuneSplit) != 0;
+        // default: two B streams when the tree is in LDS (C3: 3.30 vs 3.71 ms on one stream);
+        // one stream when the nearest-hit walk reads the tree through L2 below its LDS prefix,
+        // where the overlapped shadow / shading waves slow that chain more than they hide
+        // (C4 55.2 vs 56.6-57.3 ms, C5 318 vs 330 ms, binary16 nodes)
+        const bool prefix_src = src == 5 || src == 8;
+        const bool split = c->t(kTuneSplit) < 0 ? !prefix_src : c->t(kTuneSplit) != 0;
         // two b streams (consecutive generations' shadows and shading overlap): measured
         // 3.87 -> 3.78 ms at C3 once the shading runs in its own kernel; three are slower
         const int n_b = std::max(1, std::min(kMaxBStreams, static_cast<int>(c->t(kTuneBStreams))));

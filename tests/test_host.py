@@ -311,3 +311,15 @@ def test_light_grid_builder_extreme_spheres():
     for li in range(2):
         cands, info = sc.light_grid_candidates(li, pts)
         assert len(cands) == len(pts) and info[0] > 0
+
+
+def test_tuning_keys_listed_in_the_header():
+    """Every schedule knob the library knows is named in raytrace_amd.h's
+    rt_ctx_set_tuning comment, including the round-2 ones (compact_stack,
+    half_nodes); no GPU needed to enumerate them."""
+    keys = lr.tuning_keys()
+    assert {"split", "compact_stack", "half_nodes", "src", "prefix_kb"} <= set(keys)
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "raytrace_amd.h")).read()
+    block = hdr[hdr.index("Schedule tuning of a context"):hdr.index("int rt_ctx_set_tuning")]
+    for k in keys:
+        assert k in block, k

@@ -323,3 +323,36 @@ def test_tuning_keys_listed_in_the_header():
     block = hdr[hdr.index("Schedule tuning of a context"):hdr.index("int rt_ctx_set_tuning")]
     for k in keys:
         assert k in block, k
+
+
+def test_binary16_node_bounds_round_outward():
+    """host_bvh.cpp's binary16 conversion for the half-node prefix source
+    (DESIGN.md §4 item 5): round_down gives the largest half <= v and round_up
+    the smallest half >= v (checked against numpy's float16 neighbours), the
+    decode is exact, and values beyond +-65504 or non-finite are refused (the
+    tree then keeps f32 nodes).  Internal C++ helpers, reached by their
+    mangled names."""
+    down = lr.lib._ZN5rtamd15half_round_downEfRt
+    up = lr.lib._ZN5rtamd13half_round_upEfRt
+    dec = lr.lib._ZN5rtamd13half_to_floatEt
+    for f in (down, up):
+        f.restype, f.argtypes = C.c_bool, [C.c_float, C.POINTER(C.c_uint16)]
+    dec.restype, dec.argtypes = C.c_float, [C.c_uint16]
+    rng = np.random.default_rng(16)
+    vals = np.concatenate([rng.uniform(-80, 80, 3000), rng.uniform(-1e-3, 1e-3, 500), 10.0 ** rng.uniform(-9, 4.8, 500),
+                           [0.0, -0.0, 65504.0, -65504.0, 6.1e-5, -6.1e-5, 1e-8, 2.0 ** -24, 1.0, -1.0]]).astype(np.float32)
+    h = C.c_uint16()
+    for v in vals:
+        v = float(v)
+        assert down(v, C.byref(h))
+        lo = dec(h.value)
+        assert lo <= v and np.float32(lo) == np.float16(np.frombuffer(np.uint16(h.value).tobytes(), np.float16)[0])
+        nxt = np.nextafter(np.float16(lo), np.float16(np.inf))
+        assert float(nxt) > v or lo == v          # no larger half is <= v
+        assert up(v, C.byref(h))
+        hi = dec(h.value)
+        assert hi >= v
+        prv = np.nextafter(np.float16(hi), np.float16(-np.inf))
+        assert float(prv) < v or hi == v
+    for bad in (70000.0, -70000.0, float("inf"), float("nan")):
+        assert not down(bad, C.byref(h)) and not up(bad, C.byref(h))

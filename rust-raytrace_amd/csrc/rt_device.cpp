@@ -807,8 +807,9 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         }
         const uint32_t wg_major = c->t(kTuneDeal) != 0 ? 1u : 0u;
         if (c->t(kTuneVerbose))
-            std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d pfx %d/%d\n", src, src_occ, cam,
-                         nlists, c->deep_bvh4 ? 1 : 0, c->dsc.pfx2, c->dsc.pfx4);
+            std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d short_stack %d split %d pfx %d/%d\n",
+                         src, src_occ, cam, nlists, c->deep_bvh4 ? 1 : 0, c->short_stack ? 1 : 0, split ? 1 : 0,
+                         c->dsc.pfx2, c->dsc.pfx4);
         for (int l = 0; l < n_lanes; ++l) {
             if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
             rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1, nlists);

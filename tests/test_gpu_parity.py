@@ -297,6 +297,32 @@ def test_extreme_sphere_sizes_and_far_plane_origins(gpu_ctx, algo):
     check_parity(gpu_ctx, s, algo)
 
 
+def test_chain_of_shrinking_spheres_both_stacks(gpu_ctx):
+    """A chain of spheres halving in size and spacing toward x = 2 inside a
+    random cloud: the binned SAH peels a few spheres per level, giving the
+    deepest tree a scene this small reaches (still within the compact stack's
+    32 entries: tools/schedule_probe.py prints short_stack 1; a binned SAH
+    re-bins every node over its own extent, so depth > 32 needs far more
+    spheres than the compact source's 4096).  Compact 32-bit entries (src 9)
+    and the 64-bit stack (compact_stack=0, src 7) both match the oracle bit
+    for bit."""
+    s = scenes.config2(80, 60)
+    s.max_depth = 6
+    for i in range(46):
+        r = 0.9 * 2.0 ** -i            # sphere i at x = -2 + 4 (1 - 2^-i): each level of the SAH peels one
+        s.sphere((-2.0 + 4.0 * (1.0 - 2.0 ** -i), 1.5, -6.0), r,
+                 scenes.phong((0.5, 0.4, 0.3), (0.5, 0.5, 0.5), 20.0, (0.01, 0.01, 0.01)))
+    rng = scenes.SplitMix64(9)
+    for _ in range(150):
+        s.sphere((rng.uniform(-6, 6), rng.uniform(0.2, 4), rng.uniform(-14, -3)), rng.uniform(0.05, 0.4),
+                 scenes.phong((0.3, 0.6, 0.9), (0.4, 0.4, 0.4), 30.0, (0, 0, 0)))
+    check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+    base = gpu_render(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+    with _with_tuning(gpu_ctx, compact_stack=0):
+        wide = gpu_render(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+    assert np.array_equal(base[1], wide[1]) and base[2].rays == wide[2].rays
+
+
 @pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
 def test_light_view_grids_adversarial_lights(gpu_ctx, algo):
     """Point-light shadows through the light-view grids (host_lightgrid.cpp):
@@ -354,7 +380,7 @@ def test_half_node_prefix_source_is_bit_identical(gpu_ctx):
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
     assert np.array_equal(base[1], ref["bgr"])
     assert base[2].rays == ref["counts"]["rays"]
-    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1)]:
+    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1), dict(split=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

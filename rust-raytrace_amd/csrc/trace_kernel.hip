@@ -464,13 +464,17 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     return v;
 }
 
+// register entries on top of the compact stack (A/B builds: EXTRA=-DRT_COMPACT_REG=n)
+#ifndef RT_COMPACT_REG
+#define RT_COMPACT_REG 0
+#endif
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
     if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL)
-        return nearest_bvh_bl<kCount, 2, 0, Src<kSrc>::compact>(sc, v, r, w);
+        return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact ? RT_COMPACT_REG : 0, Src<kSrc>::compact>(sc, v, r, w);
 #ifndef RT_BL_PREFIX
 #define RT_BL_PREFIX 1
 #endif

@@ -63,7 +63,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
     {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)
-    {"compact_stack", 1, 0, 1},                  // small trees: 32-bit nearest-hit stack entries, 32 of them (src 9)
+    {"compact_stack", 1, 0, 1},                  // 32-bit nearest-hit stack entries, 32 of them (src 9; src 6 for half-node trees)
     {"half_nodes", 1, 0, 1},                     // trees beyond LDS: binary16 node bounds for the prefix source (src 5)
 };
 
@@ -80,6 +80,7 @@ struct rt_ctx {
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
     bool short_stack = false;        // binary tree fits the compact nearest-hit stack (16-bit codes, depth <= 32)
+    bool short_stack18 = false;      // ... with 18-bit codes (the binary16 prefix source, src 6)
     bool all_lights_gridded = false; // every light is a point light with a light-view grid
     unsigned long long* d_counters = nullptr;
     double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
@@ -482,6 +483,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     // entries than the deepest inner node's depth; node indices and leaf codes
     // (first << 3 | count - 1) must fit a signed 16-bit field
     c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 32768 && spheres.size() <= 4096;
+    c->short_stack18 = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 131072 && spheres.size() <= 16383;
     const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
     // binary16 nodes only for trees that do not fit LDS whole (the prefix source reads them)
     const bool big_tree = bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget;
@@ -719,6 +721,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;  // the 4-wide stack could overflow
             if (src == 7 && src_occ == 10 && c->short_stack && c->t(kTuneCompact) != 0) src = 9;
             if (src == 8 && c->dsc.bvh_h && c->t(kTuneHalf) != 0) src = 5;
+            if (src == 5 && c->short_stack18 && c->t(kTuneCompact) != 0) src = 6;
             if (c->t(kTuneSrc) >= 0) {
                 src = static_cast<int>(c->t(kTuneSrc));
                 src_occ = c->t(kTuneSrcOcc) >= 0 ? static_cast<int>(c->t(kTuneSrcOcc)) : src;
@@ -726,9 +729,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
             const bool pair_ok = ((src == 9 && src_occ == 10 && c->short_stack) ||
                                   (src == 5 && (src_occ == 13 || src_occ == 11) && c->dsc.bvh_h) ||
+                                  (src == 6 && (src_occ == 13 || src_occ == 11) && c->dsc.bvh_h && c->short_stack18) ||
                                   (ok(src) && ok(src_occ))) &&
                                  ((src == src_occ && src != 13) || ((src == 7 || src == 9) && src_occ == 10) ||
-                                  ((src == 5 || src == 8) && (src_occ == 13 || src_occ == 11)) ||
+                                  ((src == 5 || src == 6 || src == 8) && (src_occ == 13 || src_occ == 11)) ||
                                   (src == 2 && src_occ == 11) || (src == 8 && (src_occ == 13 || src_occ == 11)) ||
                                   (src == 2 && src_occ == 13));
             const bool fits = !((src == 4 || src == 7 || src == 9) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
@@ -784,7 +788,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // one stream when the nearest-hit walk reads the tree through L2 below its LDS prefix,
         // where the overlapped shadow / shading waves slow that chain more than they hide
         // (C4 55.2 vs 56.6-57.3 ms, C5 318 vs 330 ms, binary16 nodes)
-        const bool prefix_src = src == 5 || src == 8;
+        const bool prefix_src = src == 5 || src == 6 || src == 8;
         const bool split = c->t(kTuneSplit) < 0 ? !prefix_src : c->t(kTuneSplit) != 0;
         // two b streams (consecutive generations' shadows and shading overlap): measured
         // 3.87 -> 3.78 ms at C3 once the shading runs in its own kernel; three are slower
@@ -798,7 +802,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // generation 0 by camera tile ("cam" 0: per-ray like the other generations);
         // only with the binary-tree sources, whose node order the camera view shares
         int cam = 0;
-        if (src == 2 || src == 4 || src == 5 || src == 7 || src == 8 || src == 9) {
+        if (src == 2 || src == 4 || src == 5 || src == 6 || src == 7 || src == 8 || src == 9) {
             const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
             cam = cam_lds <= kLdsBudget ? 1 : 2;
             const int ce = static_cast<int>(c->t(kTuneCam));

@@ -450,19 +450,24 @@ __device__ __forceinline__ uint64_t stk_entry(int32_t node, float t) {
 __device__ __forceinline__ int32_t stk_node(uint64_t e) { return static_cast<int32_t>(static_cast<uint32_t>(e)); }
 __device__ __forceinline__ float stk_t(uint64_t e) { return __uint_as_float(static_cast<uint32_t>(e >> 32)); }
 
-// Compact 32-bit entries for small trees (host: every node index and leaf code
-// fits 16 bits, depth <= kShortStack): the low half is the node / leaf code
-// (sign-extended from 16 bits), the high half the entry t's top 16 bits.
-// Dropping the low mantissa bits moves t toward zero: a non-negative t can only
-// get smaller and a negative one stays negative, so `t <= tlim` (tlim > 0)
-// culls a subset of what the exact t would: the same leaves that can hold the
-// winner are visited, and the (t, object) winner does not depend on order.
+// Compact 32-bit entries (host: every node index and leaf code fits kBits
+// bits signed, depth <= kShortStack): the low kBits bits are the node / leaf
+// code (sign-extended), the rest the entry t's top 32 - kBits bits (sign,
+// exponent, 23 - kBits mantissa bits: 16 -> 7, 18 -> 5).  Dropping the low
+// mantissa bits moves t toward zero: a non-negative t can only get smaller and
+// a negative one stays negative, so `t <= tlim` (tlim > 0) culls a subset of
+// what the exact t would: the same leaves that can hold the winner are
+// visited, and the (t, object) winner does not depend on order.
 constexpr int kShortStack = 32;
-__device__ __forceinline__ uint32_t stk_entry16(int32_t node, float t) {
-    return (__float_as_uint(t) & 0xFFFF0000u) | (static_cast<uint32_t>(node) & 0xFFFFu);
+template <int kBits>
+__device__ __forceinline__ uint32_t stk_entry_c(int32_t node, float t) {
+    constexpr uint32_t kMask = (1u << kBits) - 1u;
+    return (__float_as_uint(t) & ~kMask) | (static_cast<uint32_t>(node) & kMask);
 }
-__device__ __forceinline__ int32_t stk_node(uint32_t e) { return static_cast<int32_t>(static_cast<int16_t>(e & 0xFFFFu)); }
-__device__ __forceinline__ float stk_t(uint32_t e) { return __uint_as_float(e & 0xFFFF0000u); }
+template <int kBits>
+__device__ __forceinline__ int32_t stk_node_c(uint32_t e) { return static_cast<int32_t>(e << (32 - kBits)) >> (32 - kBits); }
+template <int kBits>
+__device__ __forceinline__ float stk_t_c(uint32_t e) { return __uint_as_float(e & ~((1u << kBits) - 1u)); }
 
 // Scene::intersect through the BVH.  Same winner as nearest_brute: candidates
 // compete on (t, object id), independent of visiting order.
@@ -523,7 +528,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 #ifndef RT_NEAR_BL
 #define RT_NEAR_BL 1
 #endif
-template <bool kCount = false, int kNodes = 0, int kReg = 0, bool kCompact = false>
+template <bool kCount = false, int kNodes = 0, int kReg = 0, int kCompactBits = 0>
 __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
@@ -533,12 +538,20 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
     // kReg newest entries in registers (the LDS-prefix source), the rest in scratch;
-    // kCompact: 32-bit entries, kShortStack of them (128 B of scratch per lane)
+    // kCompactBits > 0: 32-bit entries with that many code bits, kShortStack of them
+    // (128 B of scratch per lane); 0: 64-bit (node, t) entries
+    constexpr bool kCompact = kCompactBits > 0;
     using StkE = std::conditional_t<kCompact, uint32_t, uint64_t>;
     RT_STACK_DECL_N(kReg, StkE, (kCompact ? kShortStack : kBvhStack));
     if constexpr (kCompact) rt_keep_in_scratch(stk_m);
     auto mk_entry = [](int32_t node, float t) -> StkE {
-        if constexpr (kCompact) return stk_entry16(node, t); else return stk_entry(node, t);
+        if constexpr (kCompact) return stk_entry_c<kCompactBits>(node, t); else return stk_entry(node, t);
+    };
+    auto e_node = [](StkE e) -> int32_t {
+        if constexpr (kCompact) return stk_node_c<kCompactBits>(e); else return stk_node(e);
+    };
+    auto e_t = [](StkE e) -> float {
+        if constexpr (kCompact) return stk_t_c<kCompactBits>(e); else return stk_t(e);
     };
     int32_t cur = sc.bvh_root;
     [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
@@ -605,7 +618,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
         cur = kNone;
         while (stk_n > 0) {
             const StkE e = stk_pop();
-            if (stk_t(e) <= tlim) { cur = stk_node(e); break; }
+            if (e_t(e) <= tlim) { cur = e_node(e); break; }
         }
         RT_WSTAMP(q3);
 #if RT_STAMP

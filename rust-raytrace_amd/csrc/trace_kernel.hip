@@ -342,6 +342,7 @@ constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup p
 // (64 VGPRs).
 constexpr int kSrcBvhP = 8;         // binary BVH, LDS prefix
 constexpr int kSrcBvhPH = 5;        // binary BVH with binary16 bounds (DevBvhNodeH), LDS prefix of twice the nodes
+constexpr int kSrcBvhPHC = 6;       // kSrcBvhPH with compact 32-bit stack entries (18-bit codes: <= 16383 spheres)
 constexpr int kSrcBvh4P = 13;       // 4-wide BVH, LDS prefix
 // Generation 0 only: camera rays by 8x8 tile, a wave-uniform traversal of the
 // binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
@@ -359,7 +360,8 @@ struct Src {
     static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
     static constexpr bool bvh = kSrc >= kSrcBvhG && !grid;
     static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P;
-    static constexpr bool half = kSrc == kSrcBvhPH;
+    static constexpr bool half = kSrc == kSrcBvhPH || kSrc == kSrcBvhPHC;
+    static constexpr int compact_bits = kSrc == kSrcBvhL8C ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
     static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P || half;
     static constexpr bool compact = kSrc == kSrcBvhL8C;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
@@ -376,7 +378,7 @@ constexpr int kCamStack = 64;
 template <int kSrc>
 __host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
     if (kSrc == kSrcBvhP) return min(sc.n_bvh, sc.pfx2);
-    if (kSrc == kSrcBvhPH) return min(sc.n_bvh, 2 * sc.pfx2);     // same LDS bytes, 32-B nodes
+    if (Src<kSrc>::half) return min(sc.n_bvh, 2 * sc.pfx2);     // same LDS bytes, 32-B nodes
     if (kSrc == kSrcBvh4P) return min(sc.n_bvh4, sc.pfx4);
     return 0;
 }
@@ -387,7 +389,7 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
     if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
-    if (kSrc == kSrcBvhPH) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNodeH);
+    if (Src<kSrc>::half) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNodeH);
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
     if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
@@ -413,7 +415,7 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.pnodes = ln;
         v.nl = nl;
         return v;
-    } else if constexpr (kSrc == kSrcBvhPH) {
+    } else if constexpr (Src<kSrc>::half) {
         DevBvhNodeH* ln = reinterpret_cast<DevBvhNodeH*>(lds);
         const int32_t nl = prefix_nodes<kSrc>(sc);
         for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh_h[i];
@@ -474,11 +476,11 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL)
-        return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact ? RT_COMPACT_REG : 0, Src<kSrc>::compact>(sc, v, r, w);
+        return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact ? RT_COMPACT_REG : 0, Src<kSrc>::compact_bits>(sc, v, r, w);
 #ifndef RT_BL_PREFIX
 #define RT_BL_PREFIX 1
 #endif
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix && RT_BL_PREFIX) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
@@ -1162,6 +1164,8 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         case kSrcBvhP * 100 + kSrcBvh4P: RT_GEN(kSrcBvhP, kSrcBvh4P); break;
         case kSrcBvhPH * 100 + kSrcBvh4P: RT_GEN(kSrcBvhPH, kSrcBvh4P); break;
         case kSrcBvhPH * 100 + kSrcBvh4G: RT_GEN(kSrcBvhPH, kSrcBvh4G); break;
+        case kSrcBvhPHC * 100 + kSrcBvh4P: RT_GEN(kSrcBvhPHC, kSrcBvh4P); break;
+        case kSrcBvhPHC * 100 + kSrcBvh4G: RT_GEN(kSrcBvhPHC, kSrcBvh4G); break;
         case kSrcBvhP * 101: RT_GEN(kSrcBvhP, kSrcBvhP); break;
         case kSrcBvhP * 100 + kSrcBvh4G: RT_GEN(kSrcBvhP, kSrcBvh4G); break;
         case kSrcBvhG * 100 + kSrcBvh4P: RT_GEN(kSrcBvhG, kSrcBvh4P); break;

@@ -6,7 +6,10 @@ wf_nearest launch; the last uninstrumented frame of each pass is used.
 MI355X_MICROARCH.md ("HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, so it is doubled.
 
-    python tools/pmc_traffic.py gpurun_out/pmc KEY [out.json]
+    python tools/pmc_traffic.py gpurun_out/pmc KEY [out.json] [chunks]
+
+A frame rendered as several wavefront chunks (C5: 7) starts a generation-0
+launch per chunk: `chunks` sums the last that many chunk-frames into one.
 """
 import collections
 import csv
@@ -45,12 +48,17 @@ def frames(path, counter):
 def main():
     root, key = sys.argv[1], sys.argv[2]
     out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     per = {}
     for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
         for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
             fr = frames(f, counter)
-            if fr:
-                per[counter] = {k: v * scale for k, v in fr[-1]["kernels"].items()}
+            if len(fr) >= chunks:
+                acc = collections.defaultdict(float)
+                for f_ in fr[-chunks:]:
+                    for k, v in f_["kernels"].items():
+                        acc[k] += v * scale
+                per[counter] = dict(acc)
                 break
     if len(per) != 2:
         sys.exit("need one FETCH_SIZE and one WRITE_SIZE pass")
@@ -66,7 +74,8 @@ def main():
                 "per_kernel_family": kernels,
                 "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace only; "
                           "KiB -> bytes; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section); "
-                          "last uninstrumented frame of each pass"}
+                          "last uninstrumented frame of each pass" +
+                          (f" ({chunks} wavefront chunks summed)" if chunks > 1 else "")}
     json.dump(doc, open(out_path, "w"), indent=1)
     print(json.dumps(doc[key], indent=1))
 

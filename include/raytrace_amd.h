@@ -261,7 +261,8 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * prefix_kb, prefix4_kb, lanes, stagger_gen, regions, split, bstreams, fuse,
  * lists, cam, deal, spread_below, lists0, path_group, cu_mask, prio, verbose,
  * grid_occ, fuse_from, compact_stack (small trees: 32-bit nearest-hit stack entries),
- * half_nodes (trees beyond LDS: binary16 node bounds for the prefix walk).
+ * half_nodes (trees beyond LDS: binary16 node bounds for the prefix walk),
+ * cam_prefix_kb (camera view read through L2: KB of its top staged in LDS).
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */
 int rt_ctx_set_tuning(rt_ctx* ctx, const char* key, int64_t value);

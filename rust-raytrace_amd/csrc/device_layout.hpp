@@ -143,6 +143,7 @@ struct DevScene {
     const DevBvhNodeH* bvh_h;       // the binary BVH with binary16 bounds (null: not representable)
     int32_t has_fresnel;            // some object uses FresnelMaterial
     int32_t pfx2, pfx4;             // prefix sources: nodes of the binary / 4-wide tree staged in LDS (set per render)
+    int32_t pfxc;                   // camera source from L2: camera nodes staged in LDS (set per render)
     int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,
                                     // AreaLight, DepthOfFieldCamera)
     int32_t skybox;                 // SkyboxBackground (raytrace.rs:234-256; path kernel only)

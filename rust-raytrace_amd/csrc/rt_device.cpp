@@ -30,7 +30,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -65,6 +65,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)
     {"compact_stack", 1, 0, 1},                  // 32-bit nearest-hit stack entries, 32 of them (src 9; src 6 for half-node trees)
     {"half_nodes", 1, 0, 1},                     // trees beyond LDS: binary16 node bounds for the prefix source (src 5)
+    {"cam_prefix_kb", 64, 0, 120},               // camera nodes from L2 (cam 2): the breadth-first top staged in LDS
 };
 
 }  // namespace
@@ -745,6 +746,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             const int kb2 = static_cast<int>(c->t(kTunePrefixKb2)), kb4 = static_cast<int>(c->t(kTunePrefixKb4));
             c->dsc.pfx2 = static_cast<int32_t>(static_cast<size_t>(std::max(kb2, 1)) * 1024 / sizeof(DevBvhNode));
             c->dsc.pfx4 = static_cast<int32_t>(static_cast<size_t>(std::max(kb4, 1)) * 1024 / (kBvh4Planes * sizeof(DevBvh4Plane)));
+            c->dsc.pfxc = static_cast<int32_t>(static_cast<size_t>(c->t(kTuneCamPrefix)) * 1024 / sizeof(DevCamNode));
             if (src_occ == 13 && kb4 <= 0) src_occ = 11;
         } else {
             src = src_occ = fits_lds ? 1 : 0;

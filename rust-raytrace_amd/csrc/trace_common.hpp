@@ -330,6 +330,8 @@ struct BvhView {
     int32_t* stk;                // this wave's LDS traversal stack (camera sources)
     const DevBvhNodeH* hpnodes;  // half-node prefix source: nodes [0, nl) in LDS (binary16 bounds)
     const DevBvhNodeH* hgnodes;  // ... and the whole half-node tree in HBM/L2
+    const DevCamNode* cng;       // camera nodes [ncl, n) are read here, [0, ncl) from cn (LDS)
+    int32_t ncl;
 };
 
 // LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
@@ -1010,7 +1012,7 @@ __device__ __forceinline__ Hit nearest_camera(const DevScene& sc, const BvhView&
     int32_t cur = sc.bvh_root;
     for (;;) {
         if (cur >= 0) {
-            const DevCamNode n = v.cn[cur];
+            const DevCamNode n = *(cur < v.ncl ? v.cn + cur : v.cng + cur);   // wave-uniform: LDS part or L2
             if constexpr (kCount) w->boxes += go ? 2 : 0;
             const bool o0 = !(n.r0[2] < tx0 || n.r0[0] > tx1 || n.r0[3] < ty0 || n.r0[1] > ty1);
             const bool o1 = !(n.r1[2] < tx0 || n.r1[0] > tx1 || n.r1[3] < ty0 || n.r1[1] > ty1);

@@ -393,6 +393,7 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
     if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
     if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
+    if (kSrc == kSrcCamG) bytes += static_cast<size_t>(min(sc.n_bvh, sc.pfxc)) * sizeof(DevCamNode);
     if (Src<kSrc>::nodes > 0)
         bytes += Src<kSrc>::cam    ? static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode)
                  : Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
@@ -434,12 +435,14 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     if constexpr (Src<kSrc>::cam) {
         v.stk = reinterpret_cast<int32_t*>(lds) + (threadIdx.x >> 6) * kCamStack;
         off = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
-        if constexpr (Src<kSrc>::nodes > 0) {
-            DevCamNode* lc = reinterpret_cast<DevCamNode*>(lds + off);
-            for (int i = threadIdx.x; i < sc.n_bvh; i += T) lc[i] = sc.cam_nodes[i];
-            v.cn = lc;
-            off += static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode);
-        }
+        // every camera node in LDS (kSrcCamL), or the breadth-first top pfxc of them (kSrcCamG)
+        const int32_t nl = Src<kSrc>::nodes > 0 ? sc.n_bvh : min(sc.n_bvh, sc.pfxc);
+        DevCamNode* lc = reinterpret_cast<DevCamNode*>(lds + off);
+        for (int i = threadIdx.x; i < nl; i += T) lc[i] = sc.cam_nodes[i];
+        v.cn = lc;
+        v.ncl = nl;
+        v.cng = sc.cam_nodes;
+        off += static_cast<size_t>(nl) * sizeof(DevCamNode);
     } else if constexpr (kSrc == kSrcLds || kSrc == kSrcGridL) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];

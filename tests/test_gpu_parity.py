@@ -380,7 +380,8 @@ def test_half_node_prefix_source_is_bit_identical(gpu_ctx):
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
     assert np.array_equal(base[1], ref["bgr"])
     assert base[2].rays == ref["counts"]["rays"]
-    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1), dict(split=1)]:
+    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1), dict(split=1),
+               dict(cam_prefix_kb=0), dict(cam_prefix_kb=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

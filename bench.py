@@ -11,26 +11,29 @@ the host gather are reported beside `value`, never in it).
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
 Every N measures the headline config C3 (the N = 1 line is the headline
-number); --config c4 --gpus N gives BASELINE config 4's curve (8192², 10k
-spheres, depth 8, one image tiled across the N GPUs).  --inflight F renders
+number; N > 1 weak-scales it, below); --config c4 --scaling strong --gpus N
+gives BASELINE config 4's curve (8192², 10k spheres, depth 8, one image tiled
+across the N GPUs).  --inflight F renders
 successive steps through F contexts into F output buffers (every step still
 one whole frame, all K finished inside the timed region); the roofline's
 per-render duration then comes from K further renders issued one at a time.
 
 Multi-GPU: run as plain `python bench.py --gpus N` the script starts N rank
 processes itself (before anything touches a GPU), one device each; under
-torchrun it uses the launcher's ranks.  The frame's rows are dealt in 16-row
-bands round-robin over the ranks (libraytrace/shard.py); no collective touches
-the data path (RCCL carries the barrier and the max-over-ranks timing only).
-Default "scaling": "strong": the same 4096^2 frame (BASELINE config 4's "image
-tiled across GPUs"), so value = rays of the whole frame x K / max-over-ranks
-time; --scaling weak renders the same view at sqrt(N) x the resolution (every
-rank the N=1 pixel count).  After the timed region every rank copies its bands
-into ONE shared page-locked host frame (the host gather of SURVEY §8(e)),
-timed and reported as `host_gather`.  --config c4 / c5 select the larger
-configs of BASELINE.json; --config c1 the reference's own scene
-(test_scene.txt: IndirectPhong Cornell box, 1024 random AA samples, 256x256,
-depth 1) on the path kernel.
+torchrun it uses the launcher's ranks.  Pixels are independent (main.rs:45-57),
+so the frame's rows are dealt in 16-row bands round-robin over the ranks
+(libraytrace/shard.py) and no collective touches the data path (RCCL carries
+the barrier and the max-over-ranks timing only).  Default "scaling": "weak"
+(the path partitions, so per-GPU work stays fixed): the same scene and view at
+sqrt(N) x the resolution, every rank rendering a 4096^2-pixel share of it, and
+value = the rays of all ranks x K / max-over-ranks time.  --scaling strong
+deals the N = 1 frame itself over the N ranks (BASELINE config 4's "image tiled
+across GPUs"; per-rank projection on one GPU: --scaling strong --shard-of N).
+After the timed region every rank copies its bands into ONE shared page-locked
+host frame (the host gather of SURVEY §8(e)), timed and reported as
+`host_gather`.  --config c4 / c5 select the larger configs of BASELINE.json;
+--config c1 the reference's own scene (test_scene.txt: IndirectPhong Cornell
+box, 1024 random AA samples, 256x256, depth 1) on the path kernel.
 
 Rays = every Scene::intersect query the reference would issue (camera +
 reflection + shadow), counted by the kernel; identical to the oracle's count
@@ -67,6 +70,9 @@ def parse():
                    help="c3 4096^2/1000 spheres/depth 8 (headline); c4 8192^2/10k/8; c5 16384^2/100k/16; "
                         "c1 test_scene.txt 256^2, 1024 random AA samples, depth 1 (path kernel)")
     p.add_argument("--spp", type=int, default=0, help="c1: AA samples (default: the scene's 1024)")
+    p.add_argument("--view", default="default", choices=["default", "dense"],
+                   help="c3/c4/c5 camera: default (0, 3, 10), 71%% of C3's camera rays miss every sphere; dense: "
+                        "just in front of the sphere box looking in (context line, never the headline)")
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--spheres", type=int, default=0)
@@ -75,15 +81,17 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0,
                    help="target CPU time of the cpu_baseline samples (split between 1 thread and all threads)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                   help="N > 1: strong = the N=1 frame dealt over N ranks (default); weak = the frame side "
-                        "grows by sqrt(N) (same scene and view, every rank renders the N=1 pixel count)")
+    p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                   help="N > 1: weak (default) = the frame side grows by sqrt(N) (same scene and view, row bands "
+                        "dealt round-robin, every rank renders the N=1 pixel count); strong = the N=1 frame dealt "
+                        "over N ranks")
     p.add_argument("--shard-of", type=int, default=0,
                    help="(diagnostic, one process) render only rank 0's row bands of an N-rank frame; "
                         "its time is what each rank of an N-GPU run spends")
     p.add_argument("--no-kernel-times", action="store_true",
                    help="skip the instrumented frames that time every launch with HIP events")
     p.add_argument("--no-gather", action="store_true", help="skip the host-gather measurement")
+    p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive rt_render measurement")
     p.add_argument("--inflight", type=int, default=1,
                    help="frames in flight: F contexts (each its own working set and streams) render successive "
                         "steps into F output buffers, so frame i+1's first generations overlap frame i's tail "
@@ -203,15 +211,26 @@ def cpu_baseline(spec, args, **draws):
 
 # ---------------------------------------------------------------- helpers
 
-def pmc_traffic(config_key):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/), or None."""
+def pmc_traffic(config_key, sources_id):
+    """HBM bytes per render from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), and where the
+    figure comes from.  Reported only when that entry was measured on these
+    native sources (sources_id) with the default tuning; otherwise None and
+    the reason (a stale figure is never passed off as this run's)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        e = d.get(config_key)
-        return float(e["hbm_bytes_per_launch"]) if e else None
+        e = json.load(open(path)).get(config_key)
     except Exception:
-        return None
+        e = None
+    if not e:
+        return None, "no committed PMC measurement for this config"
+    if e.get("sources_id") != sources_id:
+        return None, (f"stale: profiles/pmc_traffic.json[{config_key}] was measured on sources "
+                      f"{e.get('sources_id')}, this build is {sources_id}")
+    if e.get("tuning") or os.environ.get("RT_TUNE"):
+        return None, "tuning differs from the measured default schedule"
+    return float(e["hbm_bytes_per_launch"]), (f"profiles/pmc_traffic.json[{config_key}]: rocprofv3 --pmc FETCH_SIZE x2 "
+                                              f"+ WRITE_SIZE, one render, same sources ({sources_id})")
 
 
 class SharedFrame:
@@ -295,6 +314,14 @@ def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
     return best, pinned
 
 
+def weak_frame(w, h, n):
+    """Weak scaling over n ranks: the same view at sqrt(n) x the resolution,
+    sides rounded to whole 16-row bands, so each rank renders (up to that
+    rounding) the N = 1 frame's pixel count."""
+    f = n ** 0.5
+    return max(BAND, int(round(w * f / BAND)) * BAND), max(BAND, int(round(h * f / BAND)) * BAND)
+
+
 # ---------------------------------------------------------------- main
 
 def main():
@@ -358,13 +385,10 @@ def main():
     path_cfg = args.config == "c1"
     args.width = args.width or cfg[0]
     args.height = args.height or cfg[0]
+    base_wh = (args.width, args.height)
     band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
     if band_world > 1 and args.scaling == "weak":
-        # weak scaling: the same view at sqrt(N) x the resolution, so each of the N ranks renders
-        # (up to rounding to whole bands) the N=1 frame's pixel count
-        f = band_world ** 0.5
-        args.width = max(BAND, int(round(args.width * f / BAND)) * BAND)
-        args.height = max(BAND, int(round(args.height * f / BAND)) * BAND)
+        args.width, args.height = weak_frame(args.width, args.height, band_world)
     args.spheres = args.spheres or cfg[1]
     args.depth = cfg[2] if args.depth < 0 else args.depth
     if path_cfg:
@@ -373,14 +397,14 @@ def main():
             spec.antialias = args.spp
     else:
         spec = scenes.random_spheres(args.spheres, args.width, args.height, args.depth, seed=cfg[3],
-                                     box_scale=cfg[4], name=args.config)
+                                     box_scale=cfg[4], name=args.config, view=args.view)
     spp = spec.antialias
     jitter = lr.RT_JITTER_RANDOM if path_cfg else lr.RT_JITTER_CENTER
     W, H = spec.width, spec.height
     assert H % BAND == 0, "bench frames are whole bands"
     scene = lr.Scene.deserialize(spec.to_text())
     F = max(1, args.inflight)
-    ctxs = [lr.Context(local) for _ in range(F)]
+    ctxs = [lr.Context(local, tuning="env") for _ in range(F)]
     for c in ctxs:
         c.upload(scene)
     ctx = ctxs[0]
@@ -466,14 +490,14 @@ def main():
     # PCIe-inclusive rate: rt_render into reused pageable host buffers, kernels + D2H.
     # Reported beside `value`, never as it.
     host = {}
-    if world == 1:
+    if world == 1 and not args.no_pcie:
         hb = np.zeros((len(rows), pitch), np.uint8)
         hr = np.zeros((len(rows), W, 3), np.float32)
         for name, out in (("bgr", (None, hb)), ("rgb_bgr", (hr, hb))):
             ms = []
             for _ in range(3):
                 t0h = time.perf_counter()
-                ctx.render(opts, out=out)
+                ctx.render(opts, out=out, stats=False)
                 ms.append((time.perf_counter() - t0h) * 1e3)
             host[name] = min(ms)
 
@@ -500,8 +524,9 @@ def main():
         scene_bytes = args.spheres * (32 + 4) + args.spheres * 128 + 2 * 56
         algo_bytes = pixels_local * (12 + 3) + scene_bytes          # f32 RGB + u8 BGR writes + scene read once
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-        key = f"{args.config}_{W}x{H}_n{args.spheres}_d{args.depth}"
-        traffic = pmc_traffic(key) if world == 1 else None
+        key = f"{args.config}_{W}x{H}_n{args.spheres}_d{args.depth}" + ("_dense" if args.view == "dense" else "")
+        traffic, traffic_source = pmc_traffic(key, lr.sources_id()) if world == 1 else \
+            (None, "per-rank PMC traffic is measured at N = 1 only")
         kernels = {}
         for fam, (ms, n) in ktimes.items():
             if n:
@@ -518,14 +543,22 @@ def main():
                         f"samples per pixel (keyed draws, seed {cfg[3]}), depth {args.depth}")
             metric = f"Mrays/sec at {W}x{H}, test_scene.txt, {spp} AA samples, depth {args.depth}"
         else:
+            cam_txt = ("camera at (0, 3, 10) looking into the sphere box" +
+                       (" (71% of the camera rays miss every sphere)" if args.config == "c3" else "")
+                       if args.view == "default" else
+                       "dense view: camera at (0, 3.15, -0.5) inside the front of the sphere box looking in")
             workload = (f"{args.config.upper()}: {W}x{H}, {args.spheres} random Phong spheres, 2 point lights, "
-                        f"depth {args.depth}, {spp} spp centre jitter (seed {cfg[3]}); camera at (0, 3, 10) "
-                        f"looking into the sphere box" +
-                        (" (71% of the camera rays miss every sphere)" if args.config == "c3" else "") +
-                        (f"; one image tiled across {world} GPUs" if args.scaling == "strong" and world > 1 else ""))
-            metric = ("Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline"
-                      if (args.config, W, H) == ("c3", 4096, 4096)
-                      else f"Mrays/sec at {W}x{H}, {args.spheres} spheres, depth {args.depth}")
+                        f"depth {args.depth}, {spp} spp centre jitter (seed {cfg[3]}); {cam_txt}" +
+                        (f"; one image tiled across {world} GPUs" if args.scaling == "strong" and world > 1 else "") +
+                        (f"; weak scaling: the same view at {W}x{H} dealt in {BAND}-row bands over {world} GPUs, "
+                         f"each rank a {base_wh[0]}x{base_wh[1]}-pixel share" if args.scaling == "weak" and world > 1
+                         else ""))
+            # weak scaling of the headline: every rank renders a 4096^2-pixel share (the N = 1 frame)
+            headline = args.config == "c3" and args.spheres == 1000 and args.depth == 8 and args.view == "default" and (
+                (W, H) == (4096, 4096) or (args.scaling == "weak" and band_world > 1 and base_wh == (4096, 4096)))
+            metric = ("Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline" if headline
+                      else f"Mrays/sec at {W}x{H}, {args.spheres} spheres, depth {args.depth}" +
+                      (" (dense view)" if args.view == "dense" else ""))
         line = {
             "metric": metric,
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": n_gpus, "steps": args.steps,
@@ -538,7 +571,7 @@ def main():
                        "algo": args.algo},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_source,
                          "kernel": "path_kernel" if path_kernel else
                                    "whole render (wavefront launches)" if args.algo in ("auto", "wavefront") else
                                    "trace_frame_kernel", "avg_kernel_ms": round(avg_kernel_ms, 4),

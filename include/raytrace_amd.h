@@ -219,6 +219,8 @@ typedef struct {
     uint64_t shadow_box_tests, shadow_sphere_tests;   /* the shadow-query share of the two above */
     uint64_t traced_rays;     /* queries the device actually traced: `rays` / spp when a chain schedule
                                  renders spp identical centre-jitter samples once, else `rays` */
+    uint64_t chunks;          /* row chunks the wavefront schedule ran the tile as (sized to the
+                                 working-set budget, tuning wf_budget_mb); 0 for other schedules */
 } rt_stats;
 
 void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height);
@@ -256,13 +258,16 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 
 /* Schedule tuning of a context (A/B measurement; the defaults are the measured
  * best).  Keys (rt_tuning_key(i) for i = 0, 1, ... until NULL):
- * chunk_pixels (wavefront chunk cap, 0: an 80 GB working set), bvh_leaf, light_grids, light_grid_res
+ * chunk_pixels (wavefront chunk cap, 0: from the working-set budget), bvh_leaf, light_grids, light_grid_res
  * (these three take effect at the next rt_scene_upload), src, src_occ,
  * prefix_kb, prefix4_kb, lanes, stagger_gen, regions, split, bstreams, fuse,
  * lists, cam, deal, spread_below, lists0, path_group, cu_mask, prio, verbose,
  * grid_occ, fuse_from, compact_stack (small trees: 32-bit nearest-hit stack entries),
  * half_nodes (trees beyond LDS: binary16 node bounds for the prefix walk),
- * cam_prefix_kb (camera view read through L2: KB of its top staged in LDS).
+ * cam_prefix_kb (camera view read through L2: KB of its top staged in LDS),
+ * wf_budget_mb (wavefront working set of all chunk lanes, MB; 0: min(80 GB, 85%
+ * of the device's free memory); a hipMalloc that still fails halves the chunks).
+ * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */
 int rt_ctx_set_tuning(rt_ctx* ctx, const char* key, int64_t value);

@@ -8,6 +8,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -30,7 +33,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -38,14 +41,16 @@ struct TuneDef {
 };
 // -1 in src / src_occ / cam / split: chosen per scene
 constexpr TuneDef kTune[kTuneCount] = {
-    {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what kWfBudget of working set holds at the depth)
+    {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what the working-set budget holds at the depth)
     {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
     {"light_grids", 1, 0, 1},                    // light-view grids for point-light shadow queries
     {"light_grid_res", 0, 0, 4096},              // 0: from the median sphere's angular size
     {"src", -1, -1, 13},                         // nearest-hit sphere source (trace_kernel.hip kSrc*)
     {"src_occ", -1, -1, 13},                     // shadow sphere source
-    {"prefix_kb", 64, 1, 160},                   // LDS prefix of the binary tree (KB) for trees that do not fit
-    {"prefix4_kb", 0, 0, 160},                   // LDS prefix of the 4-wide tree (0: read through L2)
+    // LDS prefixes stay <= 150 KB: with the queue counters (<= 8.4 KB at 2048 regions) a
+    // workgroup's LDS then fits gfx950's 160 KB
+    {"prefix_kb", 64, 1, 150},                   // LDS prefix of the binary tree (KB) for trees that do not fit
+    {"prefix4_kb", 0, 0, 150},                   // LDS prefix of the 4-wide tree (0: read through L2)
     {"lanes", 1, 1, 8},                          // chunk lanes (each its own streams and working set)
     {"stagger_gen", 1, 0, 64},                   // lanes: chunk c+1 starts after this generation of chunk c
     {"regions", 0, 0, 2048},                     // regions per queue (0: 2 x CUs)
@@ -66,7 +71,100 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"compact_stack", 1, 0, 1},                  // 32-bit nearest-hit stack entries, 32 of them (src 9; src 6 for half-node trees)
     {"half_nodes", 1, 0, 1},                     // trees beyond LDS: binary16 node bounds for the prefix source (src 5)
     {"cam_prefix_kb", 64, 0, 120},               // camera nodes from L2 (cam 2): the breadth-first top staged in LDS
+    {"wf_budget_mb", 0, 0, INT32_MAX},           // wavefront working set of all lanes together (MB; 0: min(80 GB,
+                                                 // 85% of the device's free memory)); chunks are sized to it
 };
+
+}  // namespace
+
+namespace {
+
+// Host threads that move pinned staging slices into the caller's pageable
+// buffer (rt_render): created once per context, so a frame's copy does not pay
+// thread start-up per slice.  copy() splits one memcpy into kParts parts
+// shared by the workers and the calling thread (one thread copies pinned ->
+// pageable memory at ~20-28 GB/s, below the DMA's 56 GB/s).  Workers spin
+// briefly for the next slice before sleeping, so consecutive slices of a frame
+// do not pay a wake-up each.
+class HostCopyPool {
+public:
+    ~HostCopyPool() {
+        stop_.store(true);
+        {
+            std::lock_guard<std::mutex> g(m_);
+        }
+        cv_.notify_all();
+        for (std::thread& t : th_) t.join();
+    }
+    void copy(void* to, const void* from, size_t len) {
+        if (th_.empty()) start();
+        const size_t parts = std::max<size_t>(1, std::min<size_t>(kParts, len >> 20));   // >= 1 MiB each
+        if (parts == 1) { std::memcpy(to, from, len); return; }
+        to_ = static_cast<uint8_t*>(to);
+        from_ = static_cast<const uint8_t*>(from);
+        len_ = len;
+        parts_ = parts;
+        step_ = (len + parts - 1) / parts;
+        done_.store(0);
+        next_.store(0);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        work();
+        while (done_.load(std::memory_order_acquire) != parts) std::this_thread::yield();
+    }
+
+private:
+    static constexpr size_t kParts = 8;
+    void start() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned n = std::min<unsigned>(kParts - 1, hw > 1 ? hw - 1 : 1u);
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    void work() {                       // take parts until none is left
+        for (;;) {
+            const size_t q = next_.fetch_add(1);
+            if (q >= parts_) return;
+            const size_t a = q * step_, b = std::min(len_, a + step_);
+            if (a < b) std::memcpy(to_ + a, from_ + a, b - a);
+            done_.fetch_add(1, std::memory_order_release);
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            for (int spin = 0; g == seen && !stop_.load() && spin < 20000; ++spin) {
+                std::this_thread::yield();
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (stop_.load()) return;
+            seen = g;
+            work();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    uint8_t* to_ = nullptr;
+    const uint8_t* from_ = nullptr;
+    size_t len_ = 0, parts_ = 0, step_ = 0;
+    std::atomic<size_t> next_{0}, done_{0};
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<bool> stop_{false};
+};
+
+constexpr int kMaxBands = 16;           // row bands of one rt_render copied as they finish
+constexpr int kFoldBands = 8;           // bands of a one-chunk frame (its fold split in eight launches)
+constexpr int kRing = 4;                // pinned staging slices in flight
+constexpr size_t kSlice = 8u << 20;     // bytes per staging slice
 
 }  // namespace
 
@@ -119,9 +217,17 @@ struct rt_ctx {
     hipEvent_t render_done = nullptr; // end of the last render on its stream: the next one waits for it
     bool render_pending = false;
     uint32_t last_spp_traced = 1;     // chain schedules trace one of spp identical centre-jitter samples
-    // rt_render: two pinned staging slices for the device -> host copy of the outputs
-    void* pin[2] = {nullptr, nullptr};
-    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    uint32_t last_chunks = 0;         // wavefront chunks of the last render (0: other schedules)
+    // rt_render: pinned staging slices for the device -> host copy of the outputs, a copy
+    // stream that waits for each finished row band, and the host threads that empty the slices
+    void* pin[kRing] = {};
+    hipEvent_t pin_ev[kRing] = {};
+    hipStream_t copy_stream = nullptr;
+    bool want_bands = false;               // set by rt_render around its render: fold in bands, events after each
+    int n_bands = 0;                       // bands of the last render (0: copy after render_done)
+    hipEvent_t band_ev[kMaxBands] = {};
+    uint32_t band_row0[kMaxBands] = {}, band_nrows[kMaxBands] = {};
+    HostCopyPool pool;
     int64_t tune[kTuneCount];
     std::string err;
     rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
@@ -201,6 +307,50 @@ int ensure_bstreams(rt_ctx* c, rt_ctx::Lane& M, int nb) {
     return RT_OK;
 }
 
+// Free every lane (streams, events, working set) once its work is done.  Used
+// by rt_ctx_destroy, by rt_ctx_set_tuning when a key that shapes the streams
+// (cu_mask, prio) changes, and before a render retries with smaller chunks.
+void drop_lane_memory(rt_ctx::Lane& L) {
+    if (L.s) (void)hipStreamSynchronize(L.s);
+    for (hipStream_t x : L.sb) if (x) (void)hipStreamSynchronize(x);
+    if (L.mem) (void)hipFree(L.mem);
+    L.mem = nullptr;
+    L.bytes = 0;
+}
+
+void drop_lanes(rt_ctx* c) {
+    for (auto& L : c->lanes) {
+        drop_lane_memory(L);
+        if (L.mark) (void)hipEventDestroy(L.mark);
+        if (L.done) (void)hipEventDestroy(L.done);
+        for (hipEvent_t e : L.b_done) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
+        if (L.s) (void)hipStreamDestroy(L.s);
+        for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
+    }
+    c->lanes.clear();
+}
+
+// Working-set bytes per pixel slot of a chunk (ensure_wf's sections, per slot):
+// two queues, one shade-record array and one level array per lit generation,
+// terminals, shadow item lists.
+uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
+    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4;
+}
+
+// Default working-set budget of a render (all lanes): 85% of what the device
+// has free plus what this context's lanes already hold, at most kWfBudget.
+uint64_t default_wf_budget(rt_ctx* c) {
+    size_t fr = 0, total = 0;
+    uint64_t held = 0;
+    for (const auto& L : c->lanes) held += L.bytes;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+        (void)hipGetLastError();
+        return kWfBudget;
+    }
+    return std::min<uint64_t>(kWfBudget, static_cast<uint64_t>(0.85 * static_cast<double>(fr + held)));
+}
+
 int ensure_lanes(rt_ctx* c, int n) {
     while (static_cast<int>(c->lanes.size()) < n) {
         rt_ctx::Lane L;
@@ -253,7 +403,13 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         }
         L.mem = nullptr;
         L.bytes = 0;
-        HIP_TRY(c, hipMalloc(&L.mem, off));
+        const hipError_t e = hipMalloc(&L.mem, off);
+        if (e == hipErrorOutOfMemory) {          // the caller retries with smaller chunks
+            (void)hipGetLastError();
+            L.mem = nullptr;
+            return fail(c, RT_E_NOMEM, "wavefront working set of " + std::to_string(off >> 20) + " MB does not fit");
+        }
+        if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(wavefront working set)");
         L.bytes = off;
     }
     b.mem = static_cast<unsigned char*>(L.mem);
@@ -322,23 +478,16 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->d_path) (void)hipFree(c->d_path);
     if (c->d_rgb) (void)hipFree(c->d_rgb);
     if (c->d_bgr) (void)hipFree(c->d_bgr);
-    for (auto& L : c->lanes) {
-        if (L.s) (void)hipStreamSynchronize(L.s);
-        for (hipStream_t x : L.sb) if (x) (void)hipStreamSynchronize(x);
-        if (L.mem) (void)hipFree(L.mem);
-        if (L.mark) (void)hipEventDestroy(L.mark);
-        if (L.done) (void)hipEventDestroy(L.done);
-        for (hipEvent_t e : L.b_done) if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
-        if (L.s) (void)hipStreamDestroy(L.s);
-        for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
-    }
+    drop_lanes(c);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     if (c->render_done) (void)hipEventDestroy(c->render_done);
-    for (int i = 0; i < 2; ++i) {
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (int i = 0; i < kRing; ++i) {
         if (c->pin[i]) (void)hipHostFree(c->pin[i]);
         if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
     }
+    for (hipEvent_t e : c->band_ev) if (e) (void)hipEventDestroy(e);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -695,6 +844,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
     c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
     c->last_stream = st;
     c->last_spp_traced = 1;
+    c->last_chunks = 0;
+    c->n_bands = 0;
     if (o->tile_w == 0 || o->tile_h == 0) {
         c->last_timed = false;
         HIP_TRY(c, hipEventRecord(c->render_done, st));
@@ -751,37 +902,6 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         } else {
             src = src_occ = fits_lds ? 1 : 0;
         }
-        // chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles)
-        // (balanced: a frame slightly over the cap becomes two halves, not a full chunk plus a
-        // sliver that pays every generation's launch latency again)
-        // default chunk cap: the pixels whose working set (ensure_wf: queues, one shade-record
-        // array and one level array per lit generation, terminals) fits kWfBudget, e.g. 69 M px
-        // at depth 8 (C4's 8192^2 frame in one chunk: 62.8 vs 63.9 ms as two) and 39 M px at depth 16
-        uint64_t cap_px = static_cast<uint64_t>(c->t(kTuneChunkPixels));
-        if (cap_px == 0) {
-            const uint64_t levels = o->max_depth + 1ull;
-            const uint64_t per_px = 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * 4;
-            cap_px = std::max<uint64_t>(1ull << 20, kWfBudget / per_px);
-        }
-        uint32_t chunk_rows = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(cap_px / o->tile_w, UINT32_MAX) / 8 * 8));
-        chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
-        const uint32_t n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
-        chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);
-        const int n_lanes = std::max(1, std::min<int>(static_cast<int>(c->t(kTuneLanes)), static_cast<int>(n_chunks)));
-        const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));
-        int rc2 = ensure_lanes(c, n_lanes);
-        if (rc2 != RT_OK) return rc2;
-        const uint32_t tiles_x = (o->tile_w + 7) / 8;
-        const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
-        const uint32_t cap = o->tile_w * chunk_rows;
-        // G regions = workgroups per queue launch: two per CU, i.e. every
-        // workgroup resident at once (1024 threads with the LDS-staged BVH),
-        // so the wave-chunk dealing spreads even a small tail queue over the
-        // whole chip in one round; fewer for small chunks; R covers every slot.
-        const int g_env = static_cast<int>(c->t(kTuneRegions));
-        uint32_t G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
-        G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
-        const uint32_t R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
         // tuning "split" 0: every kernel on one in-order stream (A/B measurement);
         // "deal": 1 workgroup-major chunk dealing (default), 0 workgroup-first;
         // "bstreams": streams for the shadow + shading kernels (default 2;
@@ -816,14 +936,86 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d short_stack %d split %d pfx %d/%d\n",
                          src, src_occ, cam, nlists, c->deep_bvh4 ? 1 : 0, c->short_stack ? 1 : 0, split ? 1 : 0,
                          c->dsc.pfx2, c->dsc.pfx4);
-        for (int l = 0; l < n_lanes; ++l) {
-            if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
-            rc2 = ensure_wf(c, c->lanes[l], cap, G, R, o->max_depth + 1, nlists);
+        // Chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles), sized so
+        // the lanes' working sets (ensure_wf: queues, one shade-record array and one
+        // level array per lit generation, terminals, shadow lists) fit the budget:
+        // tuning "wf_budget_mb", else min(80 GB, 85% of the free device memory)
+        // (hipMemGetInfo), e.g. C4's 8192^2 frame in one chunk at depth 8 (62.8 vs
+        // 63.9 ms as two) and C5 in 7 at depth 16.  Balanced: a frame slightly over
+        // the cap becomes two halves, not a full chunk plus a sliver that pays every
+        // generation's launch latency again.  If hipMalloc still runs out of memory
+        // (another context, a caller's buffers), the chunks are halved and the
+        // allocation retried; results do not depend on the chunking.
+        const uint64_t levels = o->max_depth + 1ull;
+        const int lanes_req = static_cast<int>(c->t(kTuneLanes));
+        uint64_t cap_px = static_cast<uint64_t>(c->t(kTuneChunkPixels));
+        if (cap_px == 0) {
+            const uint64_t budget = c->t(kTuneWfBudgetMb) > 0 ? static_cast<uint64_t>(c->t(kTuneWfBudgetMb)) << 20
+                                                               : default_wf_budget(c);
+            cap_px = std::max<uint64_t>(1, budget / static_cast<uint64_t>(lanes_req) / wf_bytes_per_slot(levels, nlists));
+        }
+        const uint32_t tiles_x = (o->tile_w + 7) / 8;
+        const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));
+        uint32_t chunk_rows = 0, n_chunks = 0, G = 1, R = 0;
+        int n_lanes = 1;
+        for (;;) {
+            chunk_rows = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(cap_px / o->tile_w, UINT32_MAX) / 8 * 8));
+            chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
+            n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
+            chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);
+            n_lanes = std::max(1, std::min<int>(lanes_req, static_cast<int>(n_chunks)));
+            int rc2 = ensure_lanes(c, n_lanes);
             if (rc2 != RT_OK) return rc2;
+            const uint32_t slots = tiles_x * 64 * (chunk_rows / 8);
+            const uint32_t cap = o->tile_w * chunk_rows;
+            // G regions = workgroups per queue launch: two per CU, i.e. every
+            // workgroup resident at once (1024 threads with the LDS-staged BVH),
+            // so the wave-chunk dealing spreads even a small tail queue over the
+            // whole chip in one round; fewer for small chunks; R covers every slot.
+            const int g_env = static_cast<int>(c->t(kTuneRegions));
+            G = g_env > 0 ? static_cast<uint32_t>(g_env) : 2u * static_cast<uint32_t>(c->n_cu);
+            G = std::max<uint32_t>(1, std::min<uint32_t>({G, static_cast<uint32_t>(kMaxRegions), (slots + kWfThreads - 1) / kWfThreads}));
+            R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
+            for (int l = 0; l < n_lanes && rc2 == RT_OK; ++l) {
+                if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
+                rc2 = ensure_wf(c, c->lanes[l], cap, G, R, static_cast<uint32_t>(levels), nlists);
+            }
+            if (rc2 == RT_OK) break;
+            if (rc2 != RT_E_NOMEM || chunk_rows <= 8) return rc2;
+            for (auto& L : c->lanes) drop_lane_memory(L);      // retry with half the pixels per chunk
+            cap_px = std::max<uint64_t>(1, static_cast<uint64_t>(chunk_rows) * o->tile_w / 2);
+        }
+        for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
         }
+        c->last_chunks = n_chunks;
+        // rt_render copies row bands as their fold finishes: a one-chunk frame folds in
+        // kFoldBands bands, a multi-chunk one gets an event per chunk
+        int fold_bands = 1;
+        c->n_bands = 0;
+        if (c->want_bands && n_chunks <= static_cast<uint32_t>(kMaxBands)) {
+            const uint32_t nb = n_chunks == 1 ? static_cast<uint32_t>(kFoldBands) : n_chunks;
+            for (uint32_t i = 0; i < nb; ++i)
+                if (!c->band_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->band_ev[i], hipEventDisableTiming));
+            if (n_chunks == 1) {
+                fold_bands = kFoldBands;
+                const uint32_t br = (o->tile_h + kFoldBands - 1) / kFoldBands;   // as launch_wavefront splits
+                for (int i = 0; i < kFoldBands; ++i) {
+                    c->band_row0[i] = std::min(o->tile_h, i * br);
+                    c->band_nrows[i] = std::min(o->tile_h, c->band_row0[i] + br) - c->band_row0[i];
+                }
+            } else {
+                for (uint32_t i = 0; i < n_chunks; ++i) {
+                    c->band_row0[i] = i * chunk_rows;
+                    c->band_nrows[i] = std::min(chunk_rows, o->tile_h - c->band_row0[i]);
+                }
+            }
+            c->n_bands = static_cast<int>(nb);
+        }
+        if (c->t(kTuneVerbose))
+            std::fprintf(stderr, "rtamd: chunks %u x %u rows, lanes %d, G %u, R %u\n", n_chunks, chunk_rows, n_lanes, G, R);
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
         // per-launch timing needs one in-order stream
         const bool timed = (o->flags & RT_TIME_KERNELS) != 0 && n_lanes == 1;
@@ -865,6 +1057,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
             // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
             ws.fuse_from = static_cast<int>(c->t(kTuneFuseFrom));
+            ws.fold_bands = fold_bands;
+            ws.fold_ev = c->n_bands == 0 ? nullptr : (n_chunks == 1 ? c->band_ev : &c->band_ev[ci]);
             ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
                               ? (static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere) <= 64 * 1024 ? 1 : 2)
                               : 0;
@@ -942,6 +1136,7 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     s->shadow_sphere_tests = h[kTotals + 5];
     s->pixels = c->last_pixels;
     s->traced_rays = c->last_spp_traced > 1 ? s->rays / c->last_spp_traced : s->rays;
+    s->chunks = c->last_chunks;
     if (c->last_timed) {
         float ms = 0.f;
         HIP_TRY(c, hipEventSynchronize(c->ev1));
@@ -981,50 +1176,70 @@ int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
     return RT_OK;
 }
 
-// Device -> caller-owned host memory.  A page-locked destination gets the DMA
-// directly; pageable memory goes through two pinned slices, the copy engine
-// filling one while host threads move the other out.
-static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t bytes) {
+// Device -> caller-owned host memory, row band by row band: the copy stream
+// waits for each band's fold (c->band_ev, recorded by the render when
+// c->want_bands was set; otherwise for the whole render), so the PCIe transfer
+// of the first bands overlaps the fold of the later ones.  A page-locked
+// destination gets the DMA directly; pageable memory goes through kRing pinned
+// slices of kSlice bytes, the copy engine filling slices ahead while the host
+// pool empties them in order.  `pitch`: bytes per output row.
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uint32_t rows) {
+    const size_t bytes = pitch * rows;
     if (!bytes) return RT_OK;
+    if (!c->copy_stream) {
+        // a CU-masked stream (mask = every CU) gets a hardware queue of its own (ensure_bstreams),
+        // so the copies never queue behind the fold launches of the render's stream
+        std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
+        for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+        if (hipExtStreamCreateWithCUMask(&c->copy_stream, static_cast<uint32_t>(mask.size()), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        }
+    }
+    struct Piece { size_t off, len; int band; };
+    std::vector<Piece> pieces;
+    const int nb = c->n_bands > 0 ? c->n_bands : 1;
+    for (int bi = 0; bi < nb; ++bi) {
+        const size_t a = c->n_bands > 0 ? c->band_row0[bi] * pitch : 0;
+        const size_t e = c->n_bands > 0 ? (static_cast<size_t>(c->band_row0[bi]) + c->band_nrows[bi]) * pitch : bytes;
+        for (size_t o = a; o < e; o += kSlice) pieces.push_back(Piece{o, std::min(kSlice, e - o), bi});
+    }
+    auto wait_band = [&](int bi) -> hipError_t {
+        return hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[bi] : c->render_done, 0);
+    };
+    const auto* s8 = static_cast<const uint8_t*>(src);
+    auto* d8 = static_cast<uint8_t*>(dst);
     hipPointerAttribute_t attr{};
     if (hipPointerGetAttributes(&attr, dst) == hipSuccess && attr.type == hipMemoryTypeHost) {
-        HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        int last = -1;
+        for (const Piece& pc : pieces) {
+            if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
+            HIP_TRY(c, hipMemcpyAsync(d8 + pc.off, s8 + pc.off, pc.len, hipMemcpyDeviceToHost, c->copy_stream));
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
         return RT_OK;
     }
     (void)hipGetLastError();                       // a pageable pointer is not an error
-    constexpr size_t kSlice = 16u << 20;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kRing; ++i) {
         if (!c->pin[i]) HIP_TRY(c, hipHostMalloc(&c->pin[i], kSlice, hipHostMallocDefault));
         if (!c->pin_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
     }
-    auto drain = [&](size_t slice) {               // host copy of slice `slice` out of its pinned buffer
-        const size_t off = slice * kSlice, len = std::min(kSlice, bytes - off);
-        const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-        const size_t parts = std::max<size_t>(1, std::min<size_t>(hw, len >> 21));   // >= 2 MiB per thread
-        const size_t step = (len + parts - 1) / parts;
-        const auto* from = static_cast<const uint8_t*>(c->pin[slice & 1]);
-        auto* to = static_cast<uint8_t*>(dst) + off;
-        std::vector<std::thread> th;
-        for (size_t p = 1; p < parts; ++p) {
-            const size_t a = p * step, b = std::min(len, a + step);
-            if (a < b) th.emplace_back([=] { std::memcpy(to + a, from + a, b - a); });
+    const size_t n = pieces.size();
+    size_t issued = 0, drained = 0;
+    int last = -1;
+    while (drained < n) {
+        while (issued < n && issued - drained < static_cast<size_t>(kRing)) {   // slot issued % kRing is free
+            const Piece& pc = pieces[issued];
+            if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
+            const int slot = static_cast<int>(issued % kRing);
+            HIP_TRY(c, hipMemcpyAsync(c->pin[slot], s8 + pc.off, pc.len, hipMemcpyDeviceToHost, c->copy_stream));
+            HIP_TRY(c, hipEventRecord(c->pin_ev[slot], c->copy_stream));
+            ++issued;
         }
-        std::memcpy(to, from, std::min(len, step));
-        for (std::thread& t : th) t.join();
-    };
-    const size_t n = (bytes + kSlice - 1) / kSlice;
-    for (size_t i = 0; i <= n; ++i) {
-        if (i < n) {                                // slot i & 1 was drained in iteration i - 1
-            const size_t off = i * kSlice, len = std::min(kSlice, bytes - off);
-            HIP_TRY(c, hipMemcpyAsync(c->pin[i & 1], static_cast<const uint8_t*>(src) + off, len,
-                                      hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipEventRecord(c->pin_ev[i & 1], c->stream));
-        }
-        if (i >= 1) {
-            HIP_TRY(c, hipEventSynchronize(c->pin_ev[(i - 1) & 1]));
-            drain(i - 1);
-        }
+        const int slot = static_cast<int>(drained % kRing);
+        HIP_TRY(c, hipEventSynchronize(c->pin_ev[slot]));
+        c->pool.copy(d8 + pieces[drained].off, c->pin[slot], pieces[drained].len);
+        ++drained;
     }
     return RT_OK;
 }
@@ -1052,10 +1267,15 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
         HIP_TRY(c, hipMalloc(&c->d_bgr, bgr_bytes));
         c->bgr_cap = bgr_bytes;
     }
+    // an earlier rt_render's copies (copy stream) must be done with d_rgb / d_bgr: they are, since
+    // copy_to_host returns only once its last piece has been drained or synchronised
+    c->want_bands = true;
     rc = render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
+    c->want_bands = false;
     if (rc != RT_OK) return rc;
-    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, bgr_bytes)) != RT_OK) return rc;
-    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, rgb_bytes)) != RT_OK) return rc;
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, o->tile_h)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(o->tile_w) * 3 * sizeof(float), o->tile_h)) != RT_OK)
+        return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (stats) return rt_ctx_stats(c, stats);
     return RT_OK;
@@ -1072,6 +1292,13 @@ int rt_ctx_set_tuning(rt_ctx* c, const char* key, int64_t value) {
         if (std::strcmp(key, kTune[i].name) != 0) continue;
         if (value < kTune[i].lo || value > kTune[i].hi)
             return fail(c, RT_E_INVALID, std::string("tuning ") + key + " out of range");
+        // cu_mask and prio shape the lanes' streams, which are created once: rebuild
+        // the lanes (after their work is done) so the next render uses the new value
+        if ((i == kTuneCuMask || i == kTunePrio) && value != c->tune[i] && !c->lanes.empty()) {
+            if (hipSetDevice(c->device) != hipSuccess) return fail(c, RT_E_HIP, "hipSetDevice failed");
+            if (c->render_pending) (void)hipEventSynchronize(c->render_done);
+            drop_lanes(c);
+        }
         c->tune[i] = value;
         return RT_OK;
     }

@@ -971,14 +971,16 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
 // kStaged: each workgroup's 256 pixels lie in one output row (tile_w % 256
 // == 0, BGR rows unpadded and dword aligned): the workgroup assembles its
 // 3 KiB of RGB and 768 B of BGR in LDS and stores them as whole dwords.
+// Pixels [pix0, pix1) of the chunk: the whole chunk, or one row band of it
+// when the caller copies the output to the host band by band (rt_render).
 template <bool kStaged, bool kFresnel>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t pix0, uint32_t pix1) {
     __shared__ float s_rgb[3 * kBlock];
     __shared__ uint32_t s_bgr[3 * kBlock / 4];
     __shared__ double s_srgb[255];
     for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
-    const uint32_t npix = fp.tile_w * fp.rows;
-    const uint32_t base = blockIdx.x * kBlock;
+    const uint32_t npix = pix1;
+    const uint32_t base = pix0 + blockIdx.x * kBlock;
     const uint32_t p = base + threadIdx.x;
     const uint8_t nlev = p < npix ? b.nlev()[p] : kNlevDone;
     // pixels marked done were written by wf_nearest; a workgroup of them has nothing to do
@@ -1190,16 +1192,28 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const hipStream_t s = ws.a;
     const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
                         (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
-    const dim3 gf(static_cast<uint32_t>((static_cast<uint64_t>(fp.tile_w) * fp.rows + kBlock - 1) / kBlock));
-    if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
-    if (sc.has_fresnel) {
-        if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
-        else hipLaunchKernelGGL((wf_fold<false, true>), gf, dim3(kBlock), 0, s, sc, fp, b);
-    } else {
-        if (staged) hipLaunchKernelGGL((wf_fold<true, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
-        else hipLaunchKernelGGL((wf_fold<false, false>), gf, dim3(kBlock), 0, s, sc, fp, b);
+    // the fold in ws.fold_bands row bands when the caller copies band by band (an event
+    // after each: that band's output is final); band boundaries are whole rows, so with
+    // tile_w % 256 == 0 every band starts on a 256-pixel boundary (the staged fold's rows)
+    const uint32_t nbands = ws.fold_ev ? static_cast<uint32_t>(max(1, ws.fold_bands)) : 1u;
+    const uint32_t band_rows = (fp.rows + nbands - 1) / nbands;
+    for (uint32_t bi = 0; bi < nbands; ++bi) {
+        const uint32_t r0 = min(fp.rows, bi * band_rows), r1 = min(fp.rows, r0 + band_rows);
+        if (r1 > r0) {
+            const uint32_t p0 = r0 * fp.tile_w, p1 = r1 * fp.tile_w;
+            const dim3 gf((p1 - p0 + kBlock - 1) / kBlock);
+            if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
+            if (sc.has_fresnel) {
+                if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
+                else hipLaunchKernelGGL((wf_fold<false, true>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
+            } else {
+                if (staged) hipLaunchKernelGGL((wf_fold<true, false>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
+                else hipLaunchKernelGGL((wf_fold<false, false>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
+            }
+            if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
+        }
+        if (ws.fold_ev && (e = hipEventRecord(ws.fold_ev[bi], s)) != hipSuccess) return e;
     }
-    if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
     if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);
     if (ws.ma && (e = ws.ma->mark(s, kKfTally)) != hipSuccess) return e;

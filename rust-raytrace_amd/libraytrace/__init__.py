@@ -83,7 +83,8 @@ class rt_render_opts(C.Structure):
 class rt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64),
                 ("kernel_ms", C.c_double), ("box_tests", C.c_uint64), ("sphere_tests", C.c_uint64),
-                ("shadow_box_tests", C.c_uint64), ("shadow_sphere_tests", C.c_uint64), ("traced_rays", C.c_uint64)]
+                ("shadow_box_tests", C.c_uint64), ("shadow_sphere_tests", C.c_uint64), ("traced_rays", C.c_uint64),
+                ("chunks", C.c_uint64)]
 
 
 def _load():
@@ -282,6 +283,21 @@ def render_opts(width, height, **kw):
     return o
 
 
+def sources_id():
+    """16 hex digits identifying the native sources (csrc/ and include/) this
+    checkout builds: ties committed profile figures (profiles/pmc_traffic.json)
+    to the kernels they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for d in (os.path.join(pkg, "csrc"), os.path.join(os.path.dirname(pkg), "include")):
+        for name in sorted(os.listdir(d)):
+            h.update(name.encode())
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def tuning_keys():
     keys, i = [], 0
     while True:
@@ -292,26 +308,34 @@ def tuning_keys():
         i += 1
 
 
-def env_tuning():
+def env_tuning(text=None):
     """Tuning from RT_TUNE="key=value,key=value" (a convenience of this binding
-    for A/B tools; the library itself never reads the environment)."""
+    for A/B tools, read only when asked: Context(tuning="env"); the library
+    itself never reads the environment).  Malformed items raise ValueError."""
+    text = os.environ.get("RT_TUNE", "") if text is None else text
     out = {}
-    for item in filter(None, os.environ.get("RT_TUNE", "").split(",")):
-        k, v = item.split("=")
-        out[k.strip()] = int(v)
+    for item in filter(None, (x.strip() for x in text.split(","))):
+        k, sep, v = item.partition("=")
+        if not sep or not k.strip():
+            raise ValueError(f"RT_TUNE item {item!r} is not key=value")
+        try:
+            out[k.strip()] = int(v)
+        except ValueError:
+            raise ValueError(f"RT_TUNE item {item!r}: value is not an integer") from None
     return out
 
 
 class Context:
     """One device (rt_ctx).  Mirrors the reference's main.rs render step.
-    tuning: {key: value} schedule knobs (rt_ctx_set_tuning); None = RT_TUNE."""
+    tuning: {key: value} schedule knobs (rt_ctx_set_tuning); "env" = the RT_TUNE
+    environment variable (A/B tools); None = the library's defaults."""
 
     def __init__(self, device=0, tuning=None):
         h = C.c_void_p()
         _check(lib.rt_ctx_create(device, C.byref(h)))
         self._h = h
         self.device = device
-        for k, v in (env_tuning() if tuning is None else tuning).items():
+        for k, v in (env_tuning() if tuning == "env" else (tuning or {})).items():
             self.set_tuning(k, v)
 
     def set_tuning(self, key, value):
@@ -325,10 +349,11 @@ class Context:
     def upload(self, scene):
         _check(lib.rt_scene_upload(self._h, scene.handle), self._h)
 
-    def render(self, opts, rgb=True, bgr=True, out=None):
+    def render(self, opts, rgb=True, bgr=True, out=None, stats=True):
         """Synchronous render of opts' tile into host numpy arrays.
         Returns (rgb float32 [tile_h, tile_w, 3] or None, bgr uint8 [tile_h, pitch] or None, stats).
-        out: (rgb, bgr) arrays to reuse (either None to skip that output)."""
+        out: (rgb, bgr) arrays to reuse (either None to skip that output); stats=False passes
+        no rt_stats (the drop-in call of INTEGRATION.md: no counter read-back), returns None."""
         pitch = opts.bgr_pitch or 3 * opts.tile_w
         if out is not None:
             out_rgb, out_bgr = out
@@ -340,11 +365,11 @@ class Context:
         else:
             out_rgb = np.zeros((opts.tile_h, opts.tile_w, 3), np.float32) if rgb else None
             out_bgr = np.full((opts.tile_h, pitch), 0xCD, np.uint8) if bgr else None
-        st = rt_stats()
+        st = rt_stats() if stats else None
         rc = lib.rt_render(self._h, C.byref(opts),
                            out_rgb.ctypes.data_as(C.POINTER(C.c_float)) if rgb else None,
                            out_bgr.ctypes.data_as(C.POINTER(C.c_uint8)) if bgr else None,
-                           C.byref(st))
+                           C.byref(st) if stats else None)
         _check(rc, self._h)
         return out_rgb, out_bgr, st
 

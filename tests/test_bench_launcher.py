@@ -24,7 +24,7 @@ def test_gpus_two_spawns_two_ranks(backend):
     d = json.loads(lines[0])
     assert d["ranks"] == 2
     assert d["n_gpus"] == d["devices_visible"] == 0
-    assert d["scaling"] == "strong"
+    assert d["scaling"] == "weak"              # the path partitions: per-GPU work fixed as N grows
     assert d["config"] == "c3"                  # every N measures the headline config
 
 
@@ -38,6 +38,20 @@ def test_config_defaults(monkeypatch):
         monkeypatch.setattr(sys, "argv", argv)
         a = bench.parse()
         assert (a.config, a.gpus) == (cfg, gpus)
+
+
+def test_weak_scaling_keeps_the_per_rank_share():
+    """Weak scaling: every rank of an N-GPU run renders (within band rounding)
+    the 4096^2 pixels of the N = 1 headline frame, dealt in 16-row bands."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "rust-raytrace_amd")]
+    import bench
+    from libraytrace import shard
+    for n in (1, 2, 4, 8):
+        w, h = bench.weak_frame(4096, 4096, n) if n > 1 else (4096, 4096)
+        assert w % 16 == 0 and h % 16 == 0
+        for r in range(n):
+            px = len(shard.local_rows(h, bench.BAND, n, r)) * w
+            assert abs(px / 4096 ** 2 - 1) < 0.01, (n, r, px)
 
 
 def test_cpu_baseline_sample_is_bounded():

@@ -441,7 +441,8 @@ def test_kernel_times(gpu_ctx):
     assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
     # shading runs in its own kernel unless the context is tuned fuse=1 (then inside the shadow kernels)
     assert kt["shade"][1] in (0, 2 * (gens - 1))
-    assert kt["fold"][1] == 2 and kt["tally"][1] == 2
+    # rt_render folds a one-chunk frame in 8 row bands (each copied to the host as it finishes)
+    assert kt["fold"][1] == 2 * 8 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
     assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested
 
@@ -495,6 +496,9 @@ def test_multi_chunk_schedule_matches_oracle(gpu_ctx, lanes):
         one = gpu_ctx.render(o)
         with _with_tuning(gpu_ctx, chunk_pixels=256 * 16, lanes=lanes):
             many = gpu_ctx.render(o)
+        with _with_tuning(gpu_ctx, chunk_pixels=256 * 8, lanes=lanes):      # > 16 chunks: copied after the render
+            many8 = gpu_ctx.render(o)
+        assert np.array_equal(many8[1], one[1]) and np.array_equal(many8[0].view(np.uint32), one[0].view(np.uint32))
         assert np.array_equal(many[1], one[1])
         assert np.array_equal(many[0].view(np.uint32), one[0].view(np.uint32))
         assert many[2].rays == one[2].rays and many[2].shadow_rays == one[2].shadow_rays
@@ -503,6 +507,39 @@ def test_multi_chunk_schedule_matches_oracle(gpu_ctx, lanes):
         assert np.array_equal(many[1], ref["bgr"])
         check_close(many[0], ref["rgb64"])
         assert many[2].rays == ref["counts"]["rays"]
+
+
+def test_working_set_budget_splits_chunks_bit_identically(gpu_ctx):
+    """The wavefront working set is sized from a budget (tuning wf_budget_mb;
+    default: the device's free memory): a C4-workload tile (10k spheres, depth
+    8) under a small budget runs as several row chunks, bit-identical to the
+    one-chunk render."""
+    spec = scenes.config4(1024, 768)
+    base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert base[2].chunks == 1
+    with _with_tuning(gpu_ctx, wf_budget_mb=100):
+        got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    assert got[2].chunks > 2, got[2].chunks
+    assert np.array_equal(got[1], base[1])
+    assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32))
+    assert got[2].rays == base[2].rays and got[2].shadow_rays == base[2].shadow_rays
+
+
+def test_oversized_budget_falls_back_to_smaller_chunks():
+    """A budget beyond the device's 288 GB (the whole 16384^2 depth-16 tile in
+    one chunk needs ~0.5 TB): hipMalloc fails, the render halves its chunks
+    until the working set fits, and the image equals the default schedule's.
+    Own context, closed at the end (its working set is large)."""
+    spec = scenes.random_spheres(40, 16384, 16384, 16, seed=11, name="sparse")
+    o = lr.render_opts(16384, 16384, max_depth=16, spp=1, algo=lr.RT_ALGO_WAVEFRONT)
+    with lr.Context(0) as ctx:
+        ctx.upload(lr.Scene.deserialize(spec.to_text()))
+        _, ref, st0 = ctx.render(o, rgb=False)
+    with lr.Context(0, tuning={"wf_budget_mb": 600_000}) as ctx:
+        ctx.upload(lr.Scene.deserialize(spec.to_text()))
+        _, got, st = ctx.render(o, rgb=False)
+    assert st.chunks >= 2
+    assert np.array_equal(got, ref) and st.rays == st0.rays
 
 
 def test_tuning_knobs_do_not_change_results(gpu_ctx):

@@ -12,7 +12,7 @@ from libraytrace import scenes
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 D = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 spec = scenes.random_spheres(1000, W, W, D, seed=3, name="c3")
-ctx = lr.Context(0)
+ctx = lr.Context(0, tuning="env")
 ctx.upload(lr.Scene.deserialize(spec.to_text()))
 prev = None
 print("depth  nearest  shadow  box/nearest  sph/nearest  box/shadow  sph/shadow")

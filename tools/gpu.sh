@@ -11,6 +11,7 @@
 #                                              summary <name>.stats.txt and the last frame's timeline
 #                                              <name>.timeline.txt
 #   run:<name>:[ENV=v ...] <command>          any other GPU command (e.g. python3 tools/stamp_probe.py) -> <name>.log
+#   pmcx:<name>:<counters>:<program args>      ONE --pmc pass over another program (the binary itself after --)
 #   pmc:<name>:<counters, space separated>:<bench.py args>   ONE --pmc pass (--kernel-trace only)
 #                                              -> <name>/ and a per-kernel summary <name>.txt
 #
@@ -81,6 +82,15 @@ for step in "$@"; do
     [ $rc -eq 0 ] || { echo "pmc $name rc=$rc"; tail -5 "$O/$name.log"; exit $rc; }
     python3 tools/pmc_summary.py "$O/$name" > "$O/$name.txt" 2>&1
     echo "pmc $name ($ctrs) ok"
+    ;;
+  pmcx)
+    name=${rest%%:*}; r2=${rest#*:}; ctrs=${r2%%:*}; cmd=${r2#*:}
+    timeout -s KILL 300 rocprofv3 --pmc $ctrs --kernel-trace -d "$O/$name/p1" -o run --output-format csv -- \
+        $cmd > "$O/$name.log" 2>&1
+    rc=$?
+    [ $rc -eq 0 ] || { echo "pmcx $name rc=$rc"; tail -5 "$O/$name.log"; exit $rc; }
+    python3 tools/pmc_summary.py "$O/$name" > "$O/$name.txt" 2>&1
+    echo "pmcx $name ($ctrs) ok"
     ;;
   run)
     name=${rest%%:*}; split_env "${rest#*:}"

@@ -70,7 +70,12 @@ def main():
         doc = json.load(open(out_path))
     except Exception:
         doc = {}
+    import os
+    sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rust-raytrace_amd")]
+    import libraytrace
     doc[key] = {"hbm_bytes_per_launch": total, "launch": "one render (all wavefront launches of one frame)",
+                "sources_id": libraytrace.sources_id(), "tuning": os.environ.get("RT_TUNE", ""),
                 "per_kernel_family": kernels,
                 "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace only; "
                           "KiB -> bytes; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section); "

@@ -24,7 +24,7 @@ def deep_chain():
 
 
 for name, spec in (("deep_chain", deep_chain()), ("c3", scenes.config3(64, 64)), ("c4", scenes.config4(64, 64))):
-    with lr.Context(0) as ctx:
+    with lr.Context(0, tuning="env") as ctx:
         ctx.set_tuning("verbose", 1)
         ctx.upload(lr.Scene.deserialize(spec.to_text()))
         print(name, flush=True)

@@ -51,7 +51,7 @@ def main():
     chunks = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     per = {}
     for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
-        for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+        for f in sorted(glob.glob(f"{root}/**/run_counter_collection.csv", recursive=True)):
             fr = frames(f, counter)
             if len(fr) >= chunks:
                 acc = collections.defaultdict(float)

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <new>
@@ -135,8 +136,10 @@ private:
     void loop() {
         uint64_t seen = 0;
         for (;;) {
+            // spin at most ~200 us for the next slice (the DMA of one slice takes ~150 us), then sleep
             uint64_t g = gen_.load(std::memory_order_acquire);
-            for (int spin = 0; g == seen && !stop_.load() && spin < 20000; ++spin) {
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(200);
+            while (g == seen && !stop_.load() && std::chrono::steady_clock::now() < until) {
                 std::this_thread::yield();
                 g = gen_.load(std::memory_order_acquire);
             }

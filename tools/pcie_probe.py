@@ -64,6 +64,23 @@ def main():
     hpn = hp.numpy()
     ctx.render(o, out=(None, hpn))
     print(f"rt_render, BGR to page-locked host memory: {best(lambda: ctx.render(o, out=(None, hpn), stats=False)):.3f} ms")
+    # the bench's context history before its PCIe-inclusive measurement
+    pg = lambda oo: best(lambda: ctx.render(oo, out=(None, hb), stats=False), 3)
+    ob = lr.render_opts(4096, 4096, max_depth=8, spp=1, tile_h=4096, band=16, band_stride=1, band_phase=0)
+    print(f"  band=16 opts: {pg(ob):.3f} ms")
+    ot = lr.render_opts(4096, 4096, max_depth=8, spp=1, flags=o.flags | lr.RT_TIME_KERNELS)
+    for _ in range(3):
+        ctx.render_device(ot, out_rgb.data_ptr(), out_bgr.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    ctx.kernel_times()
+    print(f"  after RT_TIME_KERNELS renders: {pg(o):.3f} ms")
+    oc = lr.render_opts(4096, 4096, max_depth=8, spp=1, flags=o.flags | lr.RT_COUNT_WORK)
+    ctx.render_device(oc, out_rgb.data_ptr(), out_bgr.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    ctx.stats()
+    print(f"  after an RT_COUNT_WORK render: {pg(o):.3f} ms")
+    hb2 = np.zeros((4096, 3 * 4096), np.uint8)
+    print(f"  fresh pageable buffer (first touch inside): {pg(o):.3f} ms")
     ctx.close()
 
 

@@ -266,7 +266,11 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * half_nodes (trees beyond LDS: binary16 node bounds for the prefix walk),
  * cam_prefix_kb (camera view read through L2: KB of its top staged in LDS),
  * wf_budget_mb (wavefront working set of all chunk lanes, MB; 0: min(80 GB, 85%
- * of the device's free memory); a hipMalloc that still fails halves the chunks).
+ * of the device's free memory); a hipMalloc that still fails halves the chunks),
+ * tail_from / tail_max (trees that fit LDS: nearest-hit generations >= tail_from
+ * hand queues of <= tail_max rays to a walk with four lanes per ray on the 4-wide
+ * tree; tail_from 0 off, -1 auto: 5 for chunks of <= 32 x tail_max pixels;
+ * tail_max 0: CUs x 256).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -267,6 +267,8 @@ struct WfBufs {
     uint32_t spread_below;          // queues below this many items are dealt workgroup-first regardless
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
+    int32_t tail_from;              // > 0: nearest-hit generations >= this of a src-9 tree: queues of
+    uint32_t tail_max;              //   <= tail_max rays go to the quad kernel (src 17), the rest to src 9
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }

@@ -34,7 +34,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -74,6 +74,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"cam_prefix_kb", 64, 0, 120},               // camera nodes from L2 (cam 2): the breadth-first top staged in LDS
     {"wf_budget_mb", 0, 0, INT32_MAX},           // wavefront working set of all lanes together (MB; 0: min(80 GB,
                                                  // 85% of the device's free memory)); chunks are sized to it
+    {"tail_from", -1, -1, 99},                   // nearest-hit generations >= this (src 9 trees) hand queues of <= tail_max
+                                                 // rays to the quad walk; 0 off, -1: 5 for chunks of <= 32 x tail_max slots
+    {"tail_max", 0, 0, INT32_MAX},               // 0: CUs x 256 (one quad-walk round: one workgroup of 256 rays per CU)
 };
 
 }  // namespace
@@ -181,6 +184,7 @@ struct rt_ctx {
     DevScene dsc{};
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
+    bool quad_ok = false;            // the quad walk's LDS stack holds the 4-wide tree's deepest walk (compact codes)
     bool short_stack = false;        // binary tree fits the compact nearest-hit stack (16-bit codes, depth <= 32)
     bool short_stack18 = false;      // ... with 18-bit codes (the binary16 prefix source, src 6)
     bool all_lights_gridded = false; // every light is a point light with a light-view grid
@@ -632,6 +636,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     // traversal stacks hold 64 entries (trace_common.hpp kBvhStack / kBvh4Stack)
     if (bvh_depth(bvh) > 64) return fail(c, RT_E_UNSUPPORTED, "sphere BVH deeper than the traversal stack");
     c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
+    c->quad_ok = bvh4_stack_need(bvh4) <= 48 && bvh4.n_nodes < 32768 && spheres.size() <= 4096;
     // compact stack (trace_common.hpp kShortStack, stk_entry16): the stack never holds more
     // entries than the deepest inner node's depth; node indices and leaf codes
     // (first << 3 | count - 1) must fit a signed 16-bit field
@@ -988,7 +993,19 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             for (auto& L : c->lanes) drop_lane_memory(L);      // retry with half the pixels per chunk
             cap_px = std::max<uint64_t>(1, static_cast<uint64_t>(chunk_rows) * o->tile_w / 2);
         }
+        // the quad walk for the late generations' small queues (trace_kernel.hip kSrcBvh4Q):
+        // by default for chunks small enough that those queues fit one round of it
+        const uint32_t tail_max = c->t(kTuneTailMax) > 0 ? static_cast<uint32_t>(c->t(kTuneTailMax))
+                                                         : static_cast<uint32_t>(c->n_cu) * 256u;
+        int tail_from = static_cast<int>(c->t(kTuneTailFrom));
+        // (auto: from generation 5 in chunks of <= 32 x tail_max slots, e.g. one rank's
+        // share of an 8-way C3 frame: 0.943 -> 0.879 ms; a 4-way share, whose
+        // generations 5 and 6 still hold more rays than that, measured 2% slower)
+        if (tail_from < 0) tail_from = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8) <= 32ull * tail_max ? 5 : 0;
+        if (src != 9 || !c->quad_ok) tail_from = 0;
         for (int l = 0; l < n_lanes; ++l) {
+            c->lanes[l].b.tail_from = tail_from;
+            c->lanes[l].b.tail_max = tail_max;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));

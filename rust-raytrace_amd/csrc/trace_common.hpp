@@ -124,6 +124,7 @@ struct Work {
     uint32_t boxes = 0, spheres = 0;
 #if RT_STAMP
     unsigned long long cyc[3] = {0, 0, 0};     // RT_STAMP builds: nearest_bvh_bl's descend / leaf / pop loops
+    uint32_t wsteps[3] = {0, 0, 0};            // ... and the wave's iterations of them (counted by its first active lane)
 #endif
 };
 #if RT_STAMP
@@ -132,8 +133,13 @@ struct Work {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
         v = __builtin_amdgcn_s_memtime();                                         \
     } while (0)
+#define RT_WSTEP(i) \
+    do {                                                                          \
+        if (static_cast<unsigned>(__builtin_amdgcn_readfirstlane(__lane_id())) == __lane_id()) ++w->wsteps[i]; \
+    } while (0)
 #else
 #define RT_WSTAMP(v) ((void)0)
+#define RT_WSTEP(i) ((void)0)
 #endif
 
 template <bool kCount = false, class SpherePtr>
@@ -332,6 +338,7 @@ struct BvhView {
     const DevBvhNodeH* hgnodes;  // ... and the whole half-node tree in HBM/L2
     const DevCamNode* cng;       // camera nodes [ncl, n) are read here, [0, ncl) from cn (LDS)
     int32_t ncl;
+    uint32_t* lstk;              // quad source: this ray's LDS stack (entry i at lstk[i * kQuadStride])
 };
 
 // LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
@@ -575,6 +582,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     for (;;) {
         RT_WSTAMP(q0);
         while (cur >= 0) {
+            RT_WSTEP(0);
             float t0, t1;
             bool h0, h1;
             int32_t c0, c1;
@@ -606,6 +614,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
+                RT_WSTEP(1);
                 double t;
                 if (sphere_t(v.sph[k], r, a2, a4, t)) {
                     const int32_t obj = v.obj[k];
@@ -619,6 +628,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
         RT_WSTAMP(q2);
         cur = kNone;
         while (stk_n > 0) {
+            RT_WSTEP(2);
             const StkE e = stk_pop();
             if (e_t(e) <= tlim) { cur = e_node(e); break; }
         }
@@ -852,6 +862,112 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
             cur = stk_node(e);
             if (stk_t(e) <= tlim) break;
         }
+    }
+}
+
+// Quad-cooperative walk of the 4-wide tree in LDS (the small queues of the
+// late generations, where the launch lasts as long as its slowest walk): the
+// four lanes of a quad carry the same ray, lane q tests child slot q of each
+// node, and the quad exchanges the four entry distances through DPP
+// quad_perm moves.  Every lane then takes the same decisions: continue with
+// the nearest hit child (ties: lowest slot), push the other hit children
+// far-first onto the ray's stack in LDS (each lane writes its own entry), and
+// pop past the entries the current best rules out.  Leaf spheres are dealt
+// over the quad (lane q tests first + q, first + q + 4) and the quad's best
+// (t, object) merges into the ray's best: the same lexicographic minimum the
+// sequential loop finds (nearest_bvh4), so the winner does not depend on the
+// split.  Compact 16-bit stack entries (trees of <= 4096 spheres, host
+// checked); `stk` is the ray's LDS stack, entry i at stk[i * kQuadStride].
+constexpr int kQuadStack = 48;                       // entries per ray (host: bvh4_stack_need <= this)
+constexpr int kQuadStride = kWfThreads / 4;          // rays per workgroup
+template <int kPerm>
+__device__ __forceinline__ int32_t quad_mov(int32_t x) { return __builtin_amdgcn_mov_dpp(x, kPerm, 0xF, 0xF, false); }
+template <int kPerm>
+__device__ __forceinline__ float quad_mov(float x) { return __int_as_float(quad_mov<kPerm>(__float_as_int(x))); }
+template <int kPerm>
+__device__ __forceinline__ double quad_mov(double x) {
+    const int64_t u = __double_as_longlong(x);
+    const int32_t lo = quad_mov<kPerm>(static_cast<int32_t>(u)), hi = quad_mov<kPerm>(static_cast<int32_t>(u >> 32));
+    return __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
+}
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kQuadXor3 = 0x1B;   // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]
+
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_quad(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    const int32_t q = static_cast<int32_t>(threadIdx.x & 3u);
+    const int32_t N = v.n4;
+    const Sel4 sel = make_sel4(rb, N);
+    uint32_t* const stk = v.lstk;
+    int sp = 0;
+    constexpr int32_t kNone = INT32_MIN;
+    int32_t cur = sc.bvh4_root;
+    for (;;) {
+        while (cur >= 0) {
+            const float* P = reinterpret_cast<const float*>(v.p4 + cur) + q;      // plane k: P[4 * k * N]
+            const float tn = fmaxf(fmaxf(slab_t(P[4 * sel.x], rb.ix, rb.nox), slab_t(P[4 * (2 * N + sel.y)], rb.iy, rb.noy)),
+                                   slab_t(P[4 * (4 * N + sel.z)], rb.iz, rb.noz));
+            const float tf = fminf(fminf(slab_t(P[4 * (N - sel.x)], rb.ix, rb.nox), slab_t(P[4 * (3 * N - sel.y)], rb.iy, rb.noy)),
+                                   slab_t(P[4 * (5 * N - sel.z)], rb.iz, rb.noz));
+            const int32_t c = reinterpret_cast<const int32_t*>(P)[4 * 6 * N];
+            if constexpr (kCount) w->boxes += c != kBvh4Empty ? 1u : 0u;
+            const float n = widen_lo(tn), f = widen_hi(tf);
+            const bool hit = n <= f && f >= 0.0f && n <= tlim && c != kBvh4Empty;
+            const float t = hit ? n : __builtin_inff();
+            const float t1 = quad_mov<kQuadXor1>(t), t2 = quad_mov<kQuadXor2>(t), t3 = quad_mov<kQuadXor3>(t);
+            const int32_t c1 = quad_mov<kQuadXor1>(c), c2 = quad_mov<kQuadXor2>(c), c3 = quad_mov<kQuadXor3>(c);
+            const int32_t q1 = q ^ 1, q2 = q ^ 2, q3 = q ^ 3;
+            // this lane's rank among the quad's entries (t, slot), and the nearest one
+            const int rank = (t1 < t || (t1 == t && q1 < q)) + (t2 < t || (t2 == t && q2 < q)) + (t3 < t || (t3 == t && q3 < q));
+            const int hits = (t < __builtin_inff()) + (t1 < __builtin_inff()) + (t2 < __builtin_inff()) + (t3 < __builtin_inff());
+            float bt = t;
+            int32_t bq = q, bc = c;
+            if (t1 < bt || (t1 == bt && q1 < bq)) { bt = t1; bq = q1; bc = c1; }
+            if (t2 < bt || (t2 == bt && q2 < bq)) { bt = t2; bq = q2; bc = c2; }
+            if (t3 < bt || (t3 == bt && q3 < bq)) { bt = t3; bq = q3; bc = c3; }
+            if (hit && rank > 0) stk[(sp + hits - 1 - rank) * kQuadStride] = stk_entry_c<16>(c, t);
+            sp += hits > 0 ? hits - 1 : 0;
+            cur = hits > 0 ? bc : kNone;
+        }
+        if (cur != kNone) {
+            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+            double lt = __builtin_inf();
+            int32_t lo = INT32_MAX, lp = -1;
+            for (int k = first + q; k < first + cnt; k += 4) {
+                if constexpr (kCount) ++w->spheres;
+                double t;
+                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                    const int32_t obj = v.obj[k];
+                    if (t < lt || (t == lt && obj < lo)) { lt = t; lo = obj; lp = k; }
+                }
+            }
+            {
+                const double ot = quad_mov<kQuadXor1>(lt);
+                const int32_t oo = quad_mov<kQuadXor1>(lo), op = quad_mov<kQuadXor1>(lp);
+                if (ot < lt || (ot == lt && oo < lo)) { lt = ot; lo = oo; lp = op; }
+            }
+            {
+                const double ot = quad_mov<kQuadXor2>(lt);
+                const int32_t oo = quad_mov<kQuadXor2>(lo), op = quad_mov<kQuadXor2>(lp);
+                if (ot < lt || (ot == lt && oo < lo)) { lt = ot; lo = oo; lp = op; }
+            }
+            if (lt < h.t || (lt == h.t && lo < h.obj)) {
+                h.t = lt; h.obj = lo; h.prim = lp;
+                tlim = t_limit(lt);
+            }
+        }
+        cur = kNone;
+        while (sp > 0) {
+            --sp;
+            const uint32_t e = stk[sp * kQuadStride];
+            if (stk_t_c<16>(e) <= tlim) { cur = stk_node_c<16>(e); break; }
+        }
+        if (cur == kNone) return h;
     }
 }
 

@@ -39,12 +39,18 @@ __constant__ double c_srgb_avg[255];
 // wait, [k][0] setup (region scan + LDS staging), [1] ray load + region entry,
 // [2] traversal, [3] finish (records, rays, terminals), [4] chunks, [5] waves;
 // the counting kernels add [6] the slowest lane's and [7] all lanes' node
-// visits per chunk (divergence).  Read with rt_debug_stamps (this build only).
+// visits per chunk (divergence); [8..10] the traversal's descend / leaf / pop
+// loops (wave-cycles), [12] the slowest wave's traversal cycles, [13..15] the
+// waves' iterations of those three loops.  Read with rt_debug_stamps (this
+// build only).
 #ifndef RT_STAMP
 #define RT_STAMP 0
 #endif
 #if RT_STAMP
+// (fields 12.. in a second array: a [kMaxGenerations][16] array hits a gfx950
+// backend error, "Operand has incorrect register class")
 __device__ unsigned long long g_stamp[kMaxGenerations][12];
+__device__ unsigned long long g_stamp2[kMaxGenerations][4];
 #define RT_STAMP_AT(v)                                                            \
     do {                                                                          \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
@@ -189,9 +195,9 @@ __device__ __forceinline__ uint32_t wave_slot(const WfBufs& b, uint32_t n) {
 }
 
 // Whether this workgroup's first chunk is below n (workgroup-uniform).
-__device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n) {
+__device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n, uint32_t width = 64) {
     const uint64_t first = deal_major(b, n) ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
-    return first * 64u < n;
+    return first * width < n;
 }
 
 #define RT_FOR_CHUNKS(b, n, j)                                                              \
@@ -334,6 +340,11 @@ constexpr int kSrcBvhG = 2;         // binary BVH from HBM/L2
 constexpr int kSrcBvhL = 4;         // binary BVH + spheres in LDS
 constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
 constexpr int kSrcBvhL8C = 9;       // kSrcBvhL8 with compact 32-bit stack entries (small trees, depth <= kShortStack)
+// The 4-wide tree + spheres in LDS walked by quads of lanes (nearest_quad),
+// the rays' stacks in LDS: one workgroup per CU (up to 128 VGPRs), for the
+// small queues of the late generations, whose launches last as long as their
+// slowest walk (WfBufs::tail_from / tail_max)
+constexpr int kSrcBvh4Q = 17;
 constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
 constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
 constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
@@ -359,16 +370,17 @@ struct Src {
     static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
     static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
     static constexpr bool bvh = kSrc >= kSrcBvhG && !grid;
-    static constexpr bool wide = kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P;
+    static constexpr bool quad = kSrc == kSrcBvh4Q;
+    static constexpr bool wide = (kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P) || quad;
     static constexpr bool half = kSrc == kSrcBvhPH || kSrc == kSrcBvhPHC;
     static constexpr int compact_bits = kSrc == kSrcBvhL8C ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
     static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P || half;
     static constexpr bool compact = kSrc == kSrcBvhL8C;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
-                                    kSrc == kSrcCamL;
+                                    kSrc == kSrcCamL || quad;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL;
     static constexpr int nodes = all_lds ? 2 : half ? 3 : prefix ? 1 : 0;
-    static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4) || half ? 8 : 4;   // min waves per SIMD
+    static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 && !quad) || half ? 8 : 4;   // min waves per SIMD
 };
 
 // Per-wave traversal stack of the camera sources (wave-uniform entries).
@@ -399,7 +411,9 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
                  : Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
                                    : node_planes_bytes(sc.n_bvh);
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
-    return (bytes + 15) / 16 * 16;
+    bytes = (bytes + 15) / 16 * 16;
+    if (Src<kSrc>::quad) bytes += static_cast<size_t>(kQuadStack) * kQuadStride * sizeof(uint32_t);
+    return bytes;
 }
 
 // Stage what the source keeps in LDS (the whole tree and the spheres); returns
@@ -465,6 +479,10 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
         v.sph = ls;
         v.obj = lo;
+        if constexpr (Src<kSrc>::quad) {                 // the rays' stacks after the spheres
+            const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
+            v.lstk = reinterpret_cast<uint32_t*>(lds + at) + (threadIdx.x >> 2);
+        }
     }
     return v;
 }
@@ -475,7 +493,8 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
 #endif
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
-    if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
+    if constexpr (Src<kSrc>::quad) return nearest_quad<kCount>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL)
@@ -681,7 +700,14 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         region_scan(b.rq() + k * b.G, b.G, ql.scan, ql.wave);
         n = ql.scan[b.G];
     }
-    if (!wg_has_work(b, n)) {                  // nothing dealt here: publish empty regions, free the CU
+    // quad walk: 16 rays per wave; chunks of 16 rays when every wave takes at most one
+    // (a workgroup then appends <= 256 entries), else 64-ray chunks in four passes
+    constexpr bool kQuad = Src<kSrc>::quad;
+    // tail generations: the quad kernel takes queues of <= tail_max rays, the
+    // regular one the rest (both are launched; the other returns at once)
+    if (!kCam && b.tail_from > 0 && k >= b.tail_from && (n <= b.tail_max) != kQuad) return;
+    const uint32_t width = kQuad && n <= b.G * (kWfThreads / 4) ? 16u : 64u;
+    if (!wg_has_work(b, n, width)) {           // nothing dealt here: publish empty regions, free the CU
         if (threadIdx.x == 0) { b.rs()[k * b.G + blockIdx.x] = 0; b.rq()[(k + 1) * b.G + blockIdx.x] = 0; }
         if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = 0;
         return;
@@ -693,7 +719,10 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     Work w;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
     const size_t rbase = static_cast<size_t>(k) * b.qcap + obase;
-    RT_FOR_CHUNKS(b, n, j) {
+    for (uint32_t rt_c = wave_slot(b, n), rt_w = b.G * (kWfThreads / 64); static_cast<uint64_t>(rt_c) * width < n;
+         rt_c += rt_w)
+    for (uint32_t sub = 0; sub < (kQuad ? width / 16u : 1u); ++sub) {
+        const uint32_t j = kQuad ? rt_c * width + sub * 16u + ((threadIdx.x & 63u) >> 2) : rt_c * 64u + (threadIdx.x & 63u);
         RT_STAMP_AT(st0);
         [[maybe_unused]] const uint32_t visits0 = w.boxes;
         Ray r{};
@@ -728,7 +757,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         }
         RT_STAMP_AT(st2);
-        finish_nearest<kCam, kFresnel, kLists>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
+        finish_nearest<kCam, kFresnel, kLists>(sc, fp, b, v.sph, k, live && (!kQuad || (threadIdx.x & 3u) == 0), r, sig, p, h,
+                                               ql.count, obase, rbase);
         RT_STAMP_AT(st3);
 #if RT_STAMP
         acc[1] += st1 - st0; acc[2] += st2 - st1; acc[3] += st3 - st2; acc[4] += 1;
@@ -750,7 +780,14 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         for (int q = 0; q < 5; ++q) atomicAdd(&g_stamp[k][q], acc[q]);
         atomicAdd(&g_stamp[k][5], 1ull);
         for (int q = 0; q < 3; ++q) atomicAdd(&g_stamp[k][8 + q], w.cyc[q]);
+        atomicMax(&g_stamp2[k][0], acc[2]);
     }
+    for (int q = 0; q < 3; ++q) {
+        unsigned long long ws = w.wsteps[q];
+        for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamp2[k][1 + q], ws);
+    }
+
 #endif
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1071,13 +1108,21 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     hipError_t e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
 #define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR, false>), grid, block, \
-                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
 #define RT_NEARL(S, FR) hipLaunchKernelGGL((wf_nearest<S, false, kCount, FR, true>), grid, block, \
-                                           staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+                                           staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
     // shadow lists from generation 1 on (generation 0 feeds every (record, light) pair to the plain shadow kernel)
 #define RT_NEARC(S, FR, L) hipLaunchKernelGGL((wf_nearest<S, true, kCount, FR, L>), grid, block, \
-                                              staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+                                              staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
     const bool lists = b.nlists != 0 && (k >= 1 || ws.lists0);
+    // generations >= b.tail_from of an all-LDS compact-stack tree: the quad kernel is
+    // launched before the regular one and takes the queue when it holds <= b.tail_max
+    // rays (decided on the device, where the size is); when the quad kernel's LDS
+    // does not fit a workgroup (160 KB) the regular kernel alone takes every queue
+    const bool quad = kSrcN == kSrcBvhL8C && b.tail_from > 0 && k >= b.tail_from && k >= 1 && sc.bvh4 != nullptr &&
+                      staged_bytes<kSrcBvh4Q>(sc) + queue_lds_bytes(b.G) <= 160u * 1024u;
+    WfBufs bn = b;
+    if (!quad) bn.tail_from = 0;
     if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
         if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamL, true, true); else RT_NEARC(kSrcCamL, false, true); }
         else if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
@@ -1089,8 +1134,10 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     } else if (k == 0) {
         if (sc.has_fresnel) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, true, false);
     } else if (lists) {
+        if (quad) { if (sc.has_fresnel) RT_NEARL(kSrcBvh4Q, true); else RT_NEARL(kSrcBvh4Q, false); }
         if (sc.has_fresnel) RT_NEARL(kSrcN, true); else RT_NEARL(kSrcN, false);
     } else {
+        if (quad) { if (sc.has_fresnel) RT_NEAR(kSrcBvh4Q, false, true); else RT_NEAR(kSrcBvh4Q, false, false); }
         if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
     }
 #undef RT_NEARC
@@ -1223,12 +1270,17 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
 #if RT_STAMP
 }  // namespace rtamd
 extern "C" int rt_debug_stamps(unsigned long long* out, int n, int reset) {
-    const size_t bytes = sizeof(unsigned long long) * static_cast<size_t>(n < 12 * rtamd::kMaxGenerations ? n : 12 * rtamd::kMaxGenerations);
+    // out: 16 fields per generation
+    static unsigned long long a[rtamd::kMaxGenerations][12], b[rtamd::kMaxGenerations][4];
     if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtamd::g_stamp), bytes) != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(a, HIP_SYMBOL(rtamd::g_stamp), sizeof a) != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(b, HIP_SYMBOL(rtamd::g_stamp2), sizeof b) != hipSuccess) return -3;
+    for (int i = 0; i < n && i < 16 * rtamd::kMaxGenerations; ++i)
+        out[i] = (i % 16) < 12 ? a[i / 16][i % 16] : b[i / 16][i % 16 - 12];
     if (reset) {
-        static unsigned long long zero[rtamd::kMaxGenerations][12];
-        if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamp), zero, sizeof zero) != hipSuccess) return -3;
+        static unsigned long long za[rtamd::kMaxGenerations][12], zb[rtamd::kMaxGenerations][4];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamp), za, sizeof za) != hipSuccess) return -3;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtamd::g_stamp2), zb, sizeof zb) != hipSuccess) return -3;
     }
     return 0;
 }

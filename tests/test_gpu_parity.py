@@ -261,11 +261,7 @@ def test_render_without_scene_and_bad_opts():
 
 # ---- BVH culling must be conservative: adversarial scenes ------------------
 
-@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
-def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
-    """Odd image sizes put pixel centres exactly on the camera axes (direction
-    components exactly 0); 24 coincident spheres with different colours land in
-    different BVH leaves and must still resolve to the FIRST in file order."""
+def _axis_tie_scene():
     s = scenes.SceneSpec(width=33, height=31, max_depth=6, background=(0.1, 0.1, 0.2),
                          camera={"ctor": "new", "position": (0, 0, 0), "look": (0, 0, -1), "up": (0, 1, 0),
                                  "im_dist": 1.0})
@@ -281,7 +277,28 @@ def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
     s.sphere((-1.0, 0.0, -10.0), 1.0, scenes.phong((0.2, 0.9, 0.2), (0.5, 0.5, 0.5), 8.0, (0, 0, 0)))
     s.point_light((0.0, 5.0, 0.0), (1, 1, 1))
     s.directional_light((0.0, -1.0, 0.0), (0.3, 0.3, 0.3))
-    check_parity(gpu_ctx, s, algo)
+    return s
+
+
+@pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
+def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
+    """Odd image sizes put pixel centres exactly on the camera axes (direction
+    components exactly 0); 24 coincident spheres with different colours land in
+    different BVH leaves and must still resolve to the FIRST in file order."""
+    check_parity(gpu_ctx, _axis_tie_scene(), algo)
+
+
+@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3"])
+def test_quad_tail_walk_matches_oracle(gpu_ctx, scene):
+    """The quad walk (four lanes per ray on the 4-wide tree, trace_common.hpp
+    nearest_quad) forced onto every generation from 1 on, whatever the queue
+    size (tail_max huge: 16-ray chunks for small queues, 64-ray chunks in four
+    passes for large ones): ties across leaves, axis-aligned rays, the deepest
+    small tree and a C3 workload all match the oracle bit for bit."""
+    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene,
+         "config3": lambda: scenes.config3(160, 128)}[scene]()
+    with _with_tuning(gpu_ctx, tail_from=1, tail_max=1 << 30):
+        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
 @pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
@@ -297,15 +314,7 @@ def test_extreme_sphere_sizes_and_far_plane_origins(gpu_ctx, algo):
     check_parity(gpu_ctx, s, algo)
 
 
-def test_chain_of_shrinking_spheres_both_stacks(gpu_ctx):
-    """A chain of spheres halving in size and spacing toward x = 2 inside a
-    random cloud: the binned SAH peels a few spheres per level, giving the
-    deepest tree a scene this small reaches (still within the compact stack's
-    32 entries: tools/schedule_probe.py prints short_stack 1; a binned SAH
-    re-bins every node over its own extent, so depth > 32 needs far more
-    spheres than the compact source's 4096).  Compact 32-bit entries (src 9)
-    and the 64-bit stack (compact_stack=0, src 7) both match the oracle bit
-    for bit."""
+def _sphere_chain_scene():
     s = scenes.config2(80, 60)
     s.max_depth = 6
     for i in range(46):
@@ -316,6 +325,19 @@ def test_chain_of_shrinking_spheres_both_stacks(gpu_ctx):
     for _ in range(150):
         s.sphere((rng.uniform(-6, 6), rng.uniform(0.2, 4), rng.uniform(-14, -3)), rng.uniform(0.05, 0.4),
                  scenes.phong((0.3, 0.6, 0.9), (0.4, 0.4, 0.4), 30.0, (0, 0, 0)))
+    return s
+
+
+def test_chain_of_shrinking_spheres_both_stacks(gpu_ctx):
+    """A chain of spheres halving in size and spacing toward x = 2 inside a
+    random cloud: the binned SAH peels a few spheres per level, giving the
+    deepest tree a scene this small reaches (still within the compact stack's
+    32 entries: tools/schedule_probe.py prints short_stack 1; a binned SAH
+    re-bins every node over its own extent, so depth > 32 needs far more
+    spheres than the compact source's 4096).  Compact 32-bit entries (src 9)
+    and the 64-bit stack (compact_stack=0, src 7) both match the oracle bit
+    for bit."""
+    s = _sphere_chain_scene()
     check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
     base = gpu_render(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
     with _with_tuning(gpu_ctx, compact_stack=0):
@@ -549,7 +571,9 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
     spec = scenes.config3(192, 160)
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
     for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(fuse_from=3), dict(fuse_from=0), dict(regions=96),
-               dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10)]:
+               dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10),
+               dict(tail_from=0), dict(tail_from=1, tail_max=1 << 30), dict(tail_from=2, tail_max=20000, lists=0),
+               dict(tail_from=1, tail_max=1 << 30, regions=96)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

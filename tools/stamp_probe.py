@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=["c3", "c4"])
     ap.add_argument("--tune", default="")
+    ap.add_argument("--shard-of", type=int, default=1, help="render the last rank's 16-row bands of an N-way shard")
     a = ap.parse_args()
     import torch
     import libraytrace as lr
@@ -28,7 +29,7 @@ def main():
     lib = lr.lib
     lib.rt_debug_stamps.restype = C.c_int
     lib.rt_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
-    G, F = 34, 12
+    G, F = 34, 16
     buf = (C.c_ulonglong * (G * F))()
 
     def read(reset):
@@ -43,8 +44,11 @@ def main():
     dev = torch.device("cuda", 0)
     rgb = torch.empty((side, side, 3), dtype=torch.float32, device=dev)
     bgr = torch.empty((side, 3 * side), dtype=torch.uint8, device=dev)
-    opts = lr.render_opts(side, side, max_depth=8, spp=1, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8)
-    cnt = lr.render_opts(side, side, max_depth=8, spp=1, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK)
+    N = a.shard_of
+    shard = dict(tile_h=side // N, band=16, band_stride=N, band_phase=N - 1) if N > 1 else {}
+    opts = lr.render_opts(side, side, max_depth=8, spp=1, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8, **shard)
+    cnt = lr.render_opts(side, side, max_depth=8, spp=1, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_COUNT_WORK,
+                         **shard)
     s = torch.cuda.Stream(dev)
     for _ in range(2):
         ctx.render_device(opts, rgb.data_ptr(), bgr.data_ptr(), s.cuda_stream)
@@ -57,15 +61,17 @@ def main():
     torch.cuda.synchronize()
     counted = read(True)
     print(f"{a.config} {tune or ''}: cycles per chunk (64 rays) by phase; setup per wave; node visits per chunk")
-    print(" gen  chunks   waves  setup/wave  load/chunk  trav/chunk  fin/chunk   maxlane  meanlane  div   desc/ch   leaf/ch    pop/ch")
+    print(" gen  chunks   waves  setup/wave  load/chunk  trav/chunk  fin/chunk   maxlane  meanlane  div   desc/ch   leaf/ch    pop/ch"
+          "  slowest-wave  wave-iters/ch desc leaf pop  cycles/iter desc leaf pop")
     for g in range(G):
-        st, ld, tr, fi, ch, wv, _, _, de, le, po, _ = plain[g]
+        st, ld, tr, fi, ch, wv, _, _, de, le, po, _, slow, nd, nl, np_ = plain[g]
         mx, sm = counted[g][6], counted[g][7]
         if ch == 0:
             continue
         cc = counted[g][4] or 1
         print(f"{g:4d} {ch:7d} {wv:7d} {st / max(wv, 1):11.0f} {ld / ch:11.0f} {tr / ch:11.0f} {fi / ch:10.0f} "
-              f"{mx / cc:9.1f} {sm / cc / 64:9.1f} {mx / max(sm / 64, 1):5.2f} {de / ch:9.0f} {le / ch:9.0f} {po / ch:9.0f}")
+              f"{mx / cc:9.1f} {sm / cc / 64:9.1f} {mx / max(sm / 64, 1):5.2f} {de / ch:9.0f} {le / ch:9.0f} {po / ch:9.0f}"
+              f" {slow:13d}  {nd / ch:6.1f} {nl / ch:5.1f} {np_ / ch:5.1f}  {de / max(nd, 1):6.0f} {le / max(nl, 1):5.0f} {po / max(np_, 1):5.0f}")
     ctx.close()
 
 

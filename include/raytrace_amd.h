@@ -248,7 +248,7 @@ enum rt_kernel_family {
     RT_KF_NEAREST = 0,      /* wf_nearest, generations >= 1 */
     RT_KF_OCCLUSION = 1,    /* wf_occlusion: every (record, light) pair of a generation */
     RT_KF_SHADE = 2,        /* wf_shade */
-    RT_KF_FOLD = 3,         /* wf_fold */
+    RT_KF_FOLD = 3,         /* wf_fold, or wf_fold_gen per generation (eager_fold) */
     RT_KF_TALLY = 4,        /* wf_tally */
     RT_KF_CAMERA = 5,       /* wf_nearest, generation 0 (camera rays) */
     RT_KF_SHADOW = 6,       /* wf_shadow: the shadow item lists of a generation */
@@ -270,7 +270,8 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * tail_from / tail_max (trees that fit LDS: nearest-hit generations >= tail_from
  * hand queues of <= tail_max rays to a walk with four lanes per ray on the 4-wide
  * tree; tail_from 0 off, -1 auto: 5 for chunks of <= 32 x tail_max pixels;
- * tail_max 0: CUs x 256).
+ * tail_max 0: CUs x 256), eager_fold (1: each generation folds the pixels whose
+ * chain ended in it, on the shading streams; 0: one fold after the last generation).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -269,6 +269,9 @@ struct WfBufs {
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
     int32_t tail_from;              // > 0: nearest-hit generations >= this of a src-9 tree: queues of
     uint32_t tail_max;              //   <= tail_max rays go to the quad kernel (src 17), the rest to src 9
+    uint32_t eager;                 // 1: each generation folds the pixels whose chain ended in it
+                                    //   (wf_fold_gen on the B streams), no frame-end fold
+    uint64_t o_dn, o_rd;            // eager: chain ends found by wf_nearest, their region sizes
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
@@ -292,7 +295,17 @@ struct WfBufs {
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
     RT_HD uint32_t* oq() const { return reinterpret_cast<uint32_t*>(mem + o_oq); }
     RT_HD uint32_t* ro() const { return reinterpret_cast<uint32_t*>(mem + o_ro); }
+    // eager fold: chain ends of generation k found by wf_nearest (index = k * qcap + entry):
+    // the pixel and the object whose ambient colour ends it (INT32_MAX: background)
+    RT_HD uint32_t* dpix() const { return reinterpret_cast<uint32_t*>(mem + o_dn); }
+    RT_HD int32_t* dobj() const {
+        return reinterpret_cast<int32_t*>(mem + o_dn) + static_cast<uint64_t>(levels + 1) * qcap;
+    }
+    RT_HD uint32_t* rd() const { return reinterpret_cast<uint32_t*>(mem + o_rd); }
 };
+// eager fold: wf_shade marks a record whose chain ends there (ru(2) = pixel | kChainEnd)
+// and leaves its final colour in rf(0..2) (the hit point is dead by then)
+constexpr uint32_t kChainEnd = 0x80000000u;
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
 constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G

@@ -81,6 +81,8 @@ struct WfStreams {
                         // spheres from LDS (1) or HBM/L2 (2); 0: the general shadow kernel
     int fold_bands;     // with fold_ev: the fold runs in this many row bands of the chunk,
     hipEvent_t* fold_ev;//   fold_ev[i] recorded after band i (null: one fold launch, no events)
+    hipEvent_t* gen_done; // eager fold (WfBufs::eager): kMaxGenerations events, generation k's
+                          //   wf_fold_gen done (the next generation's fold waits for it)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -34,7 +34,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -77,6 +77,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"tail_from", -1, -1, 99},                   // nearest-hit generations >= this (src 9 trees) hand queues of <= tail_max
                                                  // rays to the quad walk; 0 off, -1: 5 for chunks of <= 32 x tail_max slots
     {"tail_max", 0, 0, INT32_MAX},               // 0: CUs x 256 (one quad-walk round: one workgroup of 256 rays per CU)
+    {"eager_fold", 1, 0, 1},                     // 1: each generation folds the chains that ended in it (B streams);
+                                                 // 0: one fold over every pixel after the last generation
 };
 
 }  // namespace
@@ -209,6 +211,7 @@ struct rt_ctx {
         hipEvent_t mark = nullptr, done = nullptr;
         std::vector<hipEvent_t> b_done;    // one per sb stream
         std::vector<hipEvent_t> near_done; // per generation: nearest-hit kernel finished (s -> sb)
+        std::vector<hipEvent_t> gen_done;  // per generation: its eager fold finished (sb -> next sb)
         void* mem = nullptr;
         size_t bytes = 0;
         WfBufs b{};
@@ -332,6 +335,7 @@ void drop_lanes(rt_ctx* c) {
         if (L.done) (void)hipEventDestroy(L.done);
         for (hipEvent_t e : L.b_done) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : L.gen_done) if (e) (void)hipEventDestroy(e);
         if (L.s) (void)hipStreamDestroy(L.s);
         for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
     }
@@ -340,9 +344,10 @@ void drop_lanes(rt_ctx* c) {
 
 // Working-set bytes per pixel slot of a chunk (ensure_wf's sections, per slot):
 // two queues, one shade-record array and one level array per lit generation,
-// terminals, shadow item lists.
+// terminals, shadow item lists, the eager fold's chain-end lists (one per generation).
 uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
-    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4;
+    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
+           (levels + 1) * 8;
 }
 
 // Default working-set budget of a render (all lanes): 85% of what the device
@@ -374,6 +379,8 @@ int ensure_lanes(rt_ctx* c, int n) {
         HIP_TRY(c, hipEventCreateWithFlags(&M.done, hipEventDisableTiming));
         M.near_done.assign(kMaxGenerations, nullptr);
         for (hipEvent_t& e : M.near_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        M.gen_done.assign(kMaxGenerations, nullptr);
+        for (hipEvent_t& e : M.gen_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return RT_OK;
 }
@@ -394,6 +401,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
     const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;
     const uint64_t s_ro = static_cast<uint64_t>(kMaxGenerations) * nl * G * 4;
+    const uint64_t s_dn = (static_cast<uint64_t>(levels) + 1) * q * 8;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
     b.o_lev = off; off = align_up(off + s_lev, 256);
@@ -402,6 +410,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_rs = off; off = align_up(off + s_reg, 256);
     b.o_oq = off; off = align_up(off + s_oq, 256);
     b.o_ro = off; off = align_up(off + s_ro, 256);
+    b.o_dn = off; off = align_up(off + s_dn, 256);
+    b.o_rd = off; off = align_up(off + s_reg, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -1009,6 +1019,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
+            // eager fold: pixel ids carry the kChainEnd flag in bit 31
+            c->lanes[l].b.eager = c->t(kTuneEagerFold) != 0 && static_cast<uint64_t>(o->tile_w) * chunk_rows < kChainEnd ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
         // rt_render copies row bands as their fold finishes: a one-chunk frame folds in
@@ -1070,6 +1082,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.mb[i] = timed ? (split ? &marks_b[i] : &marks) : nullptr;
             }
             ws.near_done = L.near_done.data();
+            ws.gen_done = L.gen_done.data();
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
             ws.cam = cam;

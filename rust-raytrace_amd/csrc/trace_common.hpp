@@ -413,9 +413,13 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
 // compiler to promote to registers is indexed per lane with divergent indices,
 // which compiles to a waterfall loop over the wave's distinct indices (the
 // 128-B compact stack measured 130x slower that way).  Passing its address to
-// an empty asm statement makes it escape, so it is never promoted.
+// an empty asm statement makes it escape, so it is never promoted.  (Its 32-bit
+// scratch offset, not the 64-bit generic pointer: the generic cast's null check
+// hit an instruction-selection error in one kernel.)
 template <class T>
-__device__ __forceinline__ void rt_keep_in_scratch(T* p) { asm volatile("" : : "v"(p)); }
+__device__ __forceinline__ void rt_keep_in_scratch(T* p) {
+    asm volatile("" : : "v"(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p))));
+}
 
 // Traversal stacks, declared as plain locals so the compiler keeps the stack
 // pointer (and the register part) in registers.  The top kReg entries live in

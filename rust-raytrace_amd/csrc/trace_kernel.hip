@@ -559,6 +559,14 @@ __device__ __forceinline__ void write_background_pixel(const FrameParams& fp, co
     b.nlev()[p] = kNlevDone;
 }
 
+// The colour that ends a chain without lighting: the background (obj INT32_MAX,
+// a miss) or the object's ambient colour (cut-off, insignificant surface).
+__device__ __forceinline__ Col end_colour(const DevScene& sc, int32_t obj) {
+    if (obj == INT32_MAX) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};
+    const DevMaterial& m = sc.mats[obj];
+    return Col{m.amb[0], m.amb[1], m.amb[2]};
+}
+
 __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
     stn(&b.term(0)[p], c.r); stn(&b.term(1)[p], c.g); stn(&b.term(2)[p], c.b);
     b.nlev()[p] = static_cast<uint8_t>(k);
@@ -567,12 +575,14 @@ __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c,
 // LDS of a queue kernel after its staged data.
 constexpr int kMaxFusedLights = 24;         // shadow lists / fused shading: the light count lives in occ bits 24..31
 constexpr int kOccCount = 24;
-constexpr int kQueueCounters = 2 + kMaxFusedLights + 1;
+constexpr int kCntDone = 2 + kMaxFusedLights + 1;     // eager fold: chain ends of this workgroup
+constexpr int kQueueCounters = kCntDone + 1;
 
 struct QueueLds {
     uint32_t* scan;     // G + 1
     uint32_t* wave;     // 16
-    uint32_t* count;    // shade records, reflection rays, then one per shadow item list, appended by this workgroup
+    uint32_t* count;    // shade records, reflection rays, then one per shadow item list, then chain
+                        // ends (eager fold), appended by this workgroup
 };
 
 __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
@@ -596,14 +606,19 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
     bool shade = false, refl = false;
     double ptx = 0.0, pty = 0.0, ptz = 0.0, nsig = 0.0;
     Ray rr{};
+    // a chain that ends here without lighting: background (end_obj INT32_MAX) or the
+    // object's ambient colour; eager fold: queued for this generation's wf_fold_gen
+    bool ends = false;
+    int32_t end_obj = INT32_MAX;
     if (live) {
         if (h.obj == INT32_MAX) {                                           // raytrace.rs:265, 228-232
             if constexpr (kCam) write_background_pixel(fp, b, p);          // no levels: final now
-            else set_terminal(b, p, Col{sc.bg[0], sc.bg[1], sc.bg[2]}, k);
+            else ends = true;
         } else {
             const DevMaterial& m = sc.mats[h.obj];
             if (static_cast<uint32_t>(k) > fp.max_depth) {                  // raytrace.rs:33 / 126
-                set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+                ends = true;
+                end_obj = h.obj;
             } else {
                 ptx = r.ox + r.dx * h.t; pty = r.oy + r.dy * h.t; ptz = r.oz + r.dz * h.t;   // ray.cast(t)
                 double nx, ny, nz;
@@ -611,7 +626,8 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
                 const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
                 const Shading sh = shading_flags<kFresnel>(m, sig, nd);
                 if (!sh.diffuse && !sh.specular) {
-                    set_terminal(b, p, Col{m.amb[0], m.amb[1], m.amb[2]}, k);
+                    ends = true;
+                    end_obj = h.obj;
                 } else {
                     shade = true;
                     if (sh.specular) {                                      // raytrace.rs:58-64 / 159-164
@@ -623,6 +639,15 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
                 }
             }
         }
+    }
+    if (b.eager) {                                         // workgroup-uniform
+        const uint32_t ds = lds_append(&counts[kCntDone], ends);
+        if (ends) {
+            stn(&b.dpix()[static_cast<size_t>(k) * b.qcap + obase + ds], p);
+            stn(&b.dobj()[static_cast<size_t>(k) * b.qcap + obase + ds], end_obj);
+        }
+    } else if (ends) {
+        set_terminal(b, p, end_colour(sc, end_obj), k);
     }
     const uint32_t slot = lds_append(&counts[0], shade);
     uint32_t occ = 0u;
@@ -708,7 +733,11 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     if (!kCam && b.tail_from > 0 && k >= b.tail_from && (n <= b.tail_max) != kQuad) return;
     const uint32_t width = kQuad && n <= b.G * (kWfThreads / 4) ? 16u : 64u;
     if (!wg_has_work(b, n, width)) {           // nothing dealt here: publish empty regions, free the CU
-        if (threadIdx.x == 0) { b.rs()[k * b.G + blockIdx.x] = 0; b.rq()[(k + 1) * b.G + blockIdx.x] = 0; }
+        if (threadIdx.x == 0) {
+            b.rs()[k * b.G + blockIdx.x] = 0;
+            b.rq()[(k + 1) * b.G + blockIdx.x] = 0;
+            if (b.eager) b.rd()[k * b.G + blockIdx.x] = 0;
+        }
         if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = 0;
         return;
     }
@@ -793,6 +822,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     if (threadIdx.x == 0) {
         b.rs()[k * b.G + blockIdx.x] = ql.count[0];
         b.rq()[(k + 1) * b.G + blockIdx.x] = ql.count[1];
+        if (b.eager) b.rd()[k * b.G + blockIdx.x] = ql.count[kCntDone];
     }
     if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = ql.count[2 + threadIdx.x];
     flush_work<kCount>(b, 2, w);
@@ -829,6 +859,9 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
         stn(&b.lobj()[st], obj);
         if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
+    } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
+        stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
+        stn(&b.ru(2)[at], p | kChainEnd);
     } else {
         set_terminal(b, p, res, k);
     }
@@ -967,10 +1000,8 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 // issued together so a pixel costs about two memory round trips per four
 // levels instead of two per level.
 template <bool kFresnel>
-__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
-    if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
-    Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
-    for (int k = static_cast<int>(nlev) - 1; k >= 0; k -= 4) {
+__device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, uint32_t p, int nlev, Col acc) {
+    for (int k = nlev - 1; k >= 0; k -= 4) {
         double sr[4], sg[4], sb[4];
         int32_t ob[4];
 #pragma unroll
@@ -1000,6 +1031,50 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
         }
     }
     return acc;
+}
+
+template <bool kFresnel>
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
+    if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
+    const Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
+    return fold_levels<kFresnel>(sc, b, p, nlev, acc);
+}
+
+// Eager fold (WfBufs::eager): the pixels whose chain ended in generation k --
+// shade records wf_shade marked kChainEnd (their final colour in rf(0..2)) and
+// the misses / cut-offs wf_nearest listed (dpix, dobj) -- folded through their
+// levels k-1 .. 0 exactly as wf_fold does, and written.  Runs on the B stream of
+// generation k after its shading and after generation k-1's wf_fold_gen (so
+// every level below k is written), off the nearest-hit chain: the frame ends
+// with the last generation's shading instead of a fold over every pixel.
+template <bool kFresnel>
+__global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    __shared__ uint32_t s_scan[2][kMaxRegions + 1];
+    __shared__ uint32_t s_wave[kWfThreads / 64];
+    __shared__ double s_srgb[255];
+    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
+    region_scan(b.rs() + k * b.G, b.G, s_scan[0], s_wave);     // (past the cut-off: all zero)
+    region_scan(b.rd() + k * b.G, b.G, s_scan[1], s_wave);     // also publishes s_srgb
+    const uint32_t nr = s_scan[0][b.G], n = nr + s_scan[1][b.G];
+    const size_t rk = static_cast<size_t>(k) * b.qcap;
+    RT_FOR_CHUNKS(b, n, j) {
+        if (j >= n) continue;
+        uint32_t p;
+        Col acc;
+        if (j < nr) {
+            const size_t at = rk + region_entry(s_scan[0], b.G, b.R, j);
+            const uint32_t pf = ldn(&b.ru(2)[at]);
+            if (!(pf & kChainEnd)) continue;                   // specular: its chain goes on
+            p = pf & ~kChainEnd;
+            acc = Col{ldn(&b.rf(0)[at]), ldn(&b.rf(1)[at]), ldn(&b.rf(2)[at])};
+        } else {
+            const size_t at = rk + region_entry(s_scan[1], b.G, b.R, j - nr);
+            p = ldn(&b.dpix()[at]);
+            acc = end_colour(sc, ldn(&b.dobj()[at]));
+        }
+        const Col res = average_samples(fold_levels<kFresnel>(sc, b, p, k, acc), fp.spp);
+        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+    }
 }
 
 // One pixel per work-item.  The quantisation table is staged in LDS: the
@@ -1101,6 +1176,10 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
     return hipGetLastError();
 }
 
+template <int kSrcO, bool kCount>
+hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
+                          hipStream_t sb, LaunchMarks* mb, bool lists);
+
 template <int kSrcN, int kSrcO, bool kCount>
 hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws) {
     const dim3 grid(b.G), block(kWfThreads);
@@ -1146,7 +1225,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     (void)lds_n;
     e = ws.ma ? ws.ma->mark(ws.a, k == 0 ? kKfCamera : kKfNearest) : hipSuccess;
     if (e != hipSuccess) return e;
-    if (static_cast<uint32_t>(k) > fp.max_depth) return hipSuccess;     // no shade records past the cut-off
+    const bool shaded = static_cast<uint32_t>(k) <= fp.max_depth;     // no shade records past the cut-off
+    if (!shaded && !b.eager) return hipSuccess;
     // shadows and shading of generation k: on a b stream once nearest_k is done
     // (generations alternate over the b streams, so consecutive ones overlap too)
     const int bi = k % ws.nb;
@@ -1156,6 +1236,26 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(sb, ws.near_done[k], 0)) != hipSuccess) return e;
     }
+    if (shaded && (e = launch_shading<kSrcO, kCount>(sc, fp, b, k, ws, sb, mb, lists)) != hipSuccess) return e;
+    if (!b.eager) return hipSuccess;
+    // eager fold of the chains that ended in generation k, after generation k-1's fold
+    // (on another b stream: every level below k is then written)
+    if (k > 0 && ws.b[(k - 1) % ws.nb] != sb && (e = hipStreamWaitEvent(sb, ws.gen_done[k - 1], 0)) != hipSuccess) return e;
+    if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_fold_gen<true>, grid, block, 0, sb, sc, fp, b, k);
+    else hipLaunchKernelGGL(wf_fold_gen<false>, grid, block, 0, sb, sc, fp, b, k);
+    if (mb && (e = mb->mark(sb, kKfFold)) != hipSuccess) return e;
+    if (sb != ws.a && (e = hipEventRecord(ws.gen_done[k], sb)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// The shadow queries and the shading of generation k on b stream sb (after its
+// nearest-hit launch).
+template <int kSrcO, bool kCount>
+hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
+                          hipStream_t sb, LaunchMarks* mb, bool lists) {
+    const dim3 grid(b.G), block(kWfThreads);
+    hipError_t e;
     if (lists) {                                 // shadow lists (planes and own sphere decided upstream)
         if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
         const size_t lds_s = staged_bytes<kSrcO>(sc) + static_cast<size_t>(b.nlists) * (b.G + 1) * 4u;
@@ -1246,7 +1346,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     const uint32_t band_rows = (fp.rows + nbands - 1) / nbands;
     for (uint32_t bi = 0; bi < nbands; ++bi) {
         const uint32_t r0 = min(fp.rows, bi * band_rows), r1 = min(fp.rows, r0 + band_rows);
-        if (r1 > r0) {
+        if (r1 > r0 && !b.eager) {                  // eager: every pixel was written by its generation
             const uint32_t p0 = r0 * fp.tile_w, p1 = r1 * fp.tile_w;
             const dim3 gf((p1 - p0 + kBlock - 1) / kBlock);
             if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;

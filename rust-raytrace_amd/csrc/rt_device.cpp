@@ -77,7 +77,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"tail_from", -1, -1, 99},                   // nearest-hit generations >= this (src 9 trees) hand queues of <= tail_max
                                                  // rays to the quad walk; 0 off, -1: 5 for chunks of <= 32 x tail_max slots
     {"tail_max", 0, 0, INT32_MAX},               // 0: CUs x 256 (one quad-walk round: one workgroup of 256 rays per CU)
-    {"eager_fold", 1, 0, 1},                     // 1: each generation folds the chains that ended in it (B streams);
+    {"eager_fold", 0, 0, 1},                     // 1: each generation folds the chains that ended in it (B streams;
+                                                 // measured slower: scattered level gathers);
                                                  // 0: one fold over every pixel after the last generation
 };
 
@@ -346,7 +347,7 @@ void drop_lanes(rt_ctx* c) {
 // two queues, one shade-record array and one level array per lit generation,
 // terminals, shadow item lists, the eager fold's chain-end lists (one per generation).
 uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
-    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
+    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (7 * 8) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
            (levels + 1) * 8;
 }
 
@@ -396,7 +397,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     // section sizes (device_layout.hpp, WfBufs)
     const uint64_t s_queue = 2ull * 8 * q * 8;
     const uint64_t s_rec = static_cast<uint64_t>(levels) * q * (7 * 8 + 4 * 4);
-    const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (4 * 8 + 4);
+    const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (7 * 8);
     const uint64_t s_term = capa * (3 * 8 + 1);
     const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
     const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;

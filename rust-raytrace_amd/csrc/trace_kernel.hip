@@ -857,8 +857,8 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
     if (specular) {
         const size_t st = static_cast<size_t>(k) * b.capa + p;
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
-        stn(&b.lobj()[st], obj);
-        if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
+        stn(&b.lf(4)[st], m.ks[0]); stn(&b.lf(5)[st], m.ks[1]); stn(&b.lf(6)[st], m.ks[2]);
+        if (kFresnel) stn(&b.lf(3)[st], m.kind == kMatFresnel ? sh.f : 1.0);
     } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
         stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
         stn(&b.ru(2)[at], p | kChainEnd);
@@ -1002,23 +1002,14 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, uint32_t p, int nlev, Col acc) {
     for (int k = nlev - 1; k >= 0; k -= 4) {
-        double sr[4], sg[4], sb[4];
-        int32_t ob[4];
+        double sr[4], sg[4], sb[4], kr[4], kg[4], kb[4], kf[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (k - u >= 0) {
+            if (k - u >= 0) {                  // the level stores its factors: no material gather
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
-                ob[u] = ldn_if<kNtFold>(&b.lobj()[at]);
                 sr[u] = ldn_if<kNtFold>(&b.lf(0)[at]); sg[u] = ldn_if<kNtFold>(&b.lf(1)[at]); sb[u] = ldn_if<kNtFold>(&b.lf(2)[at]);
-            }
-        }
-        double kr[4], kg[4], kb[4], kf[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (k - u >= 0) {
-                const DevMaterial& m = sc.mats[ob[u]];
-                kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
-                kf[u] = kFresnel && m.kind == kMatFresnel ? ldn_if<kNtFold>(&b.lf(3)[static_cast<size_t>(k - u) * b.capa + p]) : 1.0;
+                kr[u] = ldn_if<kNtFold>(&b.lf(4)[at]); kg[u] = ldn_if<kNtFold>(&b.lf(5)[at]); kb[u] = ldn_if<kNtFold>(&b.lf(6)[at]);
+                kf[u] = kFresnel ? ldn_if<kNtFold>(&b.lf(3)[at]) : 1.0;
             }
         }
 #pragma unroll
@@ -1331,6 +1322,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         }
     }
     hipError_t e;
+    // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
+    if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);
+    if (ws.ma && (e = ws.ma->mark(ws.a, kKfTally)) != hipSuccess) return e;
     for (int i = 0; i < ws.nb; ++i) {
         if (ws.b[i] == ws.a) continue;
         if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
@@ -1361,9 +1356,6 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         }
         if (ws.fold_ev && (e = hipEventRecord(ws.fold_ev[bi], s)) != hipSuccess) return e;
     }
-    if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, sc.n_lights, gens);
-    if (ws.ma && (e = ws.ma->mark(s, kKfTally)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

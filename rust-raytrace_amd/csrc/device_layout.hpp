@@ -284,10 +284,11 @@ struct WfBufs {
     RT_HD uint32_t* ru(int f) const {             // 0 object, 1 primitive, 2 pixel, 3 occlusion
         return reinterpret_cast<uint32_t*>(reinterpret_cast<double*>(mem + o_rec) + 7 * rn()) + f * rn();
     }
-    // levels (index = k * capa + p): f = 0..2 colour, 3 Schlick factor (scenes with a
-    // FresnelMaterial; 1.0 for the other objects), 4..6 the object's specular colour ks:
-    // the fold's factors without a material gather
+    // levels (index = k * capa + p): f = 0..2 colour, 3 Schlick factor
     RT_HD double* lf(int f) const { return reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(f) * levels * capa; }
+    RT_HD int32_t* lobj() const {
+        return reinterpret_cast<int32_t*>(reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(4) * levels * capa);
+    }
     RT_HD double* term(int f) const { return reinterpret_cast<double*>(mem + o_term) + static_cast<uint64_t>(f) * capa; }
     RT_HD uint8_t* nlev() const { return reinterpret_cast<uint8_t*>(reinterpret_cast<double*>(mem + o_term) + 3ull * capa); }
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }

@@ -347,7 +347,7 @@ void drop_lanes(rt_ctx* c) {
 // two queues, one shade-record array and one level array per lit generation,
 // terminals, shadow item lists, the eager fold's chain-end lists (one per generation).
 uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
-    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (7 * 8) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
+    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
            (levels + 1) * 8;
 }
 
@@ -392,12 +392,16 @@ int ensure_lanes(rt_ctx* c, int n) {
 int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels, uint32_t nlists) {
     WfBufs& b = L.b;
     const uint64_t q = static_cast<uint64_t>(G) * R;   // queue capacity (>= generation-0 slots)
+#if RT_PROBE_LEVREC
+    const uint64_t capa = align_up(std::max<uint64_t>(cap, static_cast<uint64_t>(G) * R), 64);
+#else
     const uint64_t capa = align_up(cap, 64);
+#endif
     const uint64_t nl = std::max(1u, nlists);
     // section sizes (device_layout.hpp, WfBufs)
     const uint64_t s_queue = 2ull * 8 * q * 8;
     const uint64_t s_rec = static_cast<uint64_t>(levels) * q * (7 * 8 + 4 * 4);
-    const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (7 * 8);
+    const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (4 * 8 + 4);
     const uint64_t s_term = capa * (3 * 8 + 1);
     const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
     const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;

@@ -317,6 +317,12 @@ __device__ __forceinline__ void stn_if(T* p, U v) {
     *p = static_cast<T>(v);
 }
 
+// A/B timing probe (EXTRA=-DRT_PROBE_LEVREC=1, wrong images): wf_shade writes levels and
+// terminals at the record's slot instead of the pixel's
+#ifndef RT_PROBE_LEVREC
+#define RT_PROBE_LEVREC 0
+#endif
+
 // the fold's loads (RT_NT_FOLD=1: nontemporal; measured 346 -> 413 us per fold at C3, so plain)
 #ifndef RT_NT_FOLD
 #define RT_NT_FOLD 0
@@ -854,16 +860,18 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
         light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
         add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
     }
+    // (timing probe only, wrong images: levels and terminals at the record's slot, i.e. coalesced)
+    const uint32_t pl = RT_PROBE_LEVREC ? static_cast<uint32_t>(at - static_cast<size_t>(k) * b.qcap) : p;
     if (specular) {
-        const size_t st = static_cast<size_t>(k) * b.capa + p;
+        const size_t st = static_cast<size_t>(k) * b.capa + pl;
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
-        stn(&b.lf(4)[st], m.ks[0]); stn(&b.lf(5)[st], m.ks[1]); stn(&b.lf(6)[st], m.ks[2]);
-        if (kFresnel) stn(&b.lf(3)[st], m.kind == kMatFresnel ? sh.f : 1.0);
+        stn(&b.lobj()[st], obj);
+        if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
     } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
         stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
         stn(&b.ru(2)[at], p | kChainEnd);
     } else {
-        set_terminal(b, p, res, k);
+        set_terminal(b, pl, res, k);
     }
 }
 
@@ -1002,14 +1010,24 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, uint32_t p, int nlev, Col acc) {
     for (int k = nlev - 1; k >= 0; k -= 4) {
-        double sr[4], sg[4], sb[4], kr[4], kg[4], kb[4], kf[4];
+        double sr[4], sg[4], sb[4];
+        int32_t ob[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (k - u >= 0) {                  // the level stores its factors: no material gather
+            if (k - u >= 0) {
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
+                ob[u] = ldn_if<kNtFold>(&b.lobj()[at]);
+                if (RT_PROBE_LEVREC && static_cast<uint32_t>(ob[u]) >= static_cast<uint32_t>(sc.n_spheres + sc.n_planes)) ob[u] = 0;
                 sr[u] = ldn_if<kNtFold>(&b.lf(0)[at]); sg[u] = ldn_if<kNtFold>(&b.lf(1)[at]); sb[u] = ldn_if<kNtFold>(&b.lf(2)[at]);
-                kr[u] = ldn_if<kNtFold>(&b.lf(4)[at]); kg[u] = ldn_if<kNtFold>(&b.lf(5)[at]); kb[u] = ldn_if<kNtFold>(&b.lf(6)[at]);
-                kf[u] = kFresnel ? ldn_if<kNtFold>(&b.lf(3)[at]) : 1.0;
+            }
+        }
+        double kr[4], kg[4], kb[4], kf[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k - u >= 0) {
+                const DevMaterial& m = sc.mats[ob[u]];
+                kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
+                kf[u] = kFresnel && m.kind == kMatFresnel ? ldn_if<kNtFold>(&b.lf(3)[static_cast<size_t>(k - u) * b.capa + p]) : 1.0;
             }
         }
 #pragma unroll
@@ -1027,6 +1045,7 @@ __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, 
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
     if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
+    if (RT_PROBE_LEVREC && nlev > b.levels) nlev = static_cast<uint8_t>(b.levels);   // (probe: stale entries)
     const Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
     return fold_levels<kFresnel>(sc, b, p, nlev, acc);
 }

@@ -463,17 +463,17 @@ def test_kernel_times(gpu_ctx):
     assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
     # shading runs in its own kernel unless the context is tuned fuse=1 (then inside the shadow kernels)
     assert kt["shade"][1] in (0, 2 * (gens - 1))
-    # eager fold (default): one wf_fold_gen per generation, on the shading streams
-    assert kt["fold"][1] == 2 * gens and kt["tally"][1] == 2
+    # frame-end fold (default): rt_render folds a one-chunk frame in 8 row bands (each
+    # copied to the host as it finishes)
+    assert kt["fold"][1] == 2 * 8 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
     assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested
-    # frame-end fold: rt_render folds a one-chunk frame in 8 row bands (each copied to
-    # the host as it finishes)
-    with _with_tuning(gpu_ctx, eager_fold=0):
+    # eager fold: one wf_fold_gen per generation, on the shading streams
+    with _with_tuning(gpu_ctx, eager_fold=1):
         t = gpu_ctx.render(lr.render_opts(64, 48, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS, **base))
     assert np.array_equal(plain[1], t[1])
     kt = gpu_ctx.kernel_times()
-    assert kt["fold"][1] == 8 and kt["tally"][1] == 1
+    assert kt["fold"][1] == gens and kt["tally"][1] == 1
 
 
 def _with_tuning(ctx, **kv):
@@ -581,8 +581,8 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
     for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(fuse_from=3), dict(fuse_from=0), dict(regions=96),
                dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10),
                dict(tail_from=0), dict(tail_from=1, tail_max=1 << 30), dict(tail_from=2, tail_max=20000, lists=0),
-               dict(tail_from=1, tail_max=1 << 30, regions=96), dict(eager_fold=0), dict(eager_fold=0, split=0),
-               dict(eager_fold=0, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1)]:
+               dict(tail_from=1, tail_max=1 << 30, regions=96), dict(eager_fold=1), dict(eager_fold=1, split=0),
+               dict(eager_fold=1, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

@@ -180,7 +180,6 @@ struct FrameParams {
 };
 
 
-constexpr uint8_t kNlevDone = 0xFF;   // WfBufs::nlev: pixel already written (camera ray missed)
 
 #if defined(__HIPCC__)
 #define RT_HD __host__ __device__
@@ -228,25 +227,30 @@ struct PathStack {
 // SGPRs and spills into the traversal loop's VGPRs).  Sections, each an SoA
 // of arrays:
 //   queues   [parity 2][field 8][qcap]: origin x,y,z, direction x,y,z,
-//            significance (f64), owning pixel (u32 in an 8-B slot); queues
+//            significance (f64), owning chain (u32 in an 8-B slot); queues
 //            ping-pong by generation parity;
 //   records  shade records, f64 fields [7][levels*qcap] (hit point x,y,z,
 //            incoming direction x,y,z, significance) then u32 fields
 //            [4][levels*qcap] (object id, primitive: sphere >= 0 / ~plane,
-//            pixel, occlusion mask: bit l = light l shadowed, bits 24.. = lights
+//            chain, occlusion mask: bit l = light l shadowed, bits 24.. = lights
 //            decided).  One region array per generation (generation k at
 //            k*qcap), so the nearest-hit kernels never wait for the shadow /
 //            shading kernels of earlier generations (the other stream);
 //   levels   per-level local colour r,g,b and Schlick factor (f64)
-//            [4][levels*capa], then object id (i32) [levels*capa]; [k*capa + p];
-//   term     terminal colour of each pixel's chain [3][capa] (f64), then nlev
-//            (u8, levels pushed, kNlevDone = written by wf_nearest) [capa];
+//            [4][levels*capa], then object id (i32) [levels*capa]; [k*capa + c]
+//            for chain c (chain = the entry of the lit camera hit's generation-0
+//            record, capa >= qcap; its pixel is cpix[c]), so a generation's
+//            levels are written in about its records' order;
+//   term     terminal colour of each chain [3][capa] (f64), then nlev (u8,
+//            levels pushed) [capa];
 //   rq / rs  [k*G + r]: entries of region r of Q_k / of generation k's records;
 //   oq / ro  shadow item lists (nlists > 0): for generation k and light l the
 //            records whose query toward l needs the sphere traversal; list
 //            n_lights = records with nothing left to trace.  Entry = record
 //            index within generation k; [(k*nlists + list)*qcap + entry] and
-//            region sizes [(k*nlists + list)*G + r].
+//            region sizes [(k*nlists + list)*G + r];
+//   dn / rd  eager fold only (chain ends found by wf_nearest, their region sizes);
+//   cpix     the chunk pixel of each chain [qcap] (u32).
 // Queue, record and list arrays are G regions of R entries (qcap = G*R); region
 // r is written only by workgroup r of the producing kernel.
 struct WfBufs {
@@ -257,7 +261,8 @@ struct WfBufs {
     uint64_t qcap;                  // G * R
     uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_oq, o_ro;   // byte offsets of the sections
     uint32_t cap;                   // pixel capacity
-    uint32_t capa;                  // cap rounded up to 64 (stride of the per-pixel arrays)
+    uint32_t capa;                  // qcap rounded up to 64: stride of the per-chain arrays (levels,
+                                    // terminals; chain c = generation 0's record entry c)
     uint32_t levels;                // record generations / stack levels (max_depth + 1)
     uint32_t nlists;                // n_lights + 1, or 0 (no lists: the plain shadow kernel)
     uint32_t G;                     // regions per queue
@@ -272,6 +277,7 @@ struct WfBufs {
     uint32_t eager;                 // 1: each generation folds the pixels whose chain ended in it
                                     //   (wf_fold_gen on the B streams), no frame-end fold
     uint64_t o_dn, o_rd;            // eager: chain ends found by wf_nearest, their region sizes
+    uint64_t o_cpix;                // the pixel of each chain
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
@@ -284,13 +290,14 @@ struct WfBufs {
     RT_HD uint32_t* ru(int f) const {             // 0 object, 1 primitive, 2 pixel, 3 occlusion
         return reinterpret_cast<uint32_t*>(reinterpret_cast<double*>(mem + o_rec) + 7 * rn()) + f * rn();
     }
-    // levels (index = k * capa + p): f = 0..2 colour, 3 Schlick factor
+    // levels (index = k * capa + chain): f = 0..2 colour, 3 Schlick factor
     RT_HD double* lf(int f) const { return reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(f) * levels * capa; }
     RT_HD int32_t* lobj() const {
         return reinterpret_cast<int32_t*>(reinterpret_cast<double*>(mem + o_lev) + static_cast<uint64_t>(4) * levels * capa);
     }
     RT_HD double* term(int f) const { return reinterpret_cast<double*>(mem + o_term) + static_cast<uint64_t>(f) * capa; }
     RT_HD uint8_t* nlev() const { return reinterpret_cast<uint8_t*>(reinterpret_cast<double*>(mem + o_term) + 3ull * capa); }
+    RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
     RT_HD uint32_t* oq() const { return reinterpret_cast<uint32_t*>(mem + o_oq); }

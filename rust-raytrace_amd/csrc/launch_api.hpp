@@ -79,8 +79,7 @@ struct WfStreams {
     int fuse_from;      // generations >= fuse_from shade inside the shadow kernel (one B launch instead of two)
     int grid_occ;       // every light has a light-view grid: shadow kernel without a tree walk,
                         // spheres from LDS (1) or HBM/L2 (2); 0: the general shadow kernel
-    int fold_bands;     // with fold_ev: the fold runs in this many row bands of the chunk,
-    hipEvent_t* fold_ev;//   fold_ev[i] recorded after band i (null: one fold launch, no events)
+    hipEvent_t* fold_ev;// recorded once the chunk's pixels are final (null: no event)
     hipEvent_t* gen_done; // eager fold (WfBufs::eager): kMaxGenerations events, generation k's
                           //   wf_fold_gen done (the next generation's fold waits for it)
 };

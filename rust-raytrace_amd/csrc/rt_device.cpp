@@ -171,7 +171,6 @@ private:
 };
 
 constexpr int kMaxBands = 16;           // row bands of one rt_render copied as they finish
-constexpr int kFoldBands = 8;           // bands of a one-chunk frame (its fold split in eight launches)
 constexpr int kRing = 4;                // pinned staging slices in flight
 constexpr size_t kSlice = 8u << 20;     // bytes per staging slice
 
@@ -348,7 +347,7 @@ void drop_lanes(rt_ctx* c) {
 // terminals, shadow item lists, the eager fold's chain-end lists (one per generation).
 uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
     return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
-           (levels + 1) * 8;
+           (levels + 1) * 8 + 4;
 }
 
 // Default working-set budget of a render (all lanes): 85% of what the device
@@ -392,11 +391,7 @@ int ensure_lanes(rt_ctx* c, int n) {
 int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels, uint32_t nlists) {
     WfBufs& b = L.b;
     const uint64_t q = static_cast<uint64_t>(G) * R;   // queue capacity (>= generation-0 slots)
-#if RT_PROBE_LEVREC
-    const uint64_t capa = align_up(std::max<uint64_t>(cap, static_cast<uint64_t>(G) * R), 64);
-#else
-    const uint64_t capa = align_up(cap, 64);
-#endif
+    const uint64_t capa = align_up(q, 64);               // per-chain arrays (chain = generation-0 record entry)
     const uint64_t nl = std::max(1u, nlists);
     // section sizes (device_layout.hpp, WfBufs)
     const uint64_t s_queue = 2ull * 8 * q * 8;
@@ -407,6 +402,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;
     const uint64_t s_ro = static_cast<uint64_t>(kMaxGenerations) * nl * G * 4;
     const uint64_t s_dn = (static_cast<uint64_t>(levels) + 1) * q * 8;
+    const uint64_t s_cpix = q * 4;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
     b.o_lev = off; off = align_up(off + s_lev, 256);
@@ -417,6 +413,7 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_ro = off; off = align_up(off + s_ro, 256);
     b.o_dn = off; off = align_up(off + s_dn, 256);
     b.o_rd = off; off = align_up(off + s_reg, 256);
+    b.o_cpix = off; off = align_up(off + s_cpix, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -1028,28 +1025,16 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.eager = c->t(kTuneEagerFold) != 0 && static_cast<uint64_t>(o->tile_w) * chunk_rows < kChainEnd ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
-        // rt_render copies row bands as their fold finishes: a one-chunk frame folds in
-        // kFoldBands bands, a multi-chunk one gets an event per chunk
-        int fold_bands = 1;
+        // rt_render copies each chunk's rows as soon as that chunk's fold is done (the fold
+        // runs in chain order, so a chunk's rows are final together)
         c->n_bands = 0;
         if (c->want_bands && n_chunks <= static_cast<uint32_t>(kMaxBands)) {
-            const uint32_t nb = n_chunks == 1 ? static_cast<uint32_t>(kFoldBands) : n_chunks;
-            for (uint32_t i = 0; i < nb; ++i)
+            for (uint32_t i = 0; i < n_chunks; ++i) {
                 if (!c->band_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->band_ev[i], hipEventDisableTiming));
-            if (n_chunks == 1) {
-                fold_bands = kFoldBands;
-                const uint32_t br = (o->tile_h + kFoldBands - 1) / kFoldBands;   // as launch_wavefront splits
-                for (int i = 0; i < kFoldBands; ++i) {
-                    c->band_row0[i] = std::min(o->tile_h, i * br);
-                    c->band_nrows[i] = std::min(o->tile_h, c->band_row0[i] + br) - c->band_row0[i];
-                }
-            } else {
-                for (uint32_t i = 0; i < n_chunks; ++i) {
-                    c->band_row0[i] = i * chunk_rows;
-                    c->band_nrows[i] = std::min(chunk_rows, o->tile_h - c->band_row0[i]);
-                }
+                c->band_row0[i] = i * chunk_rows;
+                c->band_nrows[i] = std::min(chunk_rows, o->tile_h - c->band_row0[i]);
             }
-            c->n_bands = static_cast<int>(nb);
+            c->n_bands = static_cast<int>(n_chunks);
         }
         if (c->t(kTuneVerbose))
             std::fprintf(stderr, "rtamd: chunks %u x %u rows, lanes %d, G %u, R %u\n", n_chunks, chunk_rows, n_lanes, G, R);
@@ -1095,8 +1080,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
             // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
             ws.fuse_from = static_cast<int>(c->t(kTuneFuseFrom));
-            ws.fold_bands = fold_bands;
-            ws.fold_ev = c->n_bands == 0 ? nullptr : (n_chunks == 1 ? c->band_ev : &c->band_ev[ci]);
+            ws.fold_ev = c->n_bands == 0 ? nullptr : &c->band_ev[ci];
             ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
                               ? (static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere) <= 64 * 1024 ? 1 : 2)
                               : 0;

@@ -317,12 +317,6 @@ __device__ __forceinline__ void stn_if(T* p, U v) {
     *p = static_cast<T>(v);
 }
 
-// A/B timing probe (EXTRA=-DRT_PROBE_LEVREC=1, wrong images): wf_shade writes levels and
-// terminals at the record's slot instead of the pixel's
-#ifndef RT_PROBE_LEVREC
-#define RT_PROBE_LEVREC 0
-#endif
-
 // the fold's loads (RT_NT_FOLD=1: nontemporal; measured 346 -> 413 us per fold at C3, so plain)
 #ifndef RT_NT_FOLD
 #define RT_NT_FOLD 0
@@ -548,8 +542,8 @@ __device__ __forceinline__ void flush_work(const WfBufs& b, int at, Work w) {
 }
 
 // A camera ray that misses everything: the pixel is the background averaged
-// over samples, precomputed on the host (FrameParams::bg_*); written here and
-// marked so wf_fold skips it.
+// over samples, precomputed on the host (FrameParams::bg_*), written here (it
+// starts no chain, so wf_fold never sees it).
 __device__ __forceinline__ void write_background_pixel(const FrameParams& fp, const WfBufs& b, uint32_t p) {
     const uint32_t lx = p % fp.tile_w, row = fp.row0 + p / fp.tile_w;
     if (fp.out_rgb) {
@@ -562,7 +556,6 @@ __device__ __forceinline__ void write_background_pixel(const FrameParams& fp, co
         if (lx == fp.tile_w - 1)       // BMP row padding is zero (main.rs:42)
             for (uint32_t k = 3u * fp.tile_w; k < fp.bgr_pitch; ++k) fp.out_bgr[static_cast<size_t>(row) * fp.bgr_pitch + k] = 0;
     }
-    b.nlev()[p] = kNlevDone;
 }
 
 // The colour that ends a chain without lighting: the background (obj INT32_MAX,
@@ -573,9 +566,10 @@ __device__ __forceinline__ Col end_colour(const DevScene& sc, int32_t obj) {
     return Col{m.amb[0], m.amb[1], m.amb[2]};
 }
 
-__device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t p, Col c, int k) {
-    stn(&b.term(0)[p], c.r); stn(&b.term(1)[p], c.g); stn(&b.term(2)[p], c.b);
-    b.nlev()[p] = static_cast<uint8_t>(k);
+// Chain c ends in generation k with colour col (wf_fold folds its k levels onto it).
+__device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t c, Col col, int k) {
+    stn(&b.term(0)[c], col.r); stn(&b.term(1)[c], col.g); stn(&b.term(2)[c], col.b);
+    b.nlev()[c] = static_cast<uint8_t>(k);
 }
 
 // LDS of a queue kernel after its staged data.
@@ -602,9 +596,13 @@ __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + 
 
 // What follows a nearest hit (all 64 lanes call it; `live` lanes carry a
 // query): a miss or a cut-off ends the chain at once (terminal colour; a
-// camera miss writes its final pixel); a lit hit becomes a shade record of
-// generation k, and a specular one also queues its reflection ray in Q_{k+1}.
-// counts[0..1]: this workgroup's LDS append counters (records, rays).
+// camera ray that ends writes its final pixel); a lit hit becomes a shade
+// record of generation k, and a specular one also queues its reflection ray in
+// Q_{k+1}.  counts[0..1]: this workgroup's LDS append counters (records, rays).
+// Chains: a lit camera hit starts chain c = its record's entry (generation 0,
+// pixel cpix[c]); its records, reflection rays, levels and terminal carry c
+// (`p` is the pixel for kCam, the chain otherwise), so the levels and
+// terminals of a generation are written in about the order of its records.
 template <bool kCam, bool kFresnel, bool kLists>
 __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FrameParams& fp, const WfBufs& b,
                                                const DevSphere* sph, int k, bool live, const Ray& r, double sig,
@@ -646,6 +644,10 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
             }
         }
     }
+    if (kCam && ends) {                                    // no levels: the final pixel now
+        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, average_samples(end_colour(sc, end_obj), fp.spp));
+        ends = false;
+    }
     if (b.eager) {                                         // workgroup-uniform
         const uint32_t ds = lds_append(&counts[kCntDone], ends);
         if (ends) {
@@ -682,6 +684,7 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         const uint32_t qs = lds_append(&counts[2 + L], none);
         if (none) stn_if<2>(&b.oq()[(rk + L) * b.qcap + obase + qs], static_cast<uint32_t>(obase) + slot);
     }
+    const uint32_t chain = kCam ? static_cast<uint32_t>(obase) + slot : p;   // (slot valid when shade)
     if (shade) {
         const size_t at = rbase + slot;
         stn(&b.rf(0)[at], ptx); stn(&b.rf(1)[at], pty); stn(&b.rf(2)[at], ptz);
@@ -689,8 +692,9 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         stn(&b.rf(6)[at], sig);
         stn(&b.ru(0)[at], static_cast<uint32_t>(h.obj));
         stn(&b.ru(1)[at], static_cast<uint32_t>(h.prim));
-        stn(&b.ru(2)[at], p);
+        stn(&b.ru(2)[at], chain);
         stn(&b.ru(3)[at], occ);
+        if constexpr (kCam) stn(&b.cpix()[chain], p);
     }
     const uint32_t rslot = lds_append(&counts[1], refl);
     if (refl) {
@@ -699,7 +703,7 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         stn(&b.qf(qn, 0)[at], rr.ox); stn(&b.qf(qn, 1)[at], rr.oy); stn(&b.qf(qn, 2)[at], rr.oz);
         stn(&b.qf(qn, 3)[at], rr.dx); stn(&b.qf(qn, 4)[at], rr.dy); stn(&b.qf(qn, 5)[at], rr.dz);
         stn(&b.qf(qn, 6)[at], nsig);
-        stn(&b.qpix(qn)[at], p);
+        stn(&b.qpix(qn)[at], chain);
     }
 }
 
@@ -844,7 +848,7 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
     const double dx = ldn_if<2>(&b.rf(3)[at]), dy = ldn_if<2>(&b.rf(4)[at]), dz = ldn_if<2>(&b.rf(5)[at]);
     const double sig = ldn_if<2>(&b.rf(6)[at]);
     const int32_t obj = static_cast<int32_t>(ldn_if<2>(&b.ru(0)[at]));
-    const uint32_t p = ldn_if<2>(&b.ru(2)[at]);
+    const uint32_t c = ldn_if<2>(&b.ru(2)[at]);             // the record's chain
     const DevMaterial& m = sc.mats[obj];
     Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
     double nx, ny, nz;
@@ -860,18 +864,16 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
         light_dir(L, ptx, pty, ptz, lx, ly, lz, r2);
         add_light(res, m, L, diffuse, specular, sh.f, lx, ly, lz, nx, ny, nz, dx, dy, dz);
     }
-    // (timing probe only, wrong images: levels and terminals at the record's slot, i.e. coalesced)
-    const uint32_t pl = RT_PROBE_LEVREC ? static_cast<uint32_t>(at - static_cast<size_t>(k) * b.qcap) : p;
     if (specular) {
-        const size_t st = static_cast<size_t>(k) * b.capa + pl;
+        const size_t st = static_cast<size_t>(k) * b.capa + c;
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
         stn(&b.lobj()[st], obj);
         if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
     } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
         stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
-        stn(&b.ru(2)[at], p | kChainEnd);
+        stn(&b.ru(2)[at], c | kChainEnd);
     } else {
-        set_terminal(b, pl, res, k);
+        set_terminal(b, c, res, k);
     }
 }
 
@@ -1017,7 +1019,6 @@ __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, 
             if (k - u >= 0) {
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
                 ob[u] = ldn_if<kNtFold>(&b.lobj()[at]);
-                if (RT_PROBE_LEVREC && static_cast<uint32_t>(ob[u]) >= static_cast<uint32_t>(sc.n_spheres + sc.n_planes)) ob[u] = 0;
                 sr[u] = ldn_if<kNtFold>(&b.lf(0)[at]); sg[u] = ldn_if<kNtFold>(&b.lf(1)[at]); sb[u] = ldn_if<kNtFold>(&b.lf(2)[at]);
             }
         }
@@ -1043,9 +1044,7 @@ __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, 
 }
 
 template <bool kFresnel>
-__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {
-    if (nlev == kNlevDone) return Col{sc.bg[0], sc.bg[1], sc.bg[2]};   // camera miss, no levels
-    if (RT_PROBE_LEVREC && nlev > b.levels) nlev = static_cast<uint8_t>(b.levels);   // (probe: stale entries)
+__device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {   // p: the chain
     const Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
     return fold_levels<kFresnel>(sc, b, p, nlev, acc);
 }
@@ -1069,72 +1068,45 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FramePara
     const size_t rk = static_cast<size_t>(k) * b.qcap;
     RT_FOR_CHUNKS(b, n, j) {
         if (j >= n) continue;
-        uint32_t p;
+        uint32_t c;                                            // the chain
         Col acc;
         if (j < nr) {
             const size_t at = rk + region_entry(s_scan[0], b.G, b.R, j);
             const uint32_t pf = ldn(&b.ru(2)[at]);
             if (!(pf & kChainEnd)) continue;                   // specular: its chain goes on
-            p = pf & ~kChainEnd;
+            c = pf & ~kChainEnd;
             acc = Col{ldn(&b.rf(0)[at]), ldn(&b.rf(1)[at]), ldn(&b.rf(2)[at])};
         } else {
             const size_t at = rk + region_entry(s_scan[1], b.G, b.R, j - nr);
-            p = ldn(&b.dpix()[at]);
+            c = ldn(&b.dpix()[at]);
             acc = end_colour(sc, ldn(&b.dobj()[at]));
         }
-        const Col res = average_samples(fold_levels<kFresnel>(sc, b, p, k, acc), fp.spp);
+        const Col res = average_samples(fold_levels<kFresnel>(sc, b, c, k, acc), fp.spp);
+        const uint32_t p = b.cpix()[c];
         write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
     }
 }
 
-// One pixel per work-item.  The quantisation table is staged in LDS: the
-// binary search indexes it with a different entry per lane, which from
-// __constant__ memory costs nine dependent vector loads per channel.
-// kStaged: each workgroup's 256 pixels lie in one output row (tile_w % 256
-// == 0, BGR rows unpadded and dword aligned): the workgroup assembles its
-// 3 KiB of RGB and 768 B of BGR in LDS and stores them as whole dwords.
-// Pixels [pix0, pix1) of the chunk: the whole chunk, or one row band of it
-// when the caller copies the output to the host band by band (rt_render).
-template <bool kStaged, bool kFresnel>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t pix0, uint32_t pix1) {
-    __shared__ float s_rgb[3 * kBlock];
-    __shared__ uint32_t s_bgr[3 * kBlock / 4];
+// One chain per work-item: chain c (generation 0's record entry c, region
+// c / R) folds its levels onto its terminal and writes pixel cpix[c].  Entries
+// past their region's record count are empty (a 256-entry block lies in one
+// region: R is a multiple of 1024).  The quantisation table is staged in LDS:
+// the binary search indexes it with a different entry per lane, which from
+// __constant__ memory costs nine dependent vector loads per channel.  Levels
+// and terminals are read in chain order, i.e. coalesced.
+template <bool kFresnel>
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
     __shared__ double s_srgb[255];
+    const uint32_t base = blockIdx.x * kBlock;
+    const uint32_t cnt = b.rs()[base / b.R];              // generation 0: rs[0 * G + region]
+    if (base % b.R >= cnt) return;                         // nothing in this block
     for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
-    const uint32_t npix = pix1;
-    const uint32_t base = pix0 + blockIdx.x * kBlock;
-    const uint32_t p = base + threadIdx.x;
-    const uint8_t nlev = p < npix ? b.nlev()[p] : kNlevDone;
-    // pixels marked done were written by wf_nearest; a workgroup of them has nothing to do
-    if (__syncthreads_and(nlev == kNlevDone)) return;
-    if constexpr (!kStaged) {
-        if (p < npix && nlev != kNlevDone) {
-            const Col res = average_samples(fold_pixel<kFresnel>(sc, b, p, nlev), fp.spp);
-            write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
-        }
-    } else {
-        // the whole 256-pixel row segment is stored; done pixels re-derive the
-        // background (bit-identical to the host-computed value) without loads
-        const Col res = average_samples(fold_pixel<kFresnel>(sc, b, p, nlev), fp.spp);   // npix % 256 == 0 here
-        s_rgb[3 * threadIdx.x + 0] = static_cast<float>(res.r);
-        s_rgb[3 * threadIdx.x + 1] = static_cast<float>(res.g);
-        s_rgb[3 * threadIdx.x + 2] = static_cast<float>(res.b);
-        __syncthreads();                                   // also publishes s_srgb
-        uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr);
-        sb[3 * threadIdx.x + 0] = to_srgb(res.b, s_srgb);
-        sb[3 * threadIdx.x + 1] = to_srgb(res.g, s_srgb);
-        sb[3 * threadIdx.x + 2] = to_srgb(res.r, s_srgb);
-        const uint32_t row = fp.row0 + base / fp.tile_w, lx0 = base % fp.tile_w;
-        if (fp.out_rgb) {
-            float* dst = fp.out_rgb + (static_cast<size_t>(row) * fp.tile_w + lx0) * 3;
-            for (int q = threadIdx.x; q < 3 * kBlock; q += kBlock) dst[q] = s_rgb[q];
-        }
-        __syncthreads();
-        if (fp.out_bgr && threadIdx.x < 3 * kBlock / 4) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(fp.out_bgr + static_cast<size_t>(row) * fp.bgr_pitch + 3 * lx0);
-            dst[threadIdx.x] = s_bgr[threadIdx.x];
-        }
-    }
+    __syncthreads();
+    const uint32_t c = base + threadIdx.x;
+    if (c % b.R >= cnt) return;
+    const uint32_t p = b.cpix()[c];
+    const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, b.nlev()[c]), fp.spp);
+    write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
 }
 
 // Scene::intersect calls of this chunk: every pixel's camera ray, every later
@@ -1351,30 +1323,15 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
     }
     const hipStream_t s = ws.a;
-    const bool staged = fp.tile_w % kBlock == 0 && fp.bgr_pitch == 3 * fp.tile_w &&
-                        (reinterpret_cast<uintptr_t>(fp.out_bgr) & 3) == 0;
-    // the fold in ws.fold_bands row bands when the caller copies band by band (an event
-    // after each: that band's output is final); band boundaries are whole rows, so with
-    // tile_w % 256 == 0 every band starts on a 256-pixel boundary (the staged fold's rows)
-    const uint32_t nbands = ws.fold_ev ? static_cast<uint32_t>(max(1, ws.fold_bands)) : 1u;
-    const uint32_t band_rows = (fp.rows + nbands - 1) / nbands;
-    for (uint32_t bi = 0; bi < nbands; ++bi) {
-        const uint32_t r0 = min(fp.rows, bi * band_rows), r1 = min(fp.rows, r0 + band_rows);
-        if (r1 > r0 && !b.eager) {                  // eager: every pixel was written by its generation
-            const uint32_t p0 = r0 * fp.tile_w, p1 = r1 * fp.tile_w;
-            const dim3 gf((p1 - p0 + kBlock - 1) / kBlock);
-            if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
-            if (sc.has_fresnel) {
-                if (staged) hipLaunchKernelGGL((wf_fold<true, true>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
-                else hipLaunchKernelGGL((wf_fold<false, true>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
-            } else {
-                if (staged) hipLaunchKernelGGL((wf_fold<true, false>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
-                else hipLaunchKernelGGL((wf_fold<false, false>), gf, dim3(kBlock), 0, s, sc, fp, b, p0, p1);
-            }
-            if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
-        }
-        if (ws.fold_ev && (e = hipEventRecord(ws.fold_ev[bi], s)) != hipSuccess) return e;
+    if (!b.eager) {
+        if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
+        const dim3 gf(static_cast<uint32_t>(b.qcap / kBlock));         // qcap = G * R, R % 1024 == 0
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), gf, dim3(kBlock), 0, s, sc, fp, b);
+        else hipLaunchKernelGGL((wf_fold<false>), gf, dim3(kBlock), 0, s, sc, fp, b);
+        if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
     }
+    // every row of the chunk is final now (the fold runs in chain order, not by rows)
+    if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, s)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -463,9 +463,8 @@ def test_kernel_times(gpu_ctx):
     assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
     # shading runs in its own kernel unless the context is tuned fuse=1 (then inside the shadow kernels)
     assert kt["shade"][1] in (0, 2 * (gens - 1))
-    # frame-end fold (default): rt_render folds a one-chunk frame in 8 row bands (each
-    # copied to the host as it finishes)
-    assert kt["fold"][1] == 2 * 8 and kt["tally"][1] == 2
+    # frame-end fold (default): one launch per chunk, in chain order
+    assert kt["fold"][1] == 2 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
     assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested
     # eager fold: one wf_fold_gen per generation, on the shading streams

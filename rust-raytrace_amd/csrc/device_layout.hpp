@@ -313,6 +313,7 @@ struct WfBufs {
 // eager fold: wf_shade marks a record whose chain ends there (ru(2) = pixel | kChainEnd)
 // and leaves its final colour in rf(0..2) (the hit point is dead by then)
 constexpr uint32_t kChainEnd = 0x80000000u;
+constexpr uint32_t kNlevRunning = 0xFFu;   // WfBufs::nlev of a chain that has not ended yet
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
 constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G

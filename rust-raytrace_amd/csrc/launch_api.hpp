@@ -81,7 +81,10 @@ struct WfStreams {
                         // spheres from LDS (1) or HBM/L2 (2); 0: the general shadow kernel
     hipEvent_t* fold_ev;// recorded once the chunk's pixels are final (null: no event)
     hipEvent_t* gen_done; // eager fold (WfBufs::eager): kMaxGenerations events, generation k's
-                          //   wf_fold_gen done (the next generation's fold waits for it)
+                          //   wf_fold_gen done (the next generation's fold waits for it); split
+                          //   fold: gen_done[K-1] = generation K-1's shading done
+    int fold_split;       // > 0: chains that ended by generation K = fold_split are folded on
+                          //   generation K's b stream (with two b streams), the rest at the end
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

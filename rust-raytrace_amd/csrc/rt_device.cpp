@@ -34,7 +34,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -79,7 +79,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"tail_max", 0, 0, INT32_MAX},               // 0: CUs x 256 (one quad-walk round: one workgroup of 256 rays per CU)
     {"eager_fold", 0, 0, 1},                     // 1: each generation folds the chains that ended in it (B streams;
                                                  // measured slower: scattered level gathers);
-                                                 // 0: one fold over every pixel after the last generation
+                                                 // 0: one fold over every chain after the last generation
+    {"fold_split", 0, 0, 32},                    // K > 0: chains that ended by generation K fold on a B stream
+                                                 // during the later generations, the rest after the last one
 };
 
 }  // namespace
@@ -1073,6 +1075,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             }
             ws.near_done = L.near_done.data();
             ws.gen_done = L.gen_done.data();
+            ws.fold_split = static_cast<int>(c->t(kTuneFoldSplit));
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
             ws.cam = cam;

@@ -694,7 +694,10 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         stn(&b.ru(1)[at], static_cast<uint32_t>(h.prim));
         stn(&b.ru(2)[at], chain);
         stn(&b.ru(3)[at], occ);
-        if constexpr (kCam) stn(&b.cpix()[chain], p);
+        if constexpr (kCam) {
+            stn(&b.cpix()[chain], p);
+            b.nlev()[chain] = kNlevRunning;                   // set_terminal gives the level count
+        }
     }
     const uint32_t rslot = lds_append(&counts[1], refl);
     if (refl) {
@@ -1094,19 +1097,37 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FramePara
 // the binary search indexes it with a different entry per lane, which from
 // __constant__ memory costs nine dependent vector loads per channel.  Levels
 // and terminals are read in chain order, i.e. coalesced.
+// Only chains of lo <= nlev <= hi: the split fold (tuning fold_split = K) folds
+// the chains that ended by generation K on a B stream while the later
+// generations run (every level and terminal they need is written by then),
+// and the rest after the last generation.
 template <bool kFresnel>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b) {
+__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
     __shared__ double s_srgb[255];
     const uint32_t base = blockIdx.x * kBlock;
     const uint32_t cnt = b.rs()[base / b.R];              // generation 0: rs[0 * G + region]
     if (base % b.R >= cnt) return;                         // nothing in this block
+    const uint32_t c = base + threadIdx.x;
+    const uint32_t nlev = c % b.R < cnt ? b.nlev()[c] : kNlevRunning;
+    const bool mine = nlev >= lo && nlev <= hi;            // (kNlevRunning: not ended yet / no chain)
+    if (__syncthreads_or(mine) == 0) return;
     for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
     __syncthreads();
-    const uint32_t c = base + threadIdx.x;
-    if (c % b.R >= cnt) return;
+    if (!mine) return;
     const uint32_t p = b.cpix()[c];
-    const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, b.nlev()[c]), fp.spp);
+    const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, static_cast<uint8_t>(nlev)), fp.spp);
     write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+}
+
+template <bool kUnused = false>
+hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& b, hipStream_t s, LaunchMarks* m,
+                       uint32_t lo, uint32_t hi) {
+    hipError_t e;
+    if (m && (e = m->begin(s)) != hipSuccess) return e;
+    const dim3 gf(static_cast<uint32_t>(b.qcap / kBlock));             // qcap = G * R, R % 1024 == 0
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), gf, dim3(kBlock), 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), gf, dim3(kBlock), 0, s, sc, fp, b, lo, hi);
+    return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 
 // Scene::intersect calls of this chunk: every pixel's camera ray, every later
@@ -1161,6 +1182,11 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
                           hipStream_t sb, LaunchMarks* mb, bool lists);
+
+// The split fold applies with B streams of their own and 1 <= K <= max_depth.
+inline bool split_fold(const WfStreams& ws, const FrameParams& fp) {
+    return ws.fold_split >= 1 && static_cast<uint32_t>(ws.fold_split) <= fp.max_depth && ws.b[0] != ws.a;
+}
 
 template <int kSrcN, int kSrcO, bool kCount>
 hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws) {
@@ -1219,7 +1245,14 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         if ((e = hipStreamWaitEvent(sb, ws.near_done[k], 0)) != hipSuccess) return e;
     }
     if (shaded && (e = launch_shading<kSrcO, kCount>(sc, fp, b, k, ws, sb, mb, lists)) != hipSuccess) return e;
-    if (!b.eager) return hipSuccess;
+    if (!b.eager) {
+        if (!split_fold(ws, fp) || sb == ws.a) return hipSuccess;
+        // split fold: the chains that ended by generation K, once the shading of K and K-1 is done
+        if (k == ws.fold_split - 1 && (e = hipEventRecord(ws.gen_done[k], sb)) != hipSuccess) return e;
+        if (k != ws.fold_split) return hipSuccess;
+        if (ws.b[(k - 1) % ws.nb] != sb && (e = hipStreamWaitEvent(sb, ws.gen_done[k - 1], 0)) != hipSuccess) return e;
+        return launch_fold(sc, fp, b, sb, mb, 0u, static_cast<uint32_t>(k));
+    }
     // eager fold of the chains that ended in generation k, after generation k-1's fold
     // (on another b stream: every level below k is then written)
     if (k > 0 && ws.b[(k - 1) % ws.nb] != sb && (e = hipStreamWaitEvent(sb, ws.gen_done[k - 1], 0)) != hipSuccess) return e;
@@ -1323,13 +1356,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
     }
     const hipStream_t s = ws.a;
-    if (!b.eager) {
-        if (ws.ma && (e = ws.ma->begin(s)) != hipSuccess) return e;
-        const dim3 gf(static_cast<uint32_t>(b.qcap / kBlock));         // qcap = G * R, R % 1024 == 0
-        if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), gf, dim3(kBlock), 0, s, sc, fp, b);
-        else hipLaunchKernelGGL((wf_fold<false>), gf, dim3(kBlock), 0, s, sc, fp, b);
-        if (ws.ma && (e = ws.ma->mark(s, kKfFold)) != hipSuccess) return e;
-    }
+    // the chains not folded early (all of them without the split)
+    if (!b.eager && (e = launch_fold(sc, fp, b, s, ws.ma, split_fold(ws, fp) ? ws.fold_split + 1u : 0u, kNlevRunning - 1u)) != hipSuccess)
+        return e;
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
     if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, s)) != hipSuccess) return e;
     return hipGetLastError();

@@ -581,7 +581,9 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10),
                dict(tail_from=0), dict(tail_from=1, tail_max=1 << 30), dict(tail_from=2, tail_max=20000, lists=0),
                dict(tail_from=1, tail_max=1 << 30, regions=96), dict(eager_fold=1), dict(eager_fold=1, split=0),
-               dict(eager_fold=1, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1)]:
+               dict(eager_fold=1, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1),
+               dict(fold_split=1), dict(fold_split=4), dict(fold_split=8), dict(fold_split=3, bstreams=1),
+               dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

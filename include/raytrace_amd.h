@@ -271,7 +271,9 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * hand queues of <= tail_max rays to a walk with four lanes per ray on the 4-wide
  * tree; tail_from 0 off, -1 auto: 5 for chunks of <= 32 x tail_max pixels;
  * tail_max 0: CUs x 256), eager_fold (1: each generation folds the pixels whose
- * chain ended in it, on the shading streams; 0: one fold after the last generation).
+ * chain ended in it, on the shading streams; 0: one fold after the last generation),
+ * fold_split (K > 0: chains that ended by generation K fold on a shading stream
+ * during the later generations, the rest after the last one).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -1114,11 +1114,7 @@ __global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, W
     for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
     __syncthreads();
     if (!mine) return;
-#ifndef RT_PROBE_FOLDW
-#define RT_PROBE_FOLDW 0
-#endif
-    // (A/B timing probe only, wrong images: the pixel written is the chain id, i.e. coalesced)
-    const uint32_t p = RT_PROBE_FOLDW ? c % (fp.tile_w * fp.rows) : b.cpix()[c];
+    const uint32_t p = b.cpix()[c];
     const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, static_cast<uint8_t>(nlev)), fp.spp);
     write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
 }

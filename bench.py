@@ -530,8 +530,12 @@ def main():
         algo_bytes = pixels_local * (12 + 3) + scene_bytes          # f32 RGB + u8 BGR writes + scene read once
         achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
         key = f"{args.config}_{W}x{H}_n{args.spheres}_d{args.depth}" + ("_dense" if args.view == "dense" else "")
-        traffic, traffic_source = pmc_traffic(key, lr.sources_id()) if world == 1 else \
-            (None, "per-rank PMC traffic is measured at N = 1 only")
+        if world > 1:
+            traffic, traffic_source = None, "per-rank PMC traffic is measured at N = 1 only"
+        elif args.shard_of > 1:                 # one rank's bands only: not the whole frame the key names
+            traffic, traffic_source = None, "PMC traffic is measured on whole frames, not on --shard-of shares"
+        else:
+            traffic, traffic_source = pmc_traffic(key, lr.sources_id())
         kernels = {}
         for fam, (ms, n) in ktimes.items():
             if n:

@@ -1,6 +1,6 @@
 """Per-launch timeline of the last uninstrumented wavefront frame of a
 rocprofv3 --kernel-trace run (directory argument): start (us from the frame's
-first launch), duration (us), stream, kernel."""
+first launch), duration (us), stream, kernel; up to the frame-end fold."""
 import csv
 import sys
 
@@ -17,11 +17,13 @@ def targs(name):
 starts = [i for i, t in enumerate(tr) if "wf_nearest<" in t["Kernel_Name"] and targs(t["Kernel_Name"])[1:3] == ["true", "false"]]
 i0 = starts[-1]
 t0 = int(tr[i0]["Start_Timestamp"])
-for t in tr[i0:]:
+for j, t in enumerate(tr[i0:]):
+    if j > 0 and "wf_nearest<" in t["Kernel_Name"] and targs(t["Kernel_Name"])[1:2] == ["true"]:
+        break                                      # the next frame (e.g. the instrumented one)
     s = (int(t["Start_Timestamp"]) - t0) / 1e3
     dur = (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3
     name = t["Kernel_Name"].replace("rtamd::(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     q = t.get("Stream_Id") or t.get("Queue_Id") or ""
     print(f"{s:8.1f} {dur:8.1f}  {q:>3}  {name}")
-    if "wf_tally" in name:
+    if name.startswith("wf_fold<"):               # the frame-end fold (after the tally since round 3)
         break

@@ -10,10 +10,10 @@ the host gather are reported beside `value`, never in it).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
-Every N measures the headline config C3 (the N = 1 line is the headline
-number; N > 1 weak-scales it, below); --config c4 --scaling strong --gpus N
-gives BASELINE config 4's curve (8192², 10k spheres, depth 8, one image tiled
-across the N GPUs).  --inflight F renders
+Every N measures the headline config C3: the N = 1 line is the headline
+number, and N > 1 deals that same 4096² frame over the N GPUs (strong
+scaling, below); --config c4 --gpus N gives BASELINE config 4's curve
+(8192², 10k spheres, depth 8, one image tiled across the N GPUs).  --inflight F renders
 successive steps through F contexts into F output buffers (every step still
 one whole frame, all K finished inside the timed region); the roofline's
 per-render duration then comes from K further renders issued one at a time.
@@ -23,12 +23,13 @@ processes itself (before anything touches a GPU), one device each; under
 torchrun it uses the launcher's ranks.  Pixels are independent (main.rs:45-57),
 so the frame's rows are dealt in 16-row bands round-robin over the ranks
 (libraytrace/shard.py) and no collective touches the data path (RCCL carries
-the barrier and the max-over-ranks timing only).  Default "scaling": "weak"
-(the path partitions, so per-GPU work stays fixed): the same scene and view at
-sqrt(N) x the resolution, every rank rendering a 4096^2-pixel share of it, and
-value = the rays of all ranks x K / max-over-ranks time.  --scaling strong
-deals the N = 1 frame itself over the N ranks (BASELINE config 4's "image tiled
-across GPUs"; per-rank projection on one GPU: --scaling strong --shard-of N).
+the barrier and the max-over-ranks timing only).  Default "scaling": "strong":
+the N = 1 frame itself dealt over the N ranks (the metric's own 4096² config,
+BASELINE config 4's "image tiled across GPUs"; per-rank projection on one GPU:
+--shard-of N), value = the frame's rays x K / max-over-ranks time.  --scaling
+weak (opt-in) renders the same scene and view at sqrt(N) x the resolution,
+every rank a 4096^2-pixel share; its line names that larger frame in
+`metric`, never the headline's.
 After the timed region every rank copies its bands into ONE shared page-locked
 host frame (the host gather of SURVEY §8(e)), timed and reported as
 `host_gather`.  --config c4 / c5 select the larger configs of BASELINE.json;
@@ -81,10 +82,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=20.0,
                    help="target CPU time of the cpu_baseline samples (split between 1 thread and all threads)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                   help="N > 1: weak (default) = the frame side grows by sqrt(N) (same scene and view, row bands "
-                        "dealt round-robin, every rank renders the N=1 pixel count); strong = the N=1 frame dealt "
-                        "over N ranks")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="N > 1: strong (default) = the N=1 frame dealt over N ranks in row bands; weak = the frame "
+                        "side grows by sqrt(N) (same scene and view, every rank renders the N=1 pixel count; the "
+                        "line's metric then names the larger frame)")
     p.add_argument("--shard-of", type=int, default=0,
                    help="(diagnostic, one process) render only rank 0's row bands of an N-rank frame; "
                         "its time is what each rank of an N-GPU run spends")
@@ -168,11 +169,13 @@ def cpu_share():
     return n
 
 
-def cpu_sample(spec, threads, budget_s, draws):
+def cpu_sample(spec, threads, budget_s, draws, use_lib=None):
     """The oracle (algorithmically the reference: same recursion, same linear
     scan, f64) on a deterministic sample of the same frame: every stride-th row,
     a centred window of columns, grown until it takes about budget_s."""
     from oracle import ref64
+    if use_lib is not None:
+        draws = dict(draws, use_lib=use_lib)
     W, H = spec.width, spec.height
     stride, tw = max(1, H // 4), min(W, 64)
     for _ in range(8):
@@ -197,11 +200,24 @@ def cpu_sample(spec, threads, budget_s, draws):
 
 
 def cpu_baseline(spec, args, **draws):
+    """the oracle built -O3 -march=native for this host (no FP
+    contraction: the same bits as the checker build, verified on a small tile
+    first) on every host thread this job may use, and on one thread."""
+    from oracle import ref64
+    import numpy as np
     share = cpu_share()
-    one = cpu_sample(spec, 1, args.cpu_seconds / 2, draws)
-    allc = cpu_sample(spec, share, args.cpu_seconds / 2, draws) if share > 1 else one
+    try:
+        nlib, build = ref64.native_lib()
+        probe = dict(x0=spec.width // 2 - 8, tile_w=16, y0=spec.height // 2 - 4, tile_h=8, threads=1, **draws)
+        a, b = ref64.render(spec, **probe), ref64.render(spec, use_lib=nlib, **probe)
+        if not (np.array_equal(a["bgr"], b["bgr"]) and np.array_equal(a["rgb32"], b["rgb32"])):
+            raise RuntimeError("the -march=native build differs from the checker build")
+    except Exception as e:                  # no compiler on this host: the checker build (-O2), said so
+        nlib, build = None, f"oracle/Makefile (-O2; native build failed: {e})"
+    one = cpu_sample(spec, 1, args.cpu_seconds / 2, draws, nlib)
+    allc = cpu_sample(spec, share, args.cpu_seconds / 2, draws, nlib) if share > 1 else one
     return {"value": allc["value"], "unit": "Mrays/s", "cores": allc["threads"], "kind": "port",
-            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "build": build,
             "sample": f"{allc['sample']}; {allc['rays']} rays in {allc['seconds']} s; oracle/ref64.c "
                       f"(linear scan, f64), {allc['threads']} threads",
             "one_thread": {"value": one["value"], "unit": "Mrays/s",
@@ -314,6 +330,32 @@ def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
     return best, pinned
 
 
+CONFIGS = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
+           "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}       # side, spheres, depth, seed, box scale (scenes.config*)
+HEADLINE_METRIC = "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline"   # BASELINE.json
+
+
+def frame_of(args, band_world):
+    """(W, H, base (W, H)) of the job's frame: the config's side (or --width/--height);
+    weak scaling over band_world > 1 ranks grows it by sqrt(band_world)."""
+    side = CONFIGS[args.config][0]
+    base = (args.width or side, args.height or side)
+    if band_world > 1 and args.scaling == "weak":
+        return weak_frame(base[0], base[1], band_world) + (base,)
+    return base + (base,)
+
+
+def metric_name(config, spheres, depth, view, W, H, scaling="strong", ranks=1):
+    """BASELINE.json's metric string only for the headline workload itself (the
+    4096^2 / 1000-sphere / depth-8 frame, default view); any other frame -- a
+    weak-scaled N-GPU frame included -- names its own size."""
+    if config == "c3" and (W, H) == (4096, 4096) and spheres == 1000 and depth == 8 and view == "default":
+        return HEADLINE_METRIC
+    return (f"Mrays/sec at {W}x{H}, {spheres} spheres, depth {depth}" + (" (dense view)" if view == "dense" else "") +
+            (f" (weak scaling: {ranks} ranks, each a {W * H // max(1, ranks)}-pixel share)"
+             if scaling == "weak" and ranks > 1 else ""))
+
+
 def weak_frame(w, h, n):
     """Weak scaling over n ranks: the same view at sqrt(n) x the resolution,
     sides rounded to whole 16-row bands, so each rank renders (up to that
@@ -368,8 +410,14 @@ def main():
     if args.dry_run:
         n_gpus = distinct_devices()
         if rank == 0:
+            dw, dh, _ = frame_of(args, world)
+            cf = CONFIGS[args.config]
             print(json.dumps({"dry_run": True, "ranks": world, "n_gpus": n_gpus, "devices_visible": n_dev,
-                              "scaling": args.scaling, "backend": args.dist_backend, "config": args.config}),
+                              "scaling": args.scaling, "backend": args.dist_backend, "config": args.config,
+                              "frame": [dw, dh],
+                              "metric": metric_name(args.config, args.spheres or cf[1],
+                                                    cf[2] if args.depth < 0 else args.depth, args.view, dw, dh,
+                                                    args.scaling, world)}),
                   flush=True)
         if world > 1:
             dist.destroy_process_group()
@@ -380,15 +428,10 @@ def main():
     from libraytrace import scenes, shard
     dev = torch.device("cuda", local)
 
-    cfg = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
-           "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}[args.config]       # scenes.config1/3/4/5
+    cfg = CONFIGS[args.config]
     path_cfg = args.config == "c1"
-    args.width = args.width or cfg[0]
-    args.height = args.height or cfg[0]
-    base_wh = (args.width, args.height)
     band_world = args.shard_of if (args.shard_of > 1 and world == 1) else world
-    if band_world > 1 and args.scaling == "weak":
-        args.width, args.height = weak_frame(args.width, args.height, band_world)
+    args.width, args.height, base_wh = frame_of(args, band_world)
     args.spheres = args.spheres or cfg[1]
     args.depth = cfg[2] if args.depth < 0 else args.depth
     if path_cfg:
@@ -405,8 +448,17 @@ def main():
     scene = lr.Scene.deserialize(spec.to_text())
     F = max(1, args.inflight)
     ctxs = [lr.Context(local, tuning="env") for _ in range(F)]
+    upload_ms = []
     for c in ctxs:
+        # rt_scene_upload: host BVH + light-view grid builds + the blob's H2D copy, paid once per scene
+        t0u = time.perf_counter()
         c.upload(scene)
+        torch.cuda.synchronize(dev)
+        upload_ms.append((time.perf_counter() - t0u) * 1e3)
+    t0u = time.perf_counter()
+    ctxs[0].upload(scene)                  # again: the blob exists, so no allocation (a caller's scene change)
+    torch.cuda.synchronize(dev)
+    upload_ms.append((time.perf_counter() - t0u) * 1e3)
     ctx = ctxs[0]
     rows = shard.local_rows(H, BAND, band_world, rank)
     algo = {"auto": lr.RT_ALGO_AUTO, "wavefront": lr.RT_ALGO_WAVEFRONT, "lds": lr.RT_ALGO_BRUTE_LDS,
@@ -562,12 +614,9 @@ def main():
                         (f"; weak scaling: the same view at {W}x{H} dealt in {BAND}-row bands over {world} GPUs, "
                          f"each rank a {base_wh[0]}x{base_wh[1]}-pixel share" if args.scaling == "weak" and world > 1
                          else ""))
-            # weak scaling of the headline: every rank renders a 4096^2-pixel share (the N = 1 frame)
-            headline = args.config == "c3" and args.spheres == 1000 and args.depth == 8 and args.view == "default" and (
-                (W, H) == (4096, 4096) or (args.scaling == "weak" and band_world > 1 and base_wh == (4096, 4096)))
-            metric = ("Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline" if headline
-                      else f"Mrays/sec at {W}x{H}, {args.spheres} spheres, depth {args.depth}" +
-                      (" (dense view)" if args.view == "dense" else ""))
+            metric = metric_name(args.config, args.spheres, args.depth, args.view, W, H, args.scaling, band_world)
+            if args.shard_of > 1 and world == 1:          # a diagnostic share, never the headline
+                metric += f" (rank 0's row bands of a {band_world}-rank frame only)"
         line = {
             "metric": metric,
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": n_gpus, "steps": args.steps,
@@ -597,6 +646,9 @@ def main():
                         "generation_queue_sizes": gen_q[:args.depth + 3] if world == 1 else None,
                         "generation_shaded": gen_s[:args.depth + 3] if world == 1 else None},
         }
+        line["upload_ms"] = {"first": round(upload_ms[0], 3), "repeat": round(min(upload_ms[1:]), 3),
+                             "note": "rt_scene_upload once per scene, outside the timed region: host SAH BVH + "
+                                     "4-wide tree + light-view grids + camera view, then one H2D copy of the blob"}
         if gather_ms is not None:
             line["host_gather"] = {"ms": round(gather_ms, 3), "pinned": bool(gather_pinned),
                                    "bytes": H * W * 15,

@@ -52,7 +52,10 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+/* 4: rt_stats gained `chunks` (80 B); rt_abi_version() added.  A caller checks
+ * rt_abi_version() == RT_ABI_VERSION of the header it was built against before
+ * passing any struct (older callers pass a smaller rt_stats). */
+#define RT_ABI_VERSION 4
 
 enum rt_status {
     RT_OK = 0,
@@ -160,6 +163,8 @@ int rt_bmp_header(uint8_t out[122], uint32_t width, uint32_t height, uint32_t* b
 int rt_write_bmp(const char* path, uint32_t width, uint32_t height, const uint8_t* bgr, uint32_t pitch);
 
 /* ---- device API ---- */
+/* The RT_ABI_VERSION this library was built with. */
+int rt_abi_version(void);
 int rt_device_count(int* n);
 int rt_ctx_create(int device, rt_ctx** out);
 void rt_ctx_destroy(rt_ctx* ctx);
@@ -227,9 +232,10 @@ void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height);
 
 /* Synchronous: renders into caller-owned HOST buffers (either may be NULL).
  * Page-locked buffers (hipHostMalloc / hipHostRegister) receive the DMA
- * directly; pageable ones are filled through two pinned 16 MiB slices, the
- * copy engine writing one while host threads empty the other.  Pass only the
- * outputs needed: BGR alone moves 3 B per pixel instead of 15. */
+ * directly; pageable ones are filled through four pinned 8 MiB staging slices,
+ * the copy engine filling slices ahead while a pool of host threads empties
+ * them in order.  Pass only the outputs needed: BGR alone moves 3 B per pixel
+ * instead of 15 (C3, 4096^2: DESIGN.md §6 gives the measured end-to-end time). */
 int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* out_bgr, rt_stats* stats);
 /* Asynchronous on `stream` (a hipStream_t; NULL = the context's own stream):
  * renders into caller-owned DEVICE buffers.  Statistics of the most recent
@@ -273,7 +279,8 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * tail_max 0: CUs x 256), eager_fold (1: each generation folds the pixels whose
  * chain ended in it, on the shading streams; 0: one fold after the last generation),
  * fold_split (K > 0: chains that ended by generation K fold on a shading stream
- * during the later generations, the rest after the last one).
+ * during the later generations, the rest after the last one; with one or two
+ * shading streams only, ignored with bstreams > 2).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

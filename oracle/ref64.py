@@ -79,10 +79,10 @@ class ref_counts(C.Structure):
                 ("plane_tests", C.c_uint64)]
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} missing: run `make -C oracle`")
-    lib = C.CDLL(LIB_PATH)
+def _load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError(f"{path} missing: run `make -C oracle`")
+    lib = C.CDLL(path)
     P = C.POINTER
     lib.ref_render.restype = C.c_int
     lib.ref_render.argtypes = [P(ref_scene), P(ref_opts), P(C.c_double), P(C.c_float), P(C.c_uint8),
@@ -106,6 +106,29 @@ def _load():
 
 
 lib = _load()
+
+# The CPU baseline build (bench.py's cpu_baseline leg): the same ref64.c at
+# -O3 -march=native, compiled on the host that runs the benchmark (the GPU
+# box's CPU differs from this container's), still without FP contraction or
+# fast-math, so it computes the same bits as the checker build above.
+NATIVE_FLAGS = ["-O3", "-march=native", "-fPIC", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-pthread",
+                "-shared"]
+
+
+def native_lib():
+    """(ctypes lib, compile command) of ref64.c built for this host; raises on failure."""
+    import hashlib
+    import subprocess
+    import tempfile
+    src = os.path.join(HERE, "ref64.c")
+    tag = hashlib.sha1(open(src, "rb").read() + open(os.path.join(HERE, "ref64.h"), "rb").read()).hexdigest()[:12]
+    out = os.path.join(tempfile.gettempdir(), f"ref64_native_{os.getuid()}_{tag}.so")
+    cc = os.environ.get("CC", "gcc")
+    if not os.path.exists(out):
+        tmp = out + f".{os.getpid()}"
+        subprocess.run([cc] + NATIVE_FLAGS + ["-o", tmp, src, "-lm"], check=True, capture_output=True)
+        os.replace(tmp, out)
+    return _load(out), " ".join([cc] + NATIVE_FLAGS) + " ref64.c"
 
 
 def _d3(v):
@@ -187,7 +210,7 @@ class OracleScene:
 
 
 def render(spec, *, max_depth=None, x0=0, tile_w=None, y0=0, tile_h=None, band=1, band_stride=1,
-           band_phase=0, jitter=0, seed=1, threads=0, want_rgb64=True, rng=0):
+           band_phase=0, jitter=0, seed=1, threads=0, want_rgb64=True, rng=0, use_lib=None):
     """Render a tile with the oracle -> dict(rgb64, rgb32, bgr, counts).
     jitter: 0 centre, 1 random; rng: 0 XorShift (the reference's generator,
     sequential), 1 keyed (the device's counter-based specification)."""
@@ -203,7 +226,7 @@ def render(spec, *, max_depth=None, x0=0, tile_w=None, y0=0, tile_h=None, band=1
     bgr = np.zeros((th, pitch), np.uint8)
     cnt = ref_counts()
     P = C.POINTER
-    rc = lib.ref_render(C.byref(sc.scene), C.byref(o),
+    rc = (use_lib or lib).ref_render(C.byref(sc.scene), C.byref(o),
                         rgb64.ctypes.data_as(P(C.c_double)) if want_rgb64 else None,
                         rgb32.ctypes.data_as(P(C.c_float)), bgr.ctypes.data_as(P(C.c_uint8)), pitch, C.byref(cnt))
     if rc != 0:

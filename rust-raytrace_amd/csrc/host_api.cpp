@@ -70,6 +70,8 @@ int rt_scene_get_desc(const rt_scene* s, rt_scene_desc* out) {
 
 void rt_scene_free(rt_scene* s) { delete s; }
 
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
 void rt_render_opts_default(rt_render_opts* o, uint32_t width, uint32_t height) {
     if (!o) return;
     std::memset(o, 0, sizeof *o);

@@ -95,12 +95,20 @@ namespace {
 // pageable memory at ~20-28 GB/s, below the DMA's 56 GB/s).  Workers spin
 // briefly for the next slice before sleeping, so consecutive slices of a frame
 // do not pay a wake-up each.
+//
+// Each job is published as a snapshot under m_: a worker copies the job's
+// fields under the mutex and counts itself in active_ before it takes parts,
+// and copy() publishes (and resets the part counters) only once active_ is 0,
+// i.e. no worker can still be inside the previous job's part loop.  So a
+// worker never mixes two jobs' fields and never claims a part of a job it did
+// not snapshot.
 class HostCopyPool {
 public:
     ~HostCopyPool() {
-        stop_.store(true);
         {
             std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (std::thread& t : th_) t.join();
@@ -108,36 +116,39 @@ public:
     void copy(void* to, const void* from, size_t len) {
         if (th_.empty()) start();
         const size_t parts = std::max<size_t>(1, std::min<size_t>(kParts, len >> 20));   // >= 1 MiB each
-        if (parts == 1) { std::memcpy(to, from, len); return; }
-        to_ = static_cast<uint8_t*>(to);
-        from_ = static_cast<const uint8_t*>(from);
-        len_ = len;
-        parts_ = parts;
-        step_ = (len + parts - 1) / parts;
-        done_.store(0);
-        next_.store(0);
+        if (parts == 1 || th_.empty()) { std::memcpy(to, from, len); return; }
+        const Job j{static_cast<uint8_t*>(to), static_cast<const uint8_t*>(from), len, parts, (len + parts - 1) / parts};
         {
-            std::lock_guard<std::mutex> g(m_);
+            std::unique_lock<std::mutex> lk(m_);
+            idle_.wait(lk, [&] { return active_ == 0; });    // every worker has left the previous job
+            job_ = j;
+            next_.store(0, std::memory_order_relaxed);
+            done_.store(0, std::memory_order_relaxed);
             gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
-        work();
+        work(j);
         while (done_.load(std::memory_order_acquire) != parts) std::this_thread::yield();
     }
 
 private:
+    struct Job {
+        uint8_t* to = nullptr;
+        const uint8_t* from = nullptr;
+        size_t len = 0, parts = 0, step = 0;
+    };
     static constexpr size_t kParts = 8;
     void start() {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned n = std::min<unsigned>(kParts - 1, hw > 1 ? hw - 1 : 1u);
         for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
     }
-    void work() {                       // take parts until none is left
+    void work(const Job& j) {           // take parts of job j until none is left
         for (;;) {
-            const size_t q = next_.fetch_add(1);
-            if (q >= parts_) return;
-            const size_t a = q * step_, b = std::min(len_, a + step_);
-            if (a < b) std::memcpy(to_ + a, from_ + a, b - a);
+            const size_t q = next_.fetch_add(1, std::memory_order_relaxed);
+            if (q >= j.parts) return;
+            const size_t a = q * j.step, b = std::min(j.len, a + j.step);
+            if (a < b) std::memcpy(j.to + a, j.from + a, b - a);
             done_.fetch_add(1, std::memory_order_release);
         }
     }
@@ -145,31 +156,34 @@ private:
         uint64_t seen = 0;
         for (;;) {
             // spin at most ~200 us for the next slice (the DMA of one slice takes ~150 us), then sleep
-            uint64_t g = gen_.load(std::memory_order_acquire);
             const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(200);
-            while (g == seen && !stop_.load() && std::chrono::steady_clock::now() < until) {
+            while (gen_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < until)
                 std::this_thread::yield();
-                g = gen_.load(std::memory_order_acquire);
-            }
-            if (g == seen) {
+            Job j;
+            {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
-                g = gen_.load(std::memory_order_acquire);
+                cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+                if (stop_) return;
+                seen = gen_.load(std::memory_order_acquire);
+                j = job_;
+                ++active_;
             }
-            if (stop_.load()) return;
-            seen = g;
-            work();
+            work(j);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                --active_;
+            }
+            idle_.notify_all();
         }
     }
     std::vector<std::thread> th_;
     std::mutex m_;
-    std::condition_variable cv_;
-    uint8_t* to_ = nullptr;
-    const uint8_t* from_ = nullptr;
-    size_t len_ = 0, parts_ = 0, step_ = 0;
+    std::condition_variable cv_, idle_;
+    Job job_;                           // the current job (written and read under m_)
+    int active_ = 0;                    // workers inside work() (under m_)
+    bool stop_ = false;                 // (under m_)
     std::atomic<size_t> next_{0}, done_{0};
     std::atomic<uint64_t> gen_{0};
-    std::atomic<bool> stop_{false};
 };
 
 constexpr int kMaxBands = 16;           // row bands of one rt_render copied as they finish
@@ -1023,8 +1037,9 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
-            // eager fold: pixel ids carry the kChainEnd flag in bit 31
-            c->lanes[l].b.eager = c->t(kTuneEagerFold) != 0 && static_cast<uint64_t>(o->tile_w) * chunk_rows < kChainEnd ? 1u : 0u;
+            // eager fold: chain ids (< qcap, which the 8-row tiles and 1024-entry regions round up
+            // past the pixel count) carry the kChainEnd flag in bit 31
+            c->lanes[l].b.eager = c->t(kTuneEagerFold) != 0 && c->lanes[l].b.qcap < kChainEnd ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
         // rt_render copies each chunk's rows as soon as that chunk's fold is done (the fold

@@ -1183,9 +1183,12 @@ template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
                           hipStream_t sb, LaunchMarks* mb, bool lists);
 
-// The split fold applies with B streams of their own and 1 <= K <= max_depth.
+// The split fold applies with B streams of their own (at most two: the fold of
+// generation K waits for K's stream and, through gen_done[K-1], for the other
+// one, so every generation <= K has been shaded only when those two streams
+// carry all of them) and 1 <= K <= max_depth.
 inline bool split_fold(const WfStreams& ws, const FrameParams& fp) {
-    return ws.fold_split >= 1 && static_cast<uint32_t>(ws.fold_split) <= fp.max_depth && ws.b[0] != ws.a;
+    return ws.fold_split >= 1 && static_cast<uint32_t>(ws.fold_split) <= fp.max_depth && ws.b[0] != ws.a && ws.nb <= 2;
 }
 
 template <int kSrcN, int kSrcO, bool kCount>

@@ -20,6 +20,7 @@ PKG_DIR = os.path.dirname(_HERE)
 LIB_PATH = os.environ.get("RT_LIBRTAMD") or os.path.join(PKG_DIR, "librtamd.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "raytrace_amd.h")
 
+RT_ABI_VERSION = 4               # include/raytrace_amd.h
 RT_OK = 0
 RT_E_INVALID, RT_E_NODEVICE, RT_E_HIP, RT_E_NOMEM = -1, -2, -3, -4
 RT_E_UNSUPPORTED, RT_E_PARSE, RT_E_NOSCENE, RT_E_IO = -5, -6, -7, -8
@@ -106,6 +107,7 @@ def _load():
         "rt_to_srgb": (C.c_uint8, [C.c_double]),
         "rt_bmp_header": (C.c_int, [P(C.c_uint8), C.c_uint32, C.c_uint32, P(C.c_uint32)]),
         "rt_write_bmp": (C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, P(C.c_uint8), C.c_uint32]),
+        "rt_abi_version": (C.c_int, []),
         "rt_device_count": (C.c_int, [P(C.c_int)]),
         "rt_ctx_create": (C.c_int, [C.c_int, P(C.c_void_p)]),
         "rt_ctx_destroy": (None, [C.c_void_p]),
@@ -127,6 +129,8 @@ def _load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    if lib.rt_abi_version() != RT_ABI_VERSION:      # the ctypes mirrors below follow this header version
+        raise ImportError(f"{LIB_PATH} has ABI {lib.rt_abi_version()}, these bindings expect {RT_ABI_VERSION}: rebuild")
     return lib
 
 

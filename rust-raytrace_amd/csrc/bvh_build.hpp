@@ -37,6 +37,16 @@ int bvh4_stack_need(const Bvh4Result& b4);
 // Depth of a binary tree (its traversal pushes at most one entry per level).
 int bvh_depth(const BvhResult& b2);
 
+// Clusters of a binary tree for the wave-cooperative query (device_layout.hpp,
+// DevCluster): subtrees of <= kClusterMax spheres; perm = the 8 octant orders,
+// each 64 * slots entries.  Empty when there are more than 64 * kClusterSlotsMax.
+struct ClusterResult {
+    std::vector<DevCluster> clusters;
+    std::vector<uint16_t> perm;
+    int slots = 0;
+};
+ClusterResult build_clusters(const BvhResult& b2, size_t n_spheres);
+
 // The binary tree's nodes with binary16 bounds rounded outward (DevBvhNodeH);
 // empty when some bound is not finite or lies outside the half range.
 std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2);

@@ -127,6 +127,23 @@ struct DevLgEntry {
     float near;
 };
 
+// Sphere clusters for the wave-cooperative nearest query (nearest_wave): the
+// subtrees of the binary BVH cut where a subtree holds <= kClusterMax spheres
+// (host_bvh.cpp build_clusters).  A cluster's spheres are one contiguous range
+// of the leaf order; its box is the binary tree's f32 box of that subtree
+// (padded and rounded outward, so every hit point the exact test can report
+// lies inside it).  cl_perm[octant][slot]: the clusters in increasing order of
+// their centres along the octant's diagonal (a heuristic near-to-far order),
+// kClusterNone in unused slots; slots = 64 * DevScene::cl_slots.
+constexpr int kClusterMax = 16;
+constexpr int kClusterSlotsMax = 4;       // clusters per lane of the wave
+constexpr uint16_t kClusterNone = 0xFFFF;
+struct alignas(16) DevCluster {
+    float lo[3], hi[3];
+    int32_t first, count;
+};
+static_assert(sizeof(DevCluster) == 32, "cluster is 32 B");
+
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -159,6 +176,9 @@ struct DevScene {
     const DevLightGrid* lgrid;       // per light (null: no grids)
     const uint32_t* lg_off;
     const DevLgEntry* lg_ent;
+    const DevCluster* clusters;      // wave-cooperative nearest query (null: not built)
+    const uint16_t* cl_perm;         // [8][64 * cl_slots]
+    int32_t n_clusters, cl_slots;    // cl_slots = ceil(n_clusters / 64) <= kClusterSlotsMax, 0 = none
 };
 
 struct FrameParams {
@@ -274,6 +294,8 @@ struct WfBufs {
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
     int32_t tail_from;              // > 0: nearest-hit generations >= this of a src-9 tree: queues of
     uint32_t tail_max;              //   <= tail_max rays go to the quad kernel (src 17), the rest to src 9
+    uint32_t wave_max;              // src 9, generations >= 1: queues of <= wave_max rays take the
+                                    //   wave-cooperative query (one ray per wave at a time, nearest_wave)
     uint32_t eager;                 // 1: each generation folds the pixels whose chain ended in it
                                     //   (wf_fold_gen on the B streams), no frame-end fold
     uint64_t o_dn, o_rd;            // eager: chain ends found by wf_nearest, their region sizes
@@ -317,6 +339,7 @@ constexpr uint32_t kNlevRunning = 0xFFu;   // WfBufs::nlev of a chain that has n
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
 constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G
+constexpr int kMaxScan = 4096;        // region sizes one region_scan covers (several generations' regions)
 constexpr int kMaxGenerations = 34;   // RT_MAX_DEPTH_LIMIT + 2 generations, + 1 spare for the last producer
 constexpr int kCntQ = 0;              // gen_totals layout: [kCntQ + k] queue sizes, [kCntS + k] shade records
 constexpr int kCntS = 64;

@@ -402,6 +402,64 @@ std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2) {
     return out;
 }
 
+ClusterResult build_clusters(const BvhResult& b2, size_t n_spheres) {
+    ClusterResult out;
+    if (n_spheres == 0) return out;
+    // (first, count) of every subtree: the builder partitions in place, so a
+    // subtree's spheres are one contiguous range of the leaf order
+    auto range = [&](int32_t ptr, auto&& self) -> std::pair<int32_t, int32_t> {
+        if (ptr < 0) return {(~ptr) >> 3, ((~ptr) & 7) + 1};
+        const auto a = self(b2.nodes[ptr].c0, self), b = self(b2.nodes[ptr].c1, self);
+        return {std::min(a.first, b.first), a.second + b.second};
+    };
+    auto cut = [&](int32_t ptr, const float lo[3], const float hi[3], auto&& self) -> void {
+        const auto r = range(ptr, range);
+        if (ptr < 0 || r.second <= kClusterMax) {
+            DevCluster c{};
+            for (int k = 0; k < 3; ++k) { c.lo[k] = lo[k]; c.hi[k] = hi[k]; }
+            c.first = r.first;
+            c.count = r.second;
+            out.clusters.push_back(c);
+            return;
+        }
+        const DevBvhNode& nd = b2.nodes[ptr];
+        self(nd.c0, nd.lo0, nd.hi0, self);
+        self(nd.c1, nd.lo1, nd.hi1, self);
+    };
+    const float inf = std::numeric_limits<float>::infinity();
+    const float all_lo[3] = {-inf, -inf, -inf}, all_hi[3] = {inf, inf, inf};
+    if (b2.root < 0) {                                   // the whole set is one leaf: one cluster, any ray tests it
+        cut(b2.root, all_lo, all_hi, cut);
+    } else {
+        const DevBvhNode& r = b2.nodes[b2.root];
+        cut(r.c0, r.lo0, r.hi0, cut);
+        cut(r.c1, r.lo1, r.hi1, cut);
+    }
+    const size_t n = out.clusters.size();
+    if (n > static_cast<size_t>(64 * kClusterSlotsMax) || n >= kClusterNone) { out.clusters.clear(); return out; }
+    out.slots = static_cast<int>((n + 63) / 64);
+    const size_t ns = static_cast<size_t>(64) * out.slots;
+    out.perm.assign(8 * ns, kClusterNone);
+    std::vector<uint16_t> ids(n);
+    for (int o = 0; o < 8; ++o) {
+        // octant o: bit a set = the ray's direction component a is negative; clusters
+        // sorted by centre . s (s_a = +1 / -1), so the ones a ray meets first come first
+        const double sx = (o & 1) ? -1.0 : 1.0, sy = (o & 2) ? -1.0 : 1.0, sz = (o & 4) ? -1.0 : 1.0;
+        auto key = [&](uint16_t i) {
+            const DevCluster& c = out.clusters[i];
+            const double cx = 0.5 * (static_cast<double>(c.lo[0]) + c.hi[0]);
+            const double cy = 0.5 * (static_cast<double>(c.lo[1]) + c.hi[1]);
+            const double cz = 0.5 * (static_cast<double>(c.lo[2]) + c.hi[2]);
+            const double k = sx * cx + sy * cy + sz * cz;
+            return std::isfinite(k) ? k : -HUGE_VAL;
+        };
+        for (size_t i = 0; i < n; ++i) ids[i] = static_cast<uint16_t>(i);
+        std::stable_sort(ids.begin(), ids.end(), [&](uint16_t a, uint16_t b) { return key(a) < key(b); });
+        for (size_t i = 0; i < n; ++i) out.perm[o * ns + i] = ids[i];
+    }
+    return out;
+}
+
 int bvh_depth(const BvhResult& b2) {
     if (b2.root < 0 || b2.nodes.empty()) return 0;
     int worst = 0;

@@ -85,6 +85,9 @@ struct WfStreams {
                           //   fold: gen_done[K-1] = generation K-1's shading done
     int fold_split;       // > 0: chains that ended by generation K = fold_split are folded on
                           //   generation K's b stream (with two b streams), the rest at the end
+    int bmerge;           // > 0: generations >= bmerge get no shadow / shading launches of their own;
+                          //   one occlusion + one shading launch over all their records follow the
+                          //   last nearest-hit launch on stream a (the latency-bound tail)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -34,7 +34,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -82,6 +82,10 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // 0: one fold over every chain after the last generation
     {"fold_split", 0, 0, 32},                    // K > 0: chains that ended by generation K fold on a B stream
                                                  // during the later generations, the rest after the last one
+    {"bmerge", 0, -1, 32},                       // T > 0: generations >= T shade in one occlusion + one shading
+                                                 // launch after the last nearest-hit launch; 0 off, -1 auto
+    {"wave_max", -1, -1, INT32_MAX},             // src 9, generations >= 1: queues of <= this many rays take the
+                                                 // wave-cooperative query (nearest_wave); 0 off, -1 auto
 };
 
 }  // namespace
@@ -206,6 +210,8 @@ struct rt_ctx {
     bool short_stack = false;        // binary tree fits the compact nearest-hit stack (16-bit codes, depth <= 32)
     bool short_stack18 = false;      // ... with 18-bit codes (the binary16 prefix source, src 6)
     bool all_lights_gridded = false; // every light is a point light with a light-view grid
+    int32_t cl_slots = 0;            // the uploaded scene's cluster slots (DevScene::cl_slots: 0 per render
+                                     // when the clusters would not fit the nearest-hit kernel's LDS budget)
     unsigned long long* d_counters = nullptr;
     double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
     void* d_path = nullptr;           // path kernel recursion stack (PathStack)
@@ -671,6 +677,7 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 32768 && spheres.size() <= 4096;
     c->short_stack18 = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 131072 && spheres.size() <= 16383;
     const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
+    const ClusterResult cls = build_clusters(bvh, spheres.size());
     // binary16 nodes only for trees that do not fit LDS whole (the prefix source reads them)
     const bool big_tree = bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget;
     const std::vector<DevBvhNodeH> hnodes = big_tree ? half_nodes(bvh) : std::vector<DevBvhNodeH>{};
@@ -704,6 +711,8 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_lg = place(lg.grids.size() * sizeof(DevLightGrid));
     const size_t o_lgoff = place(lg.off.size() * sizeof(uint32_t));
     const size_t o_lgent = place(lg.ent.size() * sizeof(DevLgEntry));
+    const size_t o_cl = place(cls.clusters.size() * sizeof(DevCluster));
+    const size_t o_clp = place(cls.perm.size() * sizeof(uint16_t));
     size_t tex_bytes = 0;
     uint64_t face_off[6] = {0, 0, 0, 0, 0, 0};
     if (skybox)
@@ -726,6 +735,8 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_lg, lg.grids.data(), lg.grids.size() * sizeof(DevLightGrid));
     put(o_lgoff, lg.off.data(), lg.off.size() * sizeof(uint32_t));
     put(o_lgent, lg.ent.data(), lg.ent.size() * sizeof(DevLgEntry));
+    put(o_cl, cls.clusters.data(), cls.clusters.size() * sizeof(DevCluster));
+    put(o_clp, cls.perm.data(), cls.perm.size() * sizeof(uint16_t));
     if (skybox)
         for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
     // every render still reading the old blob (on any stream) must be done before it is overwritten
@@ -782,6 +793,11 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.lgrid = lg.grids.empty() ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_lg);
     d.lg_off = reinterpret_cast<const uint32_t*>(base + o_lgoff);
     d.lg_ent = reinterpret_cast<const DevLgEntry*>(base + o_lgent);
+    d.clusters = cls.clusters.empty() ? nullptr : reinterpret_cast<const DevCluster*>(base + o_cl);
+    d.cl_perm = reinterpret_cast<const uint16_t*>(base + o_clp);
+    d.n_clusters = static_cast<int32_t>(cls.clusters.size());
+    d.cl_slots = cls.clusters.empty() ? 0 : cls.slots;
+    c->cl_slots = d.cl_slots;
     c->all_lights_gridded = !lights.empty() && lg.grids.size() == lights.size();
     for (const DevLightGrid& g : lg.grids) c->all_lights_gridded = c->all_lights_gridded && g.R > 0;
     c->scene_spp = s->antialias;
@@ -1031,9 +1047,24 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // generations 5 and 6 still hold more rays than that, measured 2% slower)
         if (tail_from < 0) tail_from = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8) <= 32ull * tail_max ? 5 : 0;
         if (src != 9 || !c->quad_ok) tail_from = 0;
+        // the wave-cooperative query for the late generations' small queues (src 9 with
+        // clusters whose LDS copy keeps the nearest-hit kernel at two workgroups per CU)
+        c->dsc.cl_slots = c->cl_slots;
+        {
+            const size_t cl_bytes = static_cast<size_t>(c->dsc.n_clusters) * sizeof(DevCluster) +
+                                    static_cast<size_t>(8) * 64 * c->cl_slots * sizeof(uint16_t);
+            // (axis-pair nodes 56 B each, spheres + ids, clusters, region scan and counters of G regions)
+            const size_t total = (node_bytes / sizeof(DevBvhNode) * 56 + 15) / 16 * 16 + (sph_bytes + 15) / 16 * 16 +
+                                 (cl_bytes + 15) / 16 * 16 + (static_cast<size_t>(G) + 64) * 4;
+            if (total > 80 * 1024) c->dsc.cl_slots = 0;
+        }
+        const int64_t wave_t = c->t(kTuneWaveMax);
+        const uint32_t wave_max = src != 9 || c->dsc.cl_slots == 0 ? 0u
+                                  : wave_t >= 0 ? static_cast<uint32_t>(wave_t) : 32768u;
         for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tail_from = tail_from;
             c->lanes[l].b.tail_max = tail_max;
+            c->lanes[l].b.wave_max = wave_max;
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
@@ -1091,6 +1122,18 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             ws.near_done = L.near_done.data();
             ws.gen_done = L.gen_done.data();
             ws.fold_split = static_cast<int>(c->t(kTuneFoldSplit));
+            // merged tail (tuning bmerge): only with the grid-only shadow kernel, unfused shading and the
+            // frame-end fold, and when one region scan covers the merged generations' regions
+            {
+                int T = static_cast<int>(c->t(kTuneBMerge));
+                if (T < 0) T = 0;                                  // auto: off until measured
+                const bool ok = T >= 1 && static_cast<uint32_t>(T) <= o->max_depth && split && !fuse && nlists == 0 &&
+                                !b.eager && c->all_lights_gridded && c->t(kTuneGridOcc) != 0 &&
+                                c->t(kTuneFuseFrom) > static_cast<int64_t>(o->max_depth) &&
+                                static_cast<uint64_t>(o->max_depth + 1 - T) * G <= static_cast<uint64_t>(kMaxScan) &&
+                                c->t(kTuneFoldSplit) == 0;
+                ws.bmerge = ok ? T : 0;
+            }
             ws.ma = timed ? &marks : nullptr;
             ws.fuse = fuse;
             ws.cam = cam;

@@ -339,6 +339,8 @@ struct BvhView {
     const DevCamNode* cng;       // camera nodes [ncl, n) are read here, [0, ncl) from cn (LDS)
     int32_t ncl;
     uint32_t* lstk;              // quad source: this ray's LDS stack (entry i at lstk[i * kQuadStride])
+    const DevCluster* cl;        // wave-cooperative query: the clusters and their octant orders (LDS)
+    const uint16_t* clp;
 };
 
 // LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
@@ -973,6 +975,142 @@ __device__ __forceinline__ Hit nearest_quad(const DevScene& sc, const BvhView& v
         }
         if (cur == kNone) return h;
     }
+}
+
+// ---- wave-cooperative nearest query ------------------------------------------
+// For the small queues of the late generations, whose launches last as long as
+// their slowest walk: ONE ray (wave-uniform) per wave at a time, every lane
+// working on it.  Lane l tests the boxes of the clusters in slots j*64 + l of
+// the ray's octant order (DevCluster: subtrees of <= 16 spheres, one contiguous
+// sphere range each); then, batch by batch, the next four clusters whose box
+// the ray enters no later than the current t limit are dealt over the four
+// 16-lane rows, lane i of a row testing sphere first + i with the exact f64
+// quadratic.  After each batch the wave's best t tightens the limit, and
+// clusters whose box starts beyond it are dropped (the culling argument of the
+// BVH walk).  The result is the (t, object id)
+// minimum over every sphere tested, the same lexicographic minimum the linear
+// scan finds (scene.rs:247-249).  Every lane must call it with the same ray
+// and no lane masked off (the cross-lane moves read every lane).
+template <int kCtrl>
+__device__ __forceinline__ int32_t dpp_i32(int32_t x) { return __builtin_amdgcn_mov_dpp(x, kCtrl, 0xF, 0xF, false); }
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+__device__ __forceinline__ float rl_f32(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+__device__ __forceinline__ double rl_f64(double x, int l) {
+    const int64_t u = __double_as_longlong(x);
+    const int32_t lo = __builtin_amdgcn_readlane(static_cast<int32_t>(u), l);
+    const int32_t hi = __builtin_amdgcn_readlane(static_cast<int32_t>(u >> 32), l);
+    return __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
+}
+__device__ __forceinline__ Ray rl_ray(const Ray& r, int l) {
+    return Ray{rl_f64(r.ox, l), rl_f64(r.oy, l), rl_f64(r.oz, l), rl_f64(r.dx, l), rl_f64(r.dy, l), rl_f64(r.dz, l)};
+}
+
+// min over the wave's 64 lanes (each 16-lane row by DPP, then the four rows)
+__device__ __forceinline__ float wave_min_f32(float x) {
+    x = fminf(x, __int_as_float(dpp_i32<kDppXor1>(__float_as_int(x))));
+    x = fminf(x, __int_as_float(dpp_i32<kDppXor2>(__float_as_int(x))));
+    x = fminf(x, __int_as_float(dpp_i32<kDppHalfMirror>(__float_as_int(x))));
+    x = fminf(x, __int_as_float(dpp_i32<kDppMirror>(__float_as_int(x))));
+    return fminf(fminf(rl_f32(x, 0), rl_f32(x, 16)), fminf(rl_f32(x, 32), rl_f32(x, 48)));
+}
+
+struct WaveBest {
+    double t;
+    int32_t obj, prim;
+};
+__device__ __forceinline__ bool wb_better(double t, int32_t o, const WaveBest& b) { return t < b.t || (t == b.t && o < b.obj); }
+template <int kCtrl>
+__device__ __forceinline__ void wb_step(WaveBest& b) {
+    const int64_t u = __double_as_longlong(b.t);
+    const int32_t lo = dpp_i32<kCtrl>(static_cast<int32_t>(u)), hi = dpp_i32<kCtrl>(static_cast<int32_t>(u >> 32));
+    const double ot = __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
+    const int32_t oo = dpp_i32<kCtrl>(b.obj), op = dpp_i32<kCtrl>(b.prim);
+    if (wb_better(ot, oo, b)) { b.t = ot; b.obj = oo; b.prim = op; }
+}
+// the lexicographic (t, object) minimum over the wave (wave-uniform result)
+__device__ __forceinline__ WaveBest wave_best(WaveBest b) {
+    wb_step<kDppXor1>(b);
+    wb_step<kDppXor2>(b);
+    wb_step<kDppHalfMirror>(b);
+    wb_step<kDppMirror>(b);
+    WaveBest r{rl_f64(b.t, 0), __builtin_amdgcn_readlane(b.obj, 0), __builtin_amdgcn_readlane(b.prim, 0)};
+#pragma unroll
+    for (int row = 1; row < 4; ++row) {
+        const double t = rl_f64(b.t, 16 * row);
+        const int32_t o = __builtin_amdgcn_readlane(b.obj, 16 * row), p = __builtin_amdgcn_readlane(b.prim, 16 * row);
+        if (wb_better(t, o, r)) { r.t = t; r.obj = o; r.prim = p; }
+    }
+    return r;
+}
+
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_wave(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const RayBox rb = make_raybox(r);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    const int lane = static_cast<int>(threadIdx.x & 63u);
+    const int oct = (rb.ix < 0.0f ? 1 : 0) | (rb.iy < 0.0f ? 2 : 0) | (rb.iz < 0.0f ? 4 : 0);
+    const int S = sc.cl_slots, NS = 64 * S;
+    // per slot: the cluster's entry t (NaN: missed, never <= tlim) and (first << 5 | count)
+    float te[kClusterSlotsMax];
+    int32_t pk[kClusterSlotsMax];
+    uint64_t m[kClusterSlotsMax];
+#pragma unroll
+    for (int j = 0; j < kClusterSlotsMax; ++j) {
+        te[j] = __builtin_nanf("");
+        pk[j] = 0;
+        m[j] = 0;
+        if (j < S) {
+            const uint16_t cid = v.clp[oct * NS + j * 64 + lane];
+            if (cid != kClusterNone) {
+                const DevCluster c = v.cl[cid];
+                float tn;
+                if constexpr (kCount) w->boxes += 1;
+                if (box_hit(c.lo, c.hi, rb, tlim, tn)) { te[j] = fmaxf(tn, 0.0f); pk[j] = (c.first << 5) | c.count; }
+            }
+            m[j] = __ballot(te[j] <= tlim);
+        }
+    }
+    WaveBest best{__builtin_huge_val(), INT32_MAX, 0};
+    const int q = lane >> 4, i = lane & 15;
+    for (;;) {
+        // the next four clusters in slot order (wave-uniform, scalar)
+        int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        int got = 0;
+#pragma unroll
+        for (int j = 0; j < kClusterSlotsMax; ++j) {
+            while (m[j] != 0 && got < 4) {
+                const int l = __builtin_ctzll(m[j]);
+                m[j] &= m[j] - 1;
+                const int32_t val = __builtin_amdgcn_readlane(pk[j], l);
+                if (got == 0) s0 = val; else if (got == 1) s1 = val; else if (got == 2) s2 = val; else s3 = val;
+                ++got;
+            }
+        }
+        if (got == 0) break;
+        const int32_t mine = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
+        if (q < got && i < (mine & 31)) {
+            const int k = (mine >> 5) + i;
+            if constexpr (kCount) ++w->spheres;
+            double t;
+            if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                const int32_t obj = v.obj[k];
+                if (wb_better(t, obj, best)) { best.t = t; best.obj = obj; best.prim = k; }
+            }
+        }
+        // the wave's best t so far bounds every cluster still worth testing
+        tlim = fminf(tlim, wave_min_f32(best.obj != INT32_MAX ? t_limit(best.t) : __builtin_inff()));
+#pragma unroll
+        for (int j = 0; j < kClusterSlotsMax; ++j)
+            if (j < S) m[j] &= __ballot(te[j] <= tlim);
+    }
+    const WaveBest wb = wave_best(best);
+    if (wb.obj != INT32_MAX && (wb.t < h.t || (wb.t == h.t && wb.obj < h.obj))) { h.t = wb.t; h.obj = wb.obj; h.prim = wb.prim; }
+    return h;
 }
 
 // `hint`: a sphere (leaf-order index, or -1) tested before the traversal: the

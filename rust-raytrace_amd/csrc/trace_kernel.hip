@@ -206,11 +206,13 @@ __device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n, uint32_
         if (const uint32_t j = rt_c * 64u + (threadIdx.x & 63u); true)
 
 // Exclusive scan of the G region sizes `counts` into s_scan[0..G]
-// (s_scan[G] = queue size).  s_wave: 16 words.  Ends with a barrier.
+// (s_scan[G] = queue size; G <= kMaxScan: the regions of up to kMaxScan / G
+// consecutive generations, laid out one after the other).  s_wave: 16 words.
+// Ends with a barrier.
 __device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan, uint32_t* s_wave) {
-    const uint32_t per = (G + kWfThreads - 1) / kWfThreads;       // 1 or 2
+    const uint32_t per = (G + kWfThreads - 1) / kWfThreads;       // 1 .. 4
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint32_t v[2] = {0, 0}, sum = 0;
+    uint32_t v[4] = {0, 0, 0, 0}, sum = 0;
     for (uint32_t e = 0; e < per; ++e) {
         const uint32_t i = t * per + e;
         v[e] = i < G ? counts[i] : 0u;
@@ -395,6 +397,11 @@ __host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
     return 0;
 }
 
+__host__ __device__ inline size_t cluster_lds_bytes(const DevScene& sc) {
+    return (static_cast<size_t>(sc.n_clusters) * sizeof(DevCluster) + static_cast<size_t>(8) * 64 * sc.cl_slots * sizeof(uint16_t) +
+            15) / 16 * 16;
+}
+
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
@@ -413,13 +420,16 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     bytes = (bytes + 15) / 16 * 16;
     if (Src<kSrc>::quad) bytes += static_cast<size_t>(kQuadStack) * kQuadStride * sizeof(uint32_t);
+    if (kSrc == kSrcBvhL8C && sc.cl_slots > 0)           // the wave-cooperative query's clusters and orders
+        bytes += cluster_lds_bytes(sc);
     return bytes;
 }
 
 // Stage what the source keeps in LDS (the whole tree and the spheres); returns
-// the view the queries use.
+// the view the queries use.  wave: a src-9 launch that runs the wave-cooperative
+// query (nearest_wave) stages the spheres and the clusters, not the tree.
 template <int kSrc>
-__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
+__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds, bool wave = false) {
     constexpr int T = kWfThreads;
     BvhView v{nullptr, 0, nullptr, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
     size_t off = 0;
@@ -469,7 +479,8 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.p4 = lp;
         off = static_cast<size_t>(n) * sizeof(DevBvh4Plane);
     } else if constexpr (Src<kSrc>::nodes > 0) {
-        v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
+        if (!wave) v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
+        else v.lnodes = reinterpret_cast<const float2*>(lds);
         v.nl = sc.n_bvh;
         off = node_planes_bytes(sc.n_bvh);
     }
@@ -482,6 +493,18 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         if constexpr (Src<kSrc>::quad) {                 // the rays' stacks after the spheres
             const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
             v.lstk = reinterpret_cast<uint32_t*>(lds + at) + (threadIdx.x >> 2);
+        }
+        if constexpr (kSrc == kSrcBvhL8C) {              // the clusters after the spheres (wave-cooperative query)
+            if (wave && sc.cl_slots > 0) {
+                const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
+                DevCluster* lc = reinterpret_cast<DevCluster*>(lds + at);
+                for (int i = threadIdx.x; i < sc.n_clusters; i += T) lc[i] = sc.clusters[i];
+                uint16_t* lp = reinterpret_cast<uint16_t*>(lc + sc.n_clusters);
+                const int np = 8 * 64 * sc.cl_slots;
+                for (int i = threadIdx.x; i < np; i += T) lp[i] = sc.cl_perm[i];
+                v.cl = lc;
+                v.clp = lp;
+            }
         }
     }
     return v;
@@ -741,10 +764,18 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     // quad walk: 16 rays per wave; chunks of 16 rays when every wave takes at most one
     // (a workgroup then appends <= 256 entries), else 64-ray chunks in four passes
     constexpr bool kQuad = Src<kSrc>::quad;
-    // tail generations: the quad kernel takes queues of <= tail_max rays, the
-    // regular one the rest (both are launched; the other returns at once)
-    if (!kCam && b.tail_from > 0 && k >= b.tail_from && (n <= b.tail_max) != kQuad) return;
-    const uint32_t width = kQuad && n <= b.G * (kWfThreads / 4) ? 16u : 64u;
+    // queues of <= wave_max rays (generations >= 1 of a src-9 tree with clusters): the
+    // regular kernel runs the wave-cooperative query, `width` rays per wave one after another,
+    // width = ceil(n / waves) so that every wave takes at most one chunk
+    const bool wv = kSrc == kSrcBvhL8C && !kCam && k >= 1 && b.wave_max > 0 && n <= b.wave_max;
+    // tail generations: the quad kernel takes queues of <= tail_max rays (and above wave_max
+    // when the wave query is on), the regular one the rest (both are launched; the other
+    // returns at once)
+    if (!kCam && b.tail_from > 0 && k >= b.tail_from &&
+        (n <= b.tail_max && !(b.wave_max > 0 && n <= b.wave_max)) != kQuad)
+        return;
+    const uint32_t wwidth = max(1u, min(64u, (n + b.G * (kWfThreads / 64) - 1) / (b.G * (kWfThreads / 64))));
+    const uint32_t width = kQuad && n <= b.G * (kWfThreads / 4) ? 16u : wv ? wwidth : 64u;
     if (!wg_has_work(b, n, width)) {           // nothing dealt here: publish empty regions, free the CU
         if (threadIdx.x == 0) {
             b.rs()[k * b.G + blockIdx.x] = 0;
@@ -754,7 +785,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = 0;
         return;
     }
-    const BvhView v = stage_lds<kSrc>(sc, lds);
+    const BvhView v = stage_lds<kSrc>(sc, lds, wv);
     __syncthreads();                                       // publishes the LDS staging and counters
     RT_STAMP_AT(st1);
     acc[0] = st1 - st0;
@@ -764,7 +795,8 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     for (uint32_t rt_c = wave_slot(b, n), rt_w = b.G * (kWfThreads / 64); static_cast<uint64_t>(rt_c) * width < n;
          rt_c += rt_w)
     for (uint32_t sub = 0; sub < (kQuad ? width / 16u : 1u); ++sub) {
-        const uint32_t j = kQuad ? rt_c * width + sub * 16u + ((threadIdx.x & 63u) >> 2) : rt_c * 64u + (threadIdx.x & 63u);
+        const uint32_t j = kQuad ? rt_c * width + sub * 16u + ((threadIdx.x & 63u) >> 2)
+                                 : ((threadIdx.x & 63u) < width ? rt_c * width + (threadIdx.x & 63u) : 0xFFFFFFFFu);
         RT_STAMP_AT(st0);
         [[maybe_unused]] const uint32_t visits0 = w.boxes;
         Ray r{};
@@ -795,7 +827,17 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             tile_rect(fp, b, j >> 6, tx0, ty0, tx1, ty1);
             h = nearest_camera<kCount>(sc, v, r, live, tx0, ty0, tx1, ty1, &w);
         }
-        if (live) {
+        if constexpr (kSrc == kSrcBvhL8C) {
+            if (wv) {                                    // workgroup-uniform: every lane on one ray at a time
+                for (uint32_t i = 0; i < width; ++i) {
+                    if (!__builtin_amdgcn_readlane(live ? 1 : 0, static_cast<int>(i))) continue;
+                    const Hit hi = nearest_wave<kCount>(sc, v, rl_ray(r, static_cast<int>(i)), &w);
+                    if ((threadIdx.x & 63u) == i) h = hi;
+                }
+            } else if (live) {
+                h = nearest_any<kSrc, kCount>(sc, v, r, &w);
+            }
+        } else if (live) {
             if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         }
         RT_STAMP_AT(st2);
@@ -903,13 +945,18 @@ __device__ __forceinline__ void occlusion_done(const DevScene& sc, const WfBufs&
 // one work-item per (record, light) pair -- the lights of one hit are
 // independent queries -- setting bit l of the record's occlusion mask
 // (kShade: and shading the record once its last light is done).
+// ngen > 1 (the merged tail, WfStreams::bmerge): the records of generations
+// k .. k + ngen - 1 as one item list (their region sizes are consecutive in rs,
+// and record entry = generation * qcap + region * R + offset either way).
 template <int kSrc, bool kCount, bool kShade, bool kFresnel>
-__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k,
+                                                                            int ngen) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
-    region_scan(b.rs() + k * b.G, b.G, ql.scan, ql.wave);
+    const uint32_t M = b.G * static_cast<uint32_t>(ngen);
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), M);
+    region_scan(b.rs() + k * b.G, M, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-    const uint32_t nrec = ql.scan[b.G], n = nrec * L;
+    const uint32_t nrec = ql.scan[M], n = nrec * L;
     if (!wg_has_work(b, n)) return;
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();
@@ -919,7 +966,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
     RT_FOR_CHUNKS(b, n, qi) {
         if (qi >= n) continue;
         const uint32_t l = qi / nrec, j = qi - l * nrec;
-        const size_t at = rk + region_entry(ql.scan, b.G, b.R, j);
+        const size_t at = rk + region_entry(ql.scan, M, b.R, j);
         const double ptx = ldn_if<3>(&b.rf(0)[at]), pty = ldn_if<3>(&b.rf(1)[at]), ptz = ldn_if<3>(&b.rf(2)[at]);
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
@@ -933,7 +980,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
             occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
                            ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
                            : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
-        occlusion_done<kShade, kFresnel>(sc, b, k, at, l, L, occluded);
+        occlusion_done<kShade, kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, l, L, occluded);
     }
     flush_work<kCount>(b, 4, w);
 }
@@ -993,17 +1040,19 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_shadow(DevSce
 
 // The Phong sum of every shade record of generation k (scenes without lights,
 // or with more lights than the fused kernel's count field holds).
+// (ngen > 1: generations k .. k + ngen - 1 as one list, as in wf_occlusion.)
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    __shared__ uint32_t s_scan[kMaxRegions + 1];
+__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k, int ngen) {
+    __shared__ uint32_t s_scan[kMaxScan + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
-    region_scan(b.rs() + k * b.G, b.G, s_scan, s_wave);
-    const uint32_t n = s_scan[b.G];
+    const uint32_t M = b.G * static_cast<uint32_t>(ngen);
+    region_scan(b.rs() + k * b.G, M, s_scan, s_wave);
+    const uint32_t n = s_scan[M];
     const size_t rk = static_cast<size_t>(k) * b.qcap;
     RT_FOR_CHUNKS(b, n, j) {
         if (j >= n) continue;
-        const size_t at = rk + region_entry(s_scan, b.G, b.R, j);
-        shade_record<kFresnel>(sc, b, k, at, sc.n_lights > 0 ? b.ru(3)[at] : 0u);
+        const size_t at = rk + region_entry(s_scan, M, b.R, j);
+        shade_record<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, sc.n_lights > 0 ? b.ru(3)[at] : 0u);
     }
 }
 
@@ -1181,7 +1230,7 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 
 template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
-                          hipStream_t sb, LaunchMarks* mb, bool lists);
+                          hipStream_t sb, LaunchMarks* mb, bool lists, int ngen = 1);
 
 // The split fold applies with B streams of their own (at most two: the fold of
 // generation K waits for K's stream and, through gen_done[K-1], for the other
@@ -1189,6 +1238,13 @@ hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBuf
 // carry all of them) and 1 <= K <= max_depth.
 inline bool split_fold(const WfStreams& ws, const FrameParams& fp) {
     return ws.fold_split >= 1 && static_cast<uint32_t>(ws.fold_split) <= fp.max_depth && ws.b[0] != ws.a && ws.nb <= 2;
+}
+
+template <int kSrcO, bool kCount>
+hipError_t launch_merged_tail(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const WfStreams& ws) {
+    const int k0 = ws.bmerge, ngen = static_cast<int>(fp.max_depth) + 1 - ws.bmerge;
+    if (ngen <= 0) return hipSuccess;
+    return launch_shading<kSrcO, kCount>(sc, fp, b, k0, ws, ws.a, ws.ma, false, ngen);
 }
 
 template <int kSrcN, int kSrcO, bool kCount>
@@ -1238,6 +1294,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (e != hipSuccess) return e;
     const bool shaded = static_cast<uint32_t>(k) <= fp.max_depth;     // no shade records past the cut-off
     if (!shaded && !b.eager) return hipSuccess;
+    // the merged tail: generations >= bmerge are shaded together after the last nearest-hit launch
+    if (ws.bmerge > 0 && k >= ws.bmerge) return hipSuccess;
     // shadows and shading of generation k: on a b stream once nearest_k is done
     // (generations alternate over the b streams, so consecutive ones overlap too)
     const int bi = k % ws.nb;
@@ -1271,7 +1329,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
 // nearest-hit launch).
 template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
-                          hipStream_t sb, LaunchMarks* mb, bool lists) {
+                          hipStream_t sb, LaunchMarks* mb, bool lists, int ngen) {
     const dim3 grid(b.G), block(kWfThreads);
     hipError_t e;
     if (lists) {                                 // shadow lists (planes and own sphere decided upstream)
@@ -1286,7 +1344,7 @@ hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBuf
         const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
         if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
 #define RT_OCC(S, SH, FR) hipLaunchKernelGGL((wf_occlusion<S, kCount, SH, FR>), grid, block, \
-                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), sb, sc, fp, b, k)
+                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G * ngen), sb, sc, fp, b, k, ngen)
         if (!fused && ws.grid_occ == 1) RT_OCC(kSrcGridL, false, false);
         else if (!fused && ws.grid_occ == 2) RT_OCC(kSrcGridG, false, false);
         else if (!fused) RT_OCC(kSrcO, false, false);
@@ -1300,8 +1358,8 @@ hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBuf
     }
     if (fused) return hipSuccess;
     if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, sb, sc, fp, b, k);
-    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, sb, sc, fp, b, k);
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, sb, sc, fp, b, k, ngen);
+    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, sb, sc, fp, b, k, ngen);
     return mb ? mb->mark(sb, kKfShade) : hipSuccess;
 }
 
@@ -1349,6 +1407,15 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         }
     }
     hipError_t e;
+    // the merged tail's shadows and shading (generations >= bmerge), on stream a after the last
+    // nearest-hit launch: one occlusion and one shading launch instead of two per generation
+    if (ws.bmerge > 0) {
+        const int combo = src * 100 + src_occ;
+        e = combo == kSrcBvhL8C * 100 + kSrcBvh4L
+                ? (count ? launch_merged_tail<kSrcBvh4L, true>(sc, fp, b, ws) : launch_merged_tail<kSrcBvh4L, false>(sc, fp, b, ws))
+                : (count ? launch_merged_tail<kSrcBvh4G, true>(sc, fp, b, ws) : launch_merged_tail<kSrcBvh4G, false>(sc, fp, b, ws));
+        if (e != hipSuccess) return e;
+    }
     // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
     if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);

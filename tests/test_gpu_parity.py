@@ -261,6 +261,22 @@ def test_render_without_scene_and_bad_opts():
 
 # ---- BVH culling must be conservative: adversarial scenes ------------------
 
+def _nan_plane_scene():
+    """test_nan_plane_wins's camera-in-a-plane scene (NaN plane hits) with 60
+    more spheres, so that the wave query has several clusters to cull."""
+    s = _tiny(width=17, height=13)
+    s.max_depth = 5
+    s.sphere((0, 0, -5), 1.0, scenes.phong((0.5, 0.5, 0.5), (0.3, 0.3, 0.3), 8.0, (0, 1, 0)))
+    rng = scenes.SplitMix64(21)
+    for k in range(60):
+        c = (rng.uniform(-4, 4), rng.uniform(-3, 3), rng.uniform(-12, -3))
+        s.sphere(c, rng.uniform(0.1, 0.8), scenes.phong((0.4, 0.5, 0.6), (0.5, 0.5, 0.5), 20.0, (0, 0, 0)))
+    s.plane((0, 0, 0), (0, 1, 0), scenes.phong((0.1, 0.2, 0.3), (0.2, 0.2, 0.2), 4.0, (0, 0, 1)))
+    s.point_light((3, 3, 3), (1, 1, 1))
+    s.directional_light((0, -1, 0.2), (0.5, 0.5, 0.5))
+    return s
+
+
 def _axis_tie_scene():
     s = scenes.SceneSpec(width=33, height=31, max_depth=6, background=(0.1, 0.1, 0.2),
                          camera={"ctor": "new", "position": (0, 0, 0), "look": (0, 0, -1), "up": (0, 1, 0),
@@ -299,6 +315,32 @@ def test_quad_tail_walk_matches_oracle(gpu_ctx, scene):
          "config3": lambda: scenes.config3(160, 128)}[scene]()
     with _with_tuning(gpu_ctx, tail_from=1, tail_max=1 << 30):
         check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+
+
+@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "extreme", "planes_nan"])
+def test_wave_cooperative_query_matches_oracle(gpu_ctx, scene):
+    """The wave-cooperative query (one ray per wave, clusters of <= 16 spheres
+    tested batch by batch, trace_common.hpp nearest_wave) forced onto every
+    generation from 1 on (wave_max huge): ties across clusters, axis-aligned
+    rays, a deep tree, spheres from 1e-4 to 1e4, NaN planes and a C3
+    workload all match the oracle bit for bit; with the quad walk on too, the
+    three queries share the generations by queue size."""
+    def extreme():
+        s = scenes.config2(57, 41)
+        s.max_depth = 8
+        rng = scenes.SplitMix64(9)
+        for k in range(150):
+            c = (rng.uniform(-30, 30), rng.uniform(0.001, 4), rng.uniform(-60, 0))
+            s.sphere(c, 10 ** rng.uniform(-4, 0.3), scenes.phong((0.3, 0.6, 0.9), (0.6, 0.6, 0.6), 50.0, (0, 0, 0)))
+        s.sphere((0.0, -1e4 + 0.0, -5.0), 1e4, scenes.phong((0.2, 0.2, 0.2), (0.5, 0.5, 0.5), 5.0, (0, 0, 0)))
+        return s
+    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene,
+         "config3": lambda: scenes.config3(160, 128), "extreme": extreme, "planes_nan": _nan_plane_scene}[scene]()
+    with _with_tuning(gpu_ctx, wave_max=1 << 30):
+        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+    if scene == "config3":
+        with _with_tuning(gpu_ctx, wave_max=300, tail_from=1, tail_max=3000):
+            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
 @pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
@@ -583,7 +625,9 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(tail_from=1, tail_max=1 << 30, regions=96), dict(eager_fold=1), dict(eager_fold=1, split=0),
                dict(eager_fold=1, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1),
                dict(fold_split=1), dict(fold_split=4), dict(fold_split=8), dict(fold_split=3, bstreams=1),
-               dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3)]:
+               dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3), dict(bmerge=1), dict(bmerge=3),
+               dict(bmerge=5, tail_from=1, tail_max=1 << 30), dict(bmerge=2, regions=2048), dict(wave_max=0),
+               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

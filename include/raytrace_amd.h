@@ -282,7 +282,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * during the later generations, the rest after the last one; with one or two
  * shading streams only, ignored with bstreams > 2), bmerge (T > 0: generations >= T
  * get no shadow / shading launches of their own; one occlusion and one shading
- * launch over all their records follow the last nearest-hit launch; -1 auto).
+ * launch over all their records follow the last nearest-hit launch; -1 auto),
+ * wave_max (trees that fit LDS: nearest-hit queues of generations >= 1 holding
+ * <= wave_max rays take the wave-cooperative query, one ray per wave over sphere
+ * clusters; 0 off, -1 auto).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

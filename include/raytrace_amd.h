@@ -147,6 +147,19 @@ int rt_scene_set_skybox(rt_scene* scene, const rt_texture faces[6]);
  * scene.rs:247-249); tests check the lists against that scan. */
 int rt_light_grid_candidates(const rt_scene* scene, int light, int resolution, const double* points, uint32_t n_points,
                              int32_t* counts, int32_t* ids, size_t cap, int64_t* info);
+/* Diagnostic, host only: the camera's view grid (built as
+ * rt_scene_upload builds it, spheres in file order) for camera-ray directions
+ * `dirs` (n_dirs x 3 doubles): for each direction the spheres the device may
+ * test -- the always list, then the direction's whole cell list in increasing
+ * distance bound (the device stops once a bound exceeds its best t) --
+ * counts[i] = its length, or -1 when the device tests every sphere; ids = object
+ * ids, nears = each entry's distance bound (f32), both concatenated, at most cap
+ * in all.  info[0..2] = cells per face side, stored cells, list entries.
+ * resolution: cells per face side (0: from the scene's frame size).  Replaces
+ * nothing in the reference (scene.rs:247-249 scans every object); tests check
+ * the lists against that scan. */
+int rt_view_grid_candidates(const rt_scene* scene, int resolution, const double* dirs, uint32_t n_dirs,
+                            int32_t* counts, int32_t* ids, float* nears, size_t cap, int64_t* info);
 /* Decode an image file as Texture::load does (RGB8, rows top-down).  rgb == NULL: only the size.
  * Formats: uncompressed BMP (24/32 bit) and binary PPM; others -> RT_E_UNSUPPORTED. */
 int rt_texture_load(const char* path, uint32_t* width, uint32_t* height, uint8_t* rgb, size_t cap);
@@ -285,7 +298,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * launch over all their records follow the last nearest-hit launch; -1 auto),
  * wave_max (trees that fit LDS: nearest-hit queues of generations >= 1 holding
  * <= wave_max rays take the wave-cooperative query, one ray per wave over sphere
- * clusters; 0 off, -1 auto).
+ * clusters; 0 off, -1 auto), cam (generation 0: 0 per ray, 1 / 2 camera tiles over the
+ * camera view of the tree in LDS / through L2, 3 the camera's view grid), cam_grid_res
+ * (the view grid's cells per face side, 0 from the scene's frame size, -1 none;
+ * at the next rt_scene_upload).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -76,6 +76,11 @@ struct LightGridResult {
 };
 LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
                                   const std::vector<DevLight>& lights, double pad, int r_override);
+// The camera's view grid (the same cube-map layout, one grid centred on `pos`)
+// for the camera rays' nearest-hit query; R halves until the lists hold at
+// most max_entries entries.
+LightGridResult build_view_grid(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
+                                const double pos[3], double pad, int R, size_t max_entries);
 // Host mirror of the device's candidate list (test / diagnostic).
 bool light_grid_candidates(const LightGridResult& lg, int light, const double p[3], std::vector<int32_t>& out);
 

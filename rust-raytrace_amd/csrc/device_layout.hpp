@@ -176,6 +176,9 @@ struct DevScene {
     const DevLightGrid* lgrid;       // per light (null: no grids)
     const uint32_t* lg_off;
     const DevLgEntry* lg_ent;
+    const DevLightGrid* cgrid;       // the camera's view grid (camera rays' nearest hit; null: none)
+    const uint32_t* cg_off;
+    const DevLgEntry* cg_ent;
     const DevCluster* clusters;      // wave-cooperative nearest query (null: not built)
     const uint16_t* cl_perm;         // [8][64 * cl_slots]
     int32_t n_clusters, cl_slots;    // cl_slots = ceil(n_clusters / 64) <= kClusterSlotsMax, 0 = none

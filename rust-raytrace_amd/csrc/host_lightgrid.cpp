@@ -161,6 +161,113 @@ LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const s
     return out;
 }
 
+// View grid of the camera: the same cube map, centred on the
+// camera position, for the camera rays' NEAREST-hit query.  Every camera ray
+// starts at the camera, so a hit point's direction from the camera is the ray
+// direction (up to f64 rounding) and it lies in the sphere's padded box: the
+// ray's cell lists every sphere that can report a hit.  Lists are sorted by
+// box distance from the camera (f32, rounded down), which bounds t from below,
+// so the device stops at the first entry beyond its current best t.  R cells
+// per face side; halved until the lists hold at most `max_entries` entries
+// (built by counting per cell, then filling, so large faces stay cheap).
+LightGridResult build_view_grid(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
+                                const double pos[3], double pad, int R, size_t max_entries) {
+    LightGridResult out;
+    out.grids.assign(1, DevLightGrid{});
+    DevLightGrid& g = out.grids[0];
+    g.R = 0;
+    const size_t n = spheres.size();
+    if (n == 0 || !std::isfinite(pos[0]) || !std::isfinite(pos[1]) || !std::isfinite(pos[2])) return out;
+    g.lx = pos[0]; g.ly = pos[1]; g.lz = pos[2];
+    std::vector<double> lo(3 * n), hi(3 * n), nearv(n);
+    std::vector<char> always(n, 0);
+    for (size_t k = 0; k < n; ++k) {
+        const double c[3] = {spheres[k].cx, spheres[k].cy, spheres[k].cz};
+        const double r = std::fabs(r_leaf[k]) + pad;
+        double d2 = 0.0;
+        bool finite = std::isfinite(r), at_cam = true;
+        for (int i = 0; i < 3; ++i) {
+            double a = c[i] - r - pos[i], b = c[i] + r - pos[i];
+            a -= 1e-12 * (1.0 + std::fabs(a));
+            b += 1e-12 * (1.0 + std::fabs(b));
+            lo[3 * k + i] = a; hi[3 * k + i] = b;
+            finite &= std::isfinite(a) && std::isfinite(b);
+            at_cam &= a - kNearLight <= 0.0 && 0.0 <= b + kNearLight;
+            const double gap = std::max({0.0, a, -b});
+            d2 += gap * gap;
+        }
+        always[k] = !finite || at_cam;
+        nearv[k] = finite ? std::sqrt(d2) : 0.0;
+    }
+    struct Rect { int i0, i1, j0, j1; };
+    std::vector<Rect> rect(6 * n);
+    int fx0[6], fx1[6], fy0[6], fy1[6];
+    for (R = std::max(1, R);; R = std::max(1, R / 2)) {
+        size_t total = 0;
+        for (int f = 0; f < 6; ++f) {
+            const int a = f >> 1, b = (a + 1) % 3, cax = (a + 2) % 3;
+            const double s = (f & 1) ? -1.0 : 1.0;
+            fx0[f] = R; fx1[f] = -1; fy0[f] = R; fy1[f] = -1;
+            for (size_t k = 0; k < n; ++k) {
+                Rect& q = rect[f * n + k];
+                q = Rect{1, 0, 1, 0};
+                if (always[k]) continue;
+                const double alo = s > 0 ? lo[3 * k + a] : -hi[3 * k + a];
+                const double ahi = s > 0 ? hi[3 * k + a] : -lo[3 * k + a];
+                if (!(ahi > 0.0)) continue;
+                const Range u = face_range(alo, ahi, lo[3 * k + b], hi[3 * k + b]);
+                const Range v = face_range(alo, ahi, lo[3 * k + cax], hi[3 * k + cax]);
+                if (u.empty() || v.empty() || u.lo > 1.0 + kUMargin || u.hi < -1.0 - kUMargin ||
+                    v.lo > 1.0 + kUMargin || v.hi < -1.0 - kUMargin)
+                    continue;
+                q.i0 = cell_of(u.lo - kUMargin, R); q.i1 = cell_of(u.hi + kUMargin, R);
+                q.j0 = cell_of(v.lo - kUMargin, R); q.j1 = cell_of(v.hi + kUMargin, R);
+                fx0[f] = std::min(fx0[f], q.i0); fx1[f] = std::max(fx1[f], q.i1);
+                fy0[f] = std::min(fy0[f], q.j0); fy1[f] = std::max(fy1[f], q.j1);
+                total += static_cast<size_t>(q.i1 - q.i0 + 1) * (q.j1 - q.j0 + 1);
+            }
+        }
+        if (total <= max_entries || R == 1) break;
+    }
+    g.R = R;
+    g.always_begin = 0;
+    for (size_t k = 0; k < n; ++k)
+        if (always[k]) out.ent.push_back(DevLgEntry{static_cast<int32_t>(k), 0.0f});
+    g.always_end = static_cast<uint32_t>(out.ent.size());
+    for (int f = 0; f < 6; ++f) {
+        g.off_base[f] = static_cast<uint32_t>(out.off.size());
+        if (fx1[f] < fx0[f]) { g.fx0[f] = 0; g.fy0[f] = 0; g.fw[f] = 0; g.fh[f] = 0; continue; }
+        const int w = fx1[f] - fx0[f] + 1, h = fy1[f] - fy0[f] + 1;
+        g.fx0[f] = fx0[f]; g.fy0[f] = fy0[f]; g.fw[f] = w; g.fh[f] = h;
+        const size_t cells = static_cast<size_t>(w) * h;
+        std::vector<uint32_t> cnt(cells + 1, 0);
+        for (size_t k = 0; k < n; ++k) {
+            const Rect& q = rect[f * n + k];
+            for (int j = q.j0; j <= q.j1; ++j)
+                for (int i = q.i0; i <= q.i1; ++i) ++cnt[static_cast<size_t>(j - fy0[f]) * w + (i - fx0[f])];
+        }
+        const uint32_t base = static_cast<uint32_t>(out.ent.size());
+        uint32_t run = base;
+        const size_t ob = out.off.size();
+        out.off.resize(ob + cells + 1);
+        for (size_t c = 0; c < cells; ++c) { out.off[ob + c] = run; run += cnt[c]; cnt[c] = out.off[ob + c]; }
+        out.off[ob + cells] = run;
+        out.ent.resize(run);
+        for (size_t k = 0; k < n; ++k) {        // sphere order within a cell, then sorted by distance
+            const Rect& q = rect[f * n + k];
+            float nf = static_cast<float>(nearv[k]);
+            if (static_cast<double>(nf) > nearv[k]) nf = std::nextafter(nf, 0.0f);
+            for (int j = q.j0; j <= q.j1; ++j)
+                for (int i = q.i0; i <= q.i1; ++i)
+                    out.ent[cnt[static_cast<size_t>(j - fy0[f]) * w + (i - fx0[f])]++] = DevLgEntry{static_cast<int32_t>(k), nf};
+        }
+        for (size_t c = 0; c < cells; ++c)
+            std::sort(out.ent.begin() + out.off[ob + c], out.ent.begin() + out.off[ob + c + 1],
+                      [](const DevLgEntry& x, const DevLgEntry& y) { return x.near < y.near || (x.near == y.near && x.sph < y.sph); });
+    }
+    return out;
+}
+
 // The device's candidate list for a shadow query from p toward light `li`
 // (occluded_lgrid, trace_common.hpp), with the same f32 arithmetic: the always
 // list, then p's cell up to the early stop.  Returns false when the device

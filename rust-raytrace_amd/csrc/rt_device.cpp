@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <utility>
@@ -34,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -59,7 +60,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"bstreams", 2, 1, 4},                       // streams for the shadow + shading kernels
     {"fuse", 0, 0, 1},                           // shading inside the shadow kernel
     {"lists", 1, 0, 1},                          // shadow item lists (with fuse)
-    {"cam", -1, -1, 2},                          // generation 0: 0 per ray, 1 camera tiles in LDS, 2 from L2
+    {"cam", -1, -1, 3},                          // generation 0: 0 per ray, 1 camera tiles in LDS, 2 from L2, 3 the
+                                                 // camera's view grid
     {"deal", 1, 0, 1},                           // chunk dealing: 1 workgroup-major, 0 workgroup-first
     {"spread_below", 0, 0, INT32_MAX},           // queues below this size are dealt workgroup-first
     {"lists0", 0, 0, 1},                         // shadow lists from generation 0
@@ -86,6 +88,8 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // launch after the last nearest-hit launch; 0 off, -1 auto
     {"wave_max", -1, -1, INT32_MAX},             // src 9, generations >= 1: queues of <= this many rays take the
                                                  // wave-cooperative query (nearest_wave); 0 off, -1 auto
+    {"cam_grid_res", 0, -1, 4096},               // the camera's view grid: cells per face side (0: from the scene's
+                                                 // frame size, -1: no grid); takes effect at the next rt_scene_upload
 };
 
 }  // namespace
@@ -590,6 +594,84 @@ int rt_light_grid_candidates(const rt_scene* s, int light, int resolution, const
     }
 }
 
+// The view grid's automatic resolution: a cell about 8 x 8 pixels of the scene's frame.
+static int view_grid_res(const rt_scene* s, int64_t forced) {
+    if (forced > 0) return static_cast<int>(forced);
+    const double* M = s->camera.matrix;
+    const double imd = std::sqrt(M[2] * M[2] + M[5] * M[5] + M[8] * M[8]);
+    const double side = static_cast<double>(std::max(std::max(s->width, s->height), 64u));
+    return std::isfinite(imd) ? static_cast<int>(std::lround(std::clamp(imd * side / 8.0, 16.0, 2048.0))) : 64;
+}
+constexpr size_t kViewGridEntries = size_t{32} << 20;
+
+int rt_view_grid_candidates(const rt_scene* s, int resolution, const double* dirs, uint32_t n_dirs, int32_t* counts,
+                            int32_t* ids, float* nears, size_t cap, int64_t* info) {
+    if (!s || (n_dirs && (!dirs || !counts)) || (cap && (!ids || !nears)) || resolution < 0 || resolution > 4096)
+        return RT_E_INVALID;
+    try {
+        std::vector<DevSphere> spheres;
+        std::vector<double> srad;
+        std::vector<int32_t> obj;
+        double extent = 0.0;
+        for (size_t i = 0; i < s->objects.size(); ++i) {
+            const rt_object& o = s->objects[i];
+            if (o.shape != RT_SHAPE_SPHERE) continue;
+            spheres.push_back(DevSphere{o.geom[0], o.geom[1], o.geom[2], o.geom[3] * o.geom[3]});
+            srad.push_back(o.geom[3]);
+            obj.push_back(static_cast<int32_t>(i));
+            const double r = std::fabs(o.geom[3]);
+            for (int k = 0; k < 3; ++k)
+                for (double v : {o.geom[k] - r, o.geom[k] + r})
+                    if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
+        }
+        const LightGridResult g = build_view_grid(spheres, srad, s->camera.position, 1e-5 * (1.0 + extent),
+                                                  view_grid_res(s, resolution), kViewGridEntries);
+        const DevLightGrid& G = g.grids[0];
+        if (info) {
+            info[0] = G.R;
+            int64_t cells = 0;
+            for (int f = 0; f < 6; ++f) cells += static_cast<int64_t>(G.fw[f]) * G.fh[f];
+            info[1] = cells;
+            info[2] = static_cast<int64_t>(g.ent.size());
+        }
+        size_t used = 0;
+        auto put = [&](const DevLgEntry& e) {
+            if (used == cap) throw std::length_error("candidate buffer too small");
+            ids[used] = obj[e.sph];
+            nears[used++] = e.near;
+        };
+        for (uint32_t i = 0; i < n_dirs; ++i) {
+            const size_t before = used;
+            for (uint32_t e = G.always_begin; e < G.always_end; ++e) put(g.ent[e]);
+            // the device's lookup (nearest_cgrid): f32 direction, dominant axis, clamped cell
+            const float dx = static_cast<float>(dirs[3 * i]), dy = static_cast<float>(dirs[3 * i + 1]),
+                        dz = static_cast<float>(dirs[3 * i + 2]);
+            const float ax = std::fabs(dx), ay = std::fabs(dy), az = std::fabs(dz);
+            const int fa = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+            const float da = fa == 0 ? dx : fa == 1 ? dy : dz;
+            const float db = fa == 0 ? dy : fa == 1 ? dz : dx;
+            const float dc = fa == 0 ? dz : fa == 1 ? dx : dy;
+            if (G.R <= 0 || !(std::fabs(da) > 0.0f && std::fabs(da) < 3.0e38f)) { counts[i] = -1; used = before; continue; }
+            const int f = 2 * fa + (da < 0.0f ? 1 : 0);
+            const float inv = 1.0f / std::fabs(da);
+            const float R = static_cast<float>(G.R);
+            const int ci = std::min(std::max(static_cast<int>(std::floor((db * inv + 1.0f) * 0.5f * R)), 0), G.R - 1);
+            const int cj = std::min(std::max(static_cast<int>(std::floor((dc * inv + 1.0f) * 0.5f * R)), 0), G.R - 1);
+            const int li = ci - G.fx0[f], lj = cj - G.fy0[f];
+            if (li >= 0 && lj >= 0 && li < G.fw[f] && lj < G.fh[f]) {
+                const uint32_t cell = G.off_base[f] + static_cast<uint32_t>(lj * G.fw[f] + li);
+                for (uint32_t e = g.off[cell]; e < g.off[cell + 1]; ++e) put(g.ent[e]);
+            }
+            counts[i] = static_cast<int32_t>(used - before);
+        }
+        return RT_OK;
+    } catch (const std::length_error& e) {
+        return fail(nullptr, RT_E_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return fail(nullptr, RT_E_NOMEM, e.what());
+    }
+}
+
 static int scene_upload(rt_ctx* c, const rt_scene* s) {
     HIP_TRY(c, hipSetDevice(c->device));
     // Every class of the reference except SkyboxBackground (textures) has a
@@ -694,6 +776,12 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     // light-view grids of the point lights (tuning: "light_grids" 0 disables, "light_grid_res" forces the resolution)
     LightGridResult lg;
     if (c->t(kTuneLgrid) != 0) lg = build_light_grids(spheres, r_leaf, lights, pad, static_cast<int>(c->t(kTuneLgridRes)));
+    // the camera's view grid (generation 0, tuning "cam" 3): a cell about 8 x 8 pixels of the
+    // scene's own frame size, im_dist * max(W, H) / 8 cells per face side (tuning "cam_grid_res")
+    LightGridResult cg;
+    if (s->camera.kind == RT_CAMERA_SIMPLE && c->t(kTuneCamGridRes) >= 0)
+        cg = build_view_grid(spheres, r_leaf, s->camera.position, pad, view_grid_res(s, c->t(kTuneCamGridRes)),
+                             kViewGridEntries);
     // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights][bvh], 256-B aligned pieces.
     size_t off = 0;
     auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
@@ -711,6 +799,9 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_lg = place(lg.grids.size() * sizeof(DevLightGrid));
     const size_t o_lgoff = place(lg.off.size() * sizeof(uint32_t));
     const size_t o_lgent = place(lg.ent.size() * sizeof(DevLgEntry));
+    const size_t o_cg = place(cg.grids.size() * sizeof(DevLightGrid));
+    const size_t o_cgoff = place(cg.off.size() * sizeof(uint32_t));
+    const size_t o_cgent = place(cg.ent.size() * sizeof(DevLgEntry));
     const size_t o_cl = place(cls.clusters.size() * sizeof(DevCluster));
     const size_t o_clp = place(cls.perm.size() * sizeof(uint16_t));
     size_t tex_bytes = 0;
@@ -735,6 +826,9 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_lg, lg.grids.data(), lg.grids.size() * sizeof(DevLightGrid));
     put(o_lgoff, lg.off.data(), lg.off.size() * sizeof(uint32_t));
     put(o_lgent, lg.ent.data(), lg.ent.size() * sizeof(DevLgEntry));
+    put(o_cg, cg.grids.data(), cg.grids.size() * sizeof(DevLightGrid));
+    put(o_cgoff, cg.off.data(), cg.off.size() * sizeof(uint32_t));
+    put(o_cgent, cg.ent.data(), cg.ent.size() * sizeof(DevLgEntry));
     put(o_cl, cls.clusters.data(), cls.clusters.size() * sizeof(DevCluster));
     put(o_clp, cls.perm.data(), cls.perm.size() * sizeof(uint16_t));
     if (skybox)
@@ -793,6 +887,9 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.lgrid = lg.grids.empty() ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_lg);
     d.lg_off = reinterpret_cast<const uint32_t*>(base + o_lgoff);
     d.lg_ent = reinterpret_cast<const DevLgEntry*>(base + o_lgent);
+    d.cgrid = (cg.grids.empty() || cg.grids[0].R <= 0) ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_cg);
+    d.cg_off = reinterpret_cast<const uint32_t*>(base + o_cgoff);
+    d.cg_ent = reinterpret_cast<const DevLgEntry*>(base + o_cgent);
     d.clusters = cls.clusters.empty() ? nullptr : reinterpret_cast<const DevCluster*>(base + o_cl);
     d.cl_perm = reinterpret_cast<const uint16_t*>(base + o_clp);
     d.n_clusters = static_cast<int32_t>(cls.clusters.size());
@@ -983,6 +1080,9 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             if (ce == 0) cam = 0;
             else if (ce == 2) cam = 2;
         }
+        // the camera's view grid (any sphere source): spheres staged in LDS when they fit (3), else through L2 (4)
+        if (c->t(kTuneCam) == 3 && c->dsc.cgrid)
+            cam = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) <= kLdsBudget ? 3 : 4;
         const uint32_t wg_major = c->t(kTuneDeal) != 0 ? 1u : 0u;
         if (c->t(kTuneVerbose))
             std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d short_stack %d split %d pfx %d/%d\n",

@@ -1244,6 +1244,62 @@ __device__ __forceinline__ bool occluded_lgrid(const DevScene& sc, const BvhView
     return false;
 }
 
+// ---- generation 0: the camera's view grid --------------------------------
+// Scene::intersect for a camera ray (origin = the camera position) through the
+// camera's view grid (host_lightgrid.cpp build_view_grid): the planes, the
+// always list, then the ray direction's cell in increasing box distance from
+// the camera, stopping at the first entry whose distance bound exceeds the
+// current best t (t_limit margin).  A reported hit point lies in its sphere's
+// padded box and in the ray direction from the camera, so its sphere is on
+// that cell's list, and its distance from the camera (t |d|, |d| = 1 up to
+// rounding) is at least the entry's bound: every sphere that could win or tie
+// is tested with the exact quadratic, and the (t, object id) minimum is the
+// linear scan's (scene.rs:247-249).  A degenerate direction
+// tests every sphere.
+template <bool kCount = false>
+__device__ __forceinline__ Hit nearest_cgrid(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+    Hit h = nearest_planes(sc, r);
+    if (h.nan_t || sc.n_spheres == 0) return h;
+    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
+    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const DevLightGrid& g = *sc.cgrid;
+    float lim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    auto test = [&](int32_t k) {
+        if constexpr (kCount) ++w->spheres;
+        double t;
+        if (sphere_t(v.sph[k], r, a2, a4, t)) {
+            const int32_t obj = v.obj[k];
+            if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = k; lim = t_limit(t); }
+        }
+    };
+    for (uint32_t e = g.always_begin; e < g.always_end; ++e) test(sc.cg_ent[e].sph);
+    const float dx = static_cast<float>(r.dx), dy = static_cast<float>(r.dy), dz = static_cast<float>(r.dz);
+    const float ax = fabsf(dx), ay = fabsf(dy), az = fabsf(dz);
+    const int fa = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    const float da = fa == 0 ? dx : fa == 1 ? dy : dz;
+    const float db = fa == 0 ? dy : fa == 1 ? dz : dx;
+    const float dc = fa == 0 ? dz : fa == 1 ? dx : dy;
+    if (!(fabsf(da) > 0.0f && fabsf(da) < 3.0e38f)) {
+        for (int32_t k = 0; k < sc.n_spheres; ++k) test(k);
+        return h;
+    }
+    const int f = 2 * fa + (da < 0.0f ? 1 : 0);
+    const float inv = 1.0f / fabsf(da);
+    const float R = static_cast<float>(g.R);
+    const int ci = min(max(static_cast<int>(floorf((db * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int cj = min(max(static_cast<int>(floorf((dc * inv + 1.0f) * 0.5f * R)), 0), g.R - 1);
+    const int li = ci - g.fx0[f], lj = cj - g.fy0[f];
+    if (li < 0 || lj < 0 || li >= g.fw[f] || lj >= g.fh[f]) return h;        // no sphere box in this direction
+    const uint32_t cell = g.off_base[f] + static_cast<uint32_t>(lj * g.fw[f] + li);
+    const uint32_t e0 = sc.cg_off[cell], e1 = sc.cg_off[cell + 1];
+    for (uint32_t e = e0; e < e1; ++e) {
+        const DevLgEntry en = sc.cg_ent[e];
+        if (en.near > lim) break;
+        test(en.sph);
+    }
+    return h;
+}
+
 // ---- generation 0: camera rays by 8x8 tile -----------------------------
 // Every camera ray starts at the camera, so the wave's 64 rays of one pixel
 // tile share a rectangle of image-plane coordinates [tx0, tx1] x [ty0, ty1]

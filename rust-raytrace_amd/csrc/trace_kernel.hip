@@ -366,12 +366,17 @@ constexpr int kSrcCamG = 21;        // camera nodes + spheres from HBM/L2
 // spheres from LDS or HBM/L2.
 constexpr int kSrcGridL = 14;
 constexpr int kSrcGridG = 15;
+// Generation 0 only: camera rays through the camera's view grid (nearest_cgrid),
+// spheres staged in LDS (22) or read through L2 (23).
+constexpr int kSrcCamGridL = 22;
+constexpr int kSrcCamGridG = 23;
 
 template <int kSrc>
 struct Src {
     static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
     static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
-    static constexpr bool bvh = kSrc >= kSrcBvhG && !grid;
+    static constexpr bool cgrid = kSrc == kSrcCamGridL || kSrc == kSrcCamGridG;
+    static constexpr bool bvh = kSrc >= kSrcBvhG && !grid && !cgrid;
     static constexpr bool quad = kSrc == kSrcBvh4Q;
     static constexpr bool wide = (kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P) || quad;
     static constexpr bool half = kSrc == kSrcBvhPH || kSrc == kSrcBvhPHC;
@@ -380,7 +385,7 @@ struct Src {
     static constexpr bool compact = kSrc == kSrcBvhL8C;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
                                     kSrc == kSrcCamL || quad;
-    static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL;
+    static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL || kSrc == kSrcCamGridL;
     static constexpr int nodes = all_lds ? 2 : half ? 3 : prefix ? 1 : 0;
     static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 && !quad) || half ? 8 : 4;   // min waves per SIMD
 };
@@ -407,6 +412,7 @@ template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
     if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
+    if (kSrc == kSrcCamGridL) bytes = static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
     if (Src<kSrc>::half) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNodeH);
     if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
@@ -472,6 +478,15 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
         v.sph = ls;
         return v;
+    } else if constexpr (kSrc == kSrcCamGridL) {
+        DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
+        int32_t* lo = reinterpret_cast<int32_t*>(ls + sc.n_spheres);
+        for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
+        v.sph = ls;
+        v.obj = lo;
+        return v;
+    } else if constexpr (kSrc == kSrcCamGridG) {
+        return v;
     } else if constexpr (Src<kSrc>::nodes > 0 && Src<kSrc>::wide) {
         DevBvh4Plane* lp = reinterpret_cast<DevBvh4Plane*>(lds);
         const int n = kBvh4Planes * sc.n_bvh4;
@@ -516,7 +531,8 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
 #endif
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
-    if constexpr (Src<kSrc>::quad) return nearest_quad<kCount>(sc, v, r, w);
+    if constexpr (Src<kSrc>::cgrid) return nearest_cgrid<kCount>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::quad) return nearest_quad<kCount>(sc, v, r, w);
     else if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
@@ -1275,6 +1291,12 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     } else if (k == 0 && ws.cam == 2) {
         if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamG, true, true); else RT_NEARC(kSrcCamG, false, true); }
         else if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
+    } else if (k == 0 && ws.cam == 3) {          // the camera's view grid, spheres in LDS
+        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamGridL, true, true); else RT_NEARC(kSrcCamGridL, false, true); }
+        else if (sc.has_fresnel) RT_NEAR(kSrcCamGridL, true, true); else RT_NEAR(kSrcCamGridL, true, false);
+    } else if (k == 0 && ws.cam == 4) {          // ... spheres through L2
+        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamGridG, true, true); else RT_NEARC(kSrcCamGridG, false, true); }
+        else if (sc.has_fresnel) RT_NEAR(kSrcCamGridG, true, true); else RT_NEAR(kSrcCamGridG, true, false);
     } else if (k == 0 && lists) {
         if (sc.has_fresnel) RT_NEARC(kSrcN, true, true); else RT_NEARC(kSrcN, false, true);
     } else if (k == 0) {

@@ -121,6 +121,8 @@ def _load():
         "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
         "rt_light_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, C.c_int, P(C.c_double), C.c_uint32,
                                                P(C.c_int32), P(C.c_int32), C.c_size_t, P(C.c_int64)]),
+        "rt_view_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, P(C.c_double), C.c_uint32, P(C.c_int32),
+                                              P(C.c_int32), P(C.c_float), C.c_size_t, P(C.c_int64)]),
         "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
         "rt_ctx_get_tuning": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
         "rt_tuning_key": (C.c_char_p, [C.c_int]),
@@ -215,6 +217,30 @@ class Scene:
         h = C.c_void_p()
         _check(lib.rt_scene_from_desc(C.byref(desc), C.byref(h)))
         return cls(h.value)
+
+    def view_grid_candidates(self, dirs, cap=1 << 23, resolution=0):
+        """Diagnostic (host only): for each camera-ray direction, (object ids,
+        distance bounds) the camera's view grid hands the device (None when it
+        tests every sphere), and (R, stored cells, list entries)."""
+        d = np.ascontiguousarray(dirs, dtype=np.float64).reshape(-1, 3)
+        n = d.shape[0]
+        counts = np.zeros(n, np.int32)
+        ids = np.zeros(cap, np.int32)
+        nears = np.zeros(cap, np.float32)
+        info = np.zeros(3, np.int64)
+        _check(lib.rt_view_grid_candidates(self._h, int(resolution), d.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                           counts.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           nears.ctypes.data_as(C.POINTER(C.c_float)), cap,
+                                           info.ctypes.data_as(C.POINTER(C.c_int64))))
+        out, at = [], 0
+        for c in counts:
+            if c < 0:
+                out.append(None)
+            else:
+                out.append((ids[at:at + c].copy(), nears[at:at + c].copy()))
+                at += c
+        return out, tuple(int(x) for x in info)
 
     def light_grid_candidates(self, light, points, cap=1 << 22, resolution=0):
         """Diagnostic (host only): for each point p, the object ids the light-view

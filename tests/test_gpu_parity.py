@@ -343,6 +343,32 @@ def test_wave_cooperative_query_matches_oracle(gpu_ctx, scene):
             check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
+@pytest.mark.parametrize("scene", ["axis_ties", "config3", "dense", "planes_nan", "config4", "camera_inside"])
+def test_camera_view_grid_matches_oracle(gpu_ctx, scene):
+    """Generation 0 through the camera's view grid (tuning cam 3, trace_common.hpp
+    nearest_cgrid; spheres in LDS, or through L2 for 10k spheres): camera rays
+    on the axes, coincident spheres, NaN planes, the camera inside spheres and
+    the C3 / C4 workloads match the oracle bit for bit."""
+    def camera_inside():
+        s = scenes.SceneSpec(width=41, height=29, max_depth=3, background=(0.1, 0.2, 0.3),
+                             camera={"ctor": "new", "position": (0.0, 0.0, 0.0), "look": (0.0, 0.0, -1.0),
+                                     "up": (0.0, 1.0, 0.0), "im_dist": 1.0})
+        rng = scenes.SplitMix64(31)
+        for k in range(200):
+            c = (rng.uniform(-6, 6), rng.uniform(-4, 4), rng.uniform(-15, 3))
+            s.sphere(c, rng.uniform(0.05, 1.0), scenes.phong((0.4, 0.5, 0.6), (0.5, 0.5, 0.5), 20.0, (0.01, 0, 0)))
+        s.sphere((0.2, 0.0, 0.0), 0.5, scenes.phong((0.9, 0.1, 0.1), (0.3, 0.3, 0.3), 8.0, (0.1, 0, 0)))
+        s.point_light((2, 3, 1), (1, 1, 1))
+        return s
+    s = {"axis_ties": _axis_tie_scene, "config3": lambda: scenes.config3(160, 128),
+         "dense": lambda: scenes.config3(128, 96, view="dense"), "planes_nan": _nan_plane_scene,
+         "config4": lambda: scenes.config4(96, 80), "camera_inside": camera_inside}[scene]()
+    with _with_tuning(gpu_ctx, cam=3):                       # (check_parity uploads: the grid is built then)
+        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+    with _with_tuning(gpu_ctx, cam=3, cam_grid_res=7):       # a coarse grid: long lists, same bits
+        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+
+
 @pytest.mark.parametrize("algo", [lr.RT_ALGO_WAVEFRONT, lr.RT_ALGO_WAVEFRONT_BRUTE])
 def test_extreme_sphere_sizes_and_far_plane_origins(gpu_ctx, algo):
     s = scenes.config2(97, 61)
@@ -627,7 +653,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(fold_split=1), dict(fold_split=4), dict(fold_split=8), dict(fold_split=3, bstreams=1),
                dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3), dict(bmerge=1), dict(bmerge=3),
                dict(bmerge=5, tail_from=1, tail_max=1 << 30), dict(bmerge=2, regions=2048), dict(wave_max=0),
-               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4)]:
+               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4), dict(cam=3)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

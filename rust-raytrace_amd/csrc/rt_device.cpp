@@ -1080,8 +1080,9 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             if (ce == 0) cam = 0;
             else if (ce == 2) cam = 2;
         }
-        // the camera's view grid (any sphere source): spheres staged in LDS when they fit (3), else through L2 (4)
-        if (c->t(kTuneCam) == 3 && c->dsc.cgrid)
+        // the camera's view grid (any sphere source): spheres staged in LDS when they fit (3), else through L2 (4);
+        // the default where built (C3 camera pass 520 -> 327 us, 3.46 -> 3.26 ms per frame on one box)
+        if ((c->t(kTuneCam) == 3 || (c->t(kTuneCam) < 0 && mode == RT_ALGO_WAVEFRONT)) && c->dsc.cgrid)
             cam = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) <= kLdsBudget ? 3 : 4;
         const uint32_t wg_major = c->t(kTuneDeal) != 0 ? 1u : 0u;
         if (c->t(kTuneVerbose))
@@ -1159,8 +1160,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             if (total > 80 * 1024) c->dsc.cl_slots = 0;
         }
         const int64_t wave_t = c->t(kTuneWaveMax);
+        // (auto: off -- measured slower than the quad walk on the tail of an 8-way C3 share: a ray that
+        // misses tests every cluster box it crosses, 60-78 vs 43 us per launch)
         const uint32_t wave_max = src != 9 || c->dsc.cl_slots == 0 ? 0u
-                                  : wave_t >= 0 ? static_cast<uint32_t>(wave_t) : 32768u;
+                                  : wave_t >= 0 ? static_cast<uint32_t>(wave_t) : 0u;
         for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tail_from = tail_from;
             c->lanes[l].b.tail_max = tail_max;

@@ -1155,33 +1155,38 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FramePara
     }
 }
 
-// One chain per work-item: chain c (generation 0's record entry c, region
-// c / R) folds its levels onto its terminal and writes pixel cpix[c].  Entries
-// past their region's record count are empty (a 256-entry block lies in one
-// region: R is a multiple of 1024).  The quantisation table is staged in LDS:
-// the binary search indexes it with a different entry per lane, which from
-// __constant__ memory costs nine dependent vector loads per channel.  Levels
-// and terminals are read in chain order, i.e. coalesced.
+// One chain per work-item: the chains of the chunk are generation 0's shade
+// records (chain c = record entry c), dealt densely over G workgroups through
+// the region scan of generation 0's record counts, 64 consecutive chains to a
+// wave (so levels and terminals are read in chain order, coalesced).  The
+// launch is G workgroups whatever the queue capacity: one workgroup per 256
+// entries of capacity (the first design) dispatched tens of thousands of
+// mostly empty workgroups, ~80 us of dispatch for one rank's share of an
+// 8-way C3 frame.  Chain c folds its levels onto its terminal and writes
+// pixel cpix[c].  The quantisation table is staged in LDS: the binary search
+// indexes it with a different entry per lane, which from __constant__ memory
+// costs nine dependent vector loads per channel.
 // Only chains of lo <= nlev <= hi: the split fold (tuning fold_split = K) folds
 // the chains that ended by generation K on a B stream while the later
 // generations run (every level and terminal they need is written by then),
 // and the rest after the last generation.
 template <bool kFresnel>
-__global__ __launch_bounds__(kBlock) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
+__global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
     __shared__ double s_srgb[255];
-    const uint32_t base = blockIdx.x * kBlock;
-    const uint32_t cnt = b.rs()[base / b.R];              // generation 0: rs[0 * G + region]
-    if (base % b.R >= cnt) return;                         // nothing in this block
-    const uint32_t c = base + threadIdx.x;
-    const uint32_t nlev = c % b.R < cnt ? b.nlev()[c] : kNlevRunning;
-    const bool mine = nlev >= lo && nlev <= hi;            // (kNlevRunning: not ended yet / no chain)
-    if (__syncthreads_or(mine) == 0) return;
-    for (int i = threadIdx.x; i < 255; i += kBlock) s_srgb[i] = c_srgb_avg[i];
-    __syncthreads();
-    if (!mine) return;
-    const uint32_t p = b.cpix()[c];
-    const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, static_cast<uint8_t>(nlev)), fp.spp);
-    write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+    __shared__ uint32_t s_scan[kMaxRegions + 1];
+    __shared__ uint32_t s_wave[kWfThreads / 64];
+    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
+    region_scan(b.rs(), b.G, s_scan, s_wave);             // generation 0's records = the chains (also publishes s_srgb)
+    const uint32_t n = s_scan[b.G];
+    RT_FOR_CHUNKS(b, n, j) {
+        if (j >= n) continue;
+        const uint32_t c = static_cast<uint32_t>(region_entry(s_scan, b.G, b.R, j));
+        const uint32_t nlev = b.nlev()[c];
+        if (nlev < lo || nlev > hi) continue;               // (kNlevRunning: not ended yet)
+        const uint32_t p = b.cpix()[c];
+        const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, static_cast<uint8_t>(nlev)), fp.spp);
+        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+    }
 }
 
 template <bool kUnused = false>
@@ -1189,9 +1194,8 @@ hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& 
                        uint32_t lo, uint32_t hi) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    const dim3 gf(static_cast<uint32_t>(b.qcap / kBlock));             // qcap = G * R, R % 1024 == 0
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), gf, dim3(kBlock), 0, s, sc, fp, b, lo, hi);
-    else hipLaunchKernelGGL((wf_fold<false>), gf, dim3(kBlock), 0, s, sc, fp, b, lo, hi);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 

@@ -903,17 +903,34 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
 // the shadow mask of its lights: a specular hit pushes the level's local
 // colour (its reflection ray was already queued by wf_nearest); any other hit
 // ends the chain with it.
+// A shade record's fields (loaded ahead of its shading by wf_shade).
+struct ShadeIn {
+    double ptx, pty, ptz, dx, dy, dz, sig;
+    int32_t obj, prim;
+    uint32_t c, mask;
+};
+
+__device__ __forceinline__ ShadeIn shade_load(const WfBufs& b, size_t at, bool mask) {
+    ShadeIn in;
+    in.ptx = ldn_if<2>(&b.rf(0)[at]); in.pty = ldn_if<2>(&b.rf(1)[at]); in.ptz = ldn_if<2>(&b.rf(2)[at]);
+    in.dx = ldn_if<2>(&b.rf(3)[at]); in.dy = ldn_if<2>(&b.rf(4)[at]); in.dz = ldn_if<2>(&b.rf(5)[at]);
+    in.sig = ldn_if<2>(&b.rf(6)[at]);
+    in.obj = static_cast<int32_t>(ldn_if<2>(&b.ru(0)[at]));
+    in.prim = static_cast<int32_t>(ldn_if<2>(&b.ru(1)[at]));
+    in.c = ldn_if<2>(&b.ru(2)[at]);                         // the record's chain
+    in.mask = mask ? b.ru(3)[at] : 0u;
+    return in;
+}
+
 template <bool kFresnel>
-__device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
-    const double ptx = ldn_if<2>(&b.rf(0)[at]), pty = ldn_if<2>(&b.rf(1)[at]), ptz = ldn_if<2>(&b.rf(2)[at]);
-    const double dx = ldn_if<2>(&b.rf(3)[at]), dy = ldn_if<2>(&b.rf(4)[at]), dz = ldn_if<2>(&b.rf(5)[at]);
-    const double sig = ldn_if<2>(&b.rf(6)[at]);
-    const int32_t obj = static_cast<int32_t>(ldn_if<2>(&b.ru(0)[at]));
-    const uint32_t c = ldn_if<2>(&b.ru(2)[at]);             // the record's chain
+__device__ __forceinline__ void shade_compute(const DevScene& sc, const WfBufs& b, int k, size_t at, const ShadeIn& in) {
+    const double ptx = in.ptx, pty = in.pty, ptz = in.ptz, dx = in.dx, dy = in.dy, dz = in.dz, sig = in.sig;
+    const int32_t obj = in.obj;
+    const uint32_t c = in.c, mask = in.mask;
     const DevMaterial& m = sc.mats[obj];
     Col res{m.amb[0], m.amb[1], m.amb[2]};                               // raytrace.rs:32
     double nx, ny, nz;
-    hit_normal(sc, sc.spheres, static_cast<int32_t>(ldn_if<2>(&b.ru(1)[at])), ptx, pty, ptz, nx, ny, nz);
+    hit_normal(sc, sc.spheres, in.prim, ptx, pty, ptz, nx, ny, nz);
     const double nd = nx * dx + ny * dy + nz * dz;
     const Shading sh = shading_flags<kFresnel>(m, sig, nd);
     const bool diffuse = sh.diffuse, specular = sh.specular;
@@ -936,6 +953,13 @@ __device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b
     } else {
         set_terminal(b, c, res, k);
     }
+}
+
+template <bool kFresnel>
+__device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
+    ShadeIn in = shade_load(b, at, false);
+    in.mask = mask;
+    shade_compute<kFresnel>(sc, b, k, at, in);
 }
 
 // Fused shadow + shading: each (record, light) item adds its shadow bit and
@@ -978,17 +1002,45 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
     __syncthreads();
     Work w;
     const size_t rk = static_cast<size_t>(k) * b.qcap;
-    // light-major: a wave traces 64 consecutive records toward ONE light (coherent)
-    RT_FOR_CHUNKS(b, n, qi) {
+    // light-major: a wave traces 64 consecutive records toward ONE light (coherent).
+    // Software pipelined: the next chunk's shade points are loaded (HBM) before this
+    // chunk's queries run, so their latency hides behind the list walks.
+    const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    auto item_at = [&](uint32_t qi, uint32_t& l) {
+        l = qi / nrec;
+        return rk + region_entry(ql.scan, M, b.R, qi - l * nrec);
+    };
+    uint32_t rc = wave_slot(b, n), lc = 0;
+    size_t atc = 0;
+    double pc[3] = {0.0, 0.0, 0.0};
+    int32_t hc = -1;
+    if (static_cast<uint64_t>(rc) * 64u + lane < n) {
+        atc = item_at(rc * 64u + lane, lc);
+        pc[0] = ldn_if<3>(&b.rf(0)[atc]); pc[1] = ldn_if<3>(&b.rf(1)[atc]); pc[2] = ldn_if<3>(&b.rf(2)[atc]);
+        hc = static_cast<int32_t>(b.ru(1)[atc]);
+    }
+    for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
+        const uint64_t qn = static_cast<uint64_t>(rc + W) * 64u + lane;
+        uint32_t ln = 0;
+        size_t atn = 0;
+        double pn[3] = {0.0, 0.0, 0.0};
+        int32_t hn = -1;
+        if (qn < n) {
+            atn = item_at(static_cast<uint32_t>(qn), ln);
+            pn[0] = ldn_if<3>(&b.rf(0)[atn]); pn[1] = ldn_if<3>(&b.rf(1)[atn]); pn[2] = ldn_if<3>(&b.rf(2)[atn]);
+            hn = static_cast<int32_t>(b.ru(1)[atn]);
+        }
+        const uint32_t qi = rc * 64u + lane;
+        const uint32_t l = lc;
+        const size_t at = atc;
+        const double ptx = pc[0], pty = pc[1], ptz = pc[2];
+        const int32_t hint = hc;
+        lc = ln; atc = atn; pc[0] = pn[0]; pc[1] = pn[1]; pc[2] = pn[2]; hc = hn;
         if (qi >= n) continue;
-        const uint32_t l = qi / nrec, j = qi - l * nrec;
-        const size_t at = rk + region_entry(ql.scan, M, b.R, j);
-        const double ptx = ldn_if<3>(&b.rf(0)[at]), pty = ldn_if<3>(&b.rf(1)[at]), ptz = ldn_if<3>(&b.rf(2)[at]);
         double lx, ly, lz, r2;
         const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
-        const int32_t hint = static_cast<int32_t>(b.ru(1)[at]);
         bool occluded;
         if constexpr (Src<kSrc>::grid)          // the host checked: every light has a grid
             occluded = occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w);
@@ -1065,10 +1117,32 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     region_scan(b.rs() + k * b.G, M, s_scan, s_wave);
     const uint32_t n = s_scan[M];
     const size_t rk = static_cast<size_t>(k) * b.qcap;
-    RT_FOR_CHUNKS(b, n, j) {
-        if (j >= n) continue;
-        const size_t at = rk + region_entry(s_scan, M, b.R, j);
-        shade_record<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, sc.n_lights > 0 ? b.ru(3)[at] : 0u);
+    // software pipelined: the next chunk's records are loaded (HBM) before this chunk is
+    // shaded, so at the kernel's 4 waves per SIMD their latency hides behind the f64 math
+    const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    const bool lit = sc.n_lights > 0;
+    uint32_t rc = wave_slot(b, n);
+    size_t at = 0;
+    ShadeIn cur{};
+    bool have = false;
+    if (static_cast<uint64_t>(rc) * 64u + lane < n) {
+        at = rk + region_entry(s_scan, M, b.R, rc * 64u + lane);
+        cur = shade_load(b, at, lit);
+        have = true;
+    }
+    for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
+        const uint64_t jn = static_cast<uint64_t>(rc + W) * 64u + lane;
+        size_t at_n = 0;
+        ShadeIn nxt{};
+        const bool have_n = jn < n;
+        if (have_n) {
+            at_n = rk + region_entry(s_scan, M, b.R, static_cast<uint32_t>(jn));
+            nxt = shade_load(b, at_n, lit);
+        }
+        if (have) shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, cur);
+        cur = nxt;
+        at = at_n;
+        have = have_n;
     }
 }
 

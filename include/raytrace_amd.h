@@ -301,7 +301,8 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * clusters; 0 off, -1 auto), cam (generation 0: 0 per ray, 1 / 2 camera tiles over the
  * camera view of the tree in LDS / through L2, 3 the camera's view grid), cam_grid_res
  * (the view grid's cells per face side, 0 from the scene's frame size, -1 none;
- * at the next rt_scene_upload).
+ * at the next rt_scene_upload), a_queue (1: the nearest-hit chain's stream gets a
+ * hardware queue of its own).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

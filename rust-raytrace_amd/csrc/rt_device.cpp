@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -90,6 +90,8 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // wave-cooperative query (nearest_wave); 0 off, -1 auto
     {"cam_grid_res", 0, -1, 4096},               // the camera's view grid: cells per face side (0: from the scene's
                                                  // frame size, -1: no grid); takes effect at the next rt_scene_upload
+    {"a_queue", 0, 0, 1},                        // 1: the nearest-hit chain's stream CU-masked (a hardware queue of its
+                                                 // own, so another context's frame is never queued behind it)
 };
 
 }  // namespace
@@ -396,9 +398,13 @@ int ensure_lanes(rt_ctx* c, int n) {
         rt_ctx::Lane& M = c->lanes.back();
         // prio: the nearest-hit chain (the critical path) on a high-priority stream
         int lo = 0, hi = 0;
+        std::vector<uint32_t> all((c->n_cu + 31) / 32, 0u);
+        for (int cu = 0; cu < c->n_cu; ++cu) all[cu / 32] |= 1u << (cu % 32);
         if (c->t(kTunePrio) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
             HIP_TRY(c, hipStreamCreateWithPriority(&M.s, hipStreamNonBlocking, hi));
-        } else {
+        } else if (c->t(kTuneAQueue) == 0 ||
+                   hipExtStreamCreateWithCUMask(&M.s, static_cast<uint32_t>(all.size()), all.data()) != hipSuccess) {
+            (void)hipGetLastError();
             HIP_TRY(c, hipStreamCreateWithFlags(&M.s, hipStreamNonBlocking));
         }
         HIP_TRY(c, hipEventCreateWithFlags(&M.mark, hipEventDisableTiming));
@@ -1480,7 +1486,7 @@ int rt_ctx_set_tuning(rt_ctx* c, const char* key, int64_t value) {
             return fail(c, RT_E_INVALID, std::string("tuning ") + key + " out of range");
         // cu_mask and prio shape the lanes' streams, which are created once: rebuild
         // the lanes (after their work is done) so the next render uses the new value
-        if ((i == kTuneCuMask || i == kTunePrio) && value != c->tune[i] && !c->lanes.empty()) {
+        if ((i == kTuneCuMask || i == kTunePrio || i == kTuneAQueue) && value != c->tune[i] && !c->lanes.empty()) {
             if (hipSetDevice(c->device) != hipSuccess) return fail(c, RT_E_HIP, "hipSetDevice failed");
             if (c->render_pending) (void)hipEventSynchronize(c->render_done);
             drop_lanes(c);

@@ -1252,14 +1252,33 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
     for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
     region_scan(b.rs(), b.G, s_scan, s_wave);             // generation 0's records = the chains (also publishes s_srgb)
     const uint32_t n = s_scan[b.G];
-    RT_FOR_CHUNKS(b, n, j) {
-        if (j >= n) continue;
-        const uint32_t c = static_cast<uint32_t>(region_entry(s_scan, b.G, b.R, j));
-        const uint32_t nlev = b.nlev()[c];
-        if (nlev < lo || nlev > hi) continue;               // (kNlevRunning: not ended yet)
-        const uint32_t p = b.cpix()[c];
-        const Col res = average_samples(fold_pixel<kFresnel>(sc, b, c, static_cast<uint8_t>(nlev)), fp.spp);
-        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+    // software pipelined: the next chunk's chain header (level count, pixel, terminal) is
+    // loaded before this chain's levels are folded, one dependent round trip less per chain
+    const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    struct Head {
+        uint32_t c, nlev, p;
+        Col term;
+    };
+    auto head = [&](uint64_t j) {
+        Head hd{0u, kNlevRunning, 0u, Col{0.0, 0.0, 0.0}};
+        if (j < n) {
+            hd.c = static_cast<uint32_t>(region_entry(s_scan, b.G, b.R, static_cast<uint32_t>(j)));
+            hd.nlev = b.nlev()[hd.c];
+            hd.p = b.cpix()[hd.c];
+            hd.term = Col{ldn_if<kNtFold>(&b.term(0)[hd.c]), ldn_if<kNtFold>(&b.term(1)[hd.c]),
+                          ldn_if<kNtFold>(&b.term(2)[hd.c])};
+        }
+        return hd;
+    };
+    uint32_t rc = wave_slot(b, n);
+    Head cur = head(static_cast<uint64_t>(rc) * 64u + lane);
+    for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
+        const Head nxt = head(static_cast<uint64_t>(rc + W) * 64u + lane);
+        if (cur.nlev >= lo && cur.nlev <= hi) {             // (kNlevRunning: not ended yet, or no chain)
+            const Col res = average_samples(fold_levels<kFresnel>(sc, b, cur.c, static_cast<int>(cur.nlev), cur.term), fp.spp);
+            write_pixel(fp, cur.p % fp.tile_w, fp.row0 + cur.p / fp.tile_w, res, s_srgb);
+        }
+        cur = nxt;
     }
 }
 

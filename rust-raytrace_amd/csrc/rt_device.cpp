@@ -319,6 +319,9 @@ static_assert(kLightArea == RT_LIGHT_AREA, "DevLight::kind mirrors rt_light_kind
 // LDS per traversal workgroup for staged scene data (1024 threads, two resident per CU)
 constexpr size_t kLdsBudget = 72 * 1024;
 constexpr uint64_t kWfBudget = 80ull << 30;     // default wavefront working set per lane (of 288 GB HBM)
+// device memory a working set must leave free: the runtime's per-queue scratch
+// (up to 32 waves x 256 CUs x 64 lanes x ~600 B per queue, for several queues)
+constexpr size_t kRuntimeHeadroom = 4ull << 30;
 
 // The b streams need hardware queues of their own: HIP deals streams over a
 // few shared queues (GPU_MAX_HW_QUEUES), and two streams on one queue run
@@ -454,6 +457,16 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         }
         L.mem = nullptr;
         L.bytes = 0;
+        // ask only for what the device has free, less the runtime's scratch headroom: a request
+        // beyond it is answered without hipMalloc (the runtime has crashed inside a failing
+        // hipMalloc of a few hundred GB, seen with an explicit oversized wf_budget_mb), and a
+        // working set that took the last free bytes would leave nothing for the scratch the
+        // runtime allocates per hardware queue at a kernel's first launch there
+        size_t fr = 0, total = 0;
+        if (hipMemGetInfo(&fr, &total) == hipSuccess && (off > fr || fr - off < kRuntimeHeadroom))
+            return fail(c, RT_E_NOMEM, "wavefront working set of " + std::to_string(off >> 20) + " MB does not fit (" +
+                                           std::to_string(fr >> 20) + " MB free)");
+        (void)hipGetLastError();
         const hipError_t e = hipMalloc(&L.mem, off);
         if (e == hipErrorOutOfMemory) {          // the caller retries with smaller chunks
             (void)hipGetLastError();
@@ -1170,6 +1183,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // misses tests every cluster box it crosses, 60-78 vs 43 us per launch)
         const uint32_t wave_max = src != 9 || c->dsc.cl_slots == 0 ? 0u
                                   : wave_t >= 0 ? static_cast<uint32_t>(wave_t) : 0u;
+        if (wave_max == 0) c->dsc.cl_slots = 0;         // (the clusters are staged only for that query)
         for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tail_from = tail_from;
             c->lanes[l].b.tail_max = tail_max;

@@ -89,19 +89,60 @@ __device__ __forceinline__ uint8_t to_srgb(double v, const double* table) {
 
 __device__ __forceinline__ uint8_t to_srgb(double v) { return to_srgb(v, c_srgb_avg); }
 
+// The per-ray constants of shapes.rs:60-89's quadratic: a2 = 2.0*a and
+// a4 = 4.0*a (the same f64 products the reference forms per test) and the
+// reciprocal of a2 refined exactly as gfx950's f64 division refines its
+// denominator (v_rcp_f64, then two Newton steps r += r*(1 - a2*r)).  `win` is
+// the exponent window of numerators div_a2 may finish with that hoisted
+// reciprocal (0: none, the ray's a2 is outside [2^-100, 2^101)).
+struct SphK {
+    double a2, a4, ra2;
+    uint32_t win;
+};
+
+__device__ __forceinline__ SphK sphere_k(double a) {
+    SphK k;
+    k.a2 = 2.0 * a;
+    k.a4 = 4.0 * a;
+    double r = __builtin_amdgcn_rcp(k.a2);
+    double e = fma(-k.a2, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-k.a2, r, 1.0);
+    k.ra2 = fma(r, e, r);
+    const uint32_t ea = (static_cast<uint32_t>(__double2hiint(k.a2)) >> 20) & 0x7FFu;
+    k.win = ea - 923u < 201u ? 1500u : 0u;
+    return k;
+}
+
+// x / a2, correctly rounded.  The compiler's f64 division is v_div_scale (of
+// numerator and denominator), that reciprocal, q0 = x*r, e = fma(-a2, q0, x),
+// v_div_fmas = fma(e, r, q0), v_div_fixup.  With a2 in [2^-100, 2^101) and
+// |x| in [2^-900, 2^600) (biased exponent 123..1622) div_scale scales neither
+// operand (exponent gap < 768, no denormal quotient or reciprocal, x not tiny)
+// and div_fixup returns q with sign(x), so the three operations below give the
+// division's bits; any other x (0, denormal, huge, inf, NaN) takes the division.
+__device__ __forceinline__ double div_a2(double x, const SphK& k) {
+    const uint32_t ex = (static_cast<uint32_t>(__double2hiint(x)) >> 20) & 0x7FFu;
+    if (ex - 123u < k.win) {
+        const double q0 = x * k.ra2;
+        const double e = fma(-k.a2, q0, x);
+        return fma(e, k.ra2, q0);
+    }
+    return x / k.a2;
+}
+
 // shapes.rs:60-89: the exact quadratic; true + the t the reference returns, or
-// false for None.  `a2` = 2.0*a, `a4` = 4.0*a are hoisted per ray (the same
-// f64 products the reference forms per test).
-__device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, double a2, double a4, double& t) {
+// false for None.
+__device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, const SphK& k, double& t) {
     const double ocx = r.ox - s.cx, ocy = r.oy - s.cy, ocz = r.oz - s.cz;
     const double b = 2.0 * (r.dx * ocx + r.dy * ocy + r.dz * ocz);
     const double cc = (ocx * ocx + ocy * ocy + ocz * ocz) - s.rr;
-    const double disc = b * b - a4 * cc;
+    const double disc = b * b - k.a4 * cc;
     if (disc > 0.0) {
         const double sq = sqrt(disc);
-        const double t1 = (-b - sq) / a2;
+        const double t1 = div_a2(-b - sq, k);
         if (t1 > 0.0) { t = t1; return true; }
-        const double t2 = (-b + sq) / a2;
+        const double t2 = div_a2(-b + sq, k);
         if (t2 > 0.0) { t = t2; return true; }
     }
     return false;
@@ -161,14 +202,14 @@ __device__ __forceinline__ Hit nearest_brute(const DevScene& sc, SpherePtr S, co
     }
     if (h.nan_t) return h;      // no sphere can produce a NaN t
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;     // direction.sqnorm()
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const int n = sc.n_spheres;
     if constexpr (kCount) w->spheres += n;
 #pragma unroll 2
     for (int i = 0; i < n; ++i) {
         const DevSphere s = S[i];
         double t;
-        if (sphere_t(s, r, a2, a4, t)) {
+        if (sphere_t(s, r, sk, t)) {
             const int32_t obj = sc.sphere_obj[i];
             if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = i; }
         }
@@ -196,13 +237,13 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
     }
     if (plane_block) return true;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const int n = sc.n_spheres;
     for (int i = 0; i < n; ++i) {
         const DevSphere s = S[i];
         double t;
         if constexpr (kCount) ++w->spheres;
-        if (sphere_t(s, r, a2, a4, t)) {
+        if (sphere_t(s, r, sk, t)) {
             if (!has_range || t * t < r2) return true;
         }
     }
@@ -491,7 +532,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     RT_STACK_DECL(kReg, uint64_t);
@@ -516,7 +557,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                if (sphere_t(v.sph[k], r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
@@ -548,7 +589,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
@@ -622,7 +663,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             for (int k = first; k < first + cnt; ++k) {
                 RT_WSTEP(1);
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                if (sphere_t(v.sph[k], r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
@@ -661,11 +702,11 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     if (plane_block) return true;
     if (sc.n_spheres == 0) return false;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     if (hint >= 0) {                     // see occluded_bvh4
         if constexpr (kCount) ++w->spheres;
         double t;
-        if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+        if (sphere_t(v.sph[hint], r, sk, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
@@ -692,7 +733,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+                if (sphere_t(v.sph[k], r, sk, t) && (!has_range || t * t < r2)) return true;
             }
         }
         if (stk_n == 0) return false;
@@ -721,7 +762,7 @@ __device__ __forceinline__ int shadow_prefilter(const DevScene& sc, const DevSph
     if (hint >= 0) {
         const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
         double t;
-        if (sphere_t(S[hint], r, 2.0 * a, 4.0 * a, t) && (!has_range || t * t < r2)) return 1;
+        if (sphere_t(S[hint], r, sphere_k(a), t) && (!has_range || t * t < r2)) return 1;
     }
     return 2;
 }
@@ -831,7 +872,7 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     RT_STACK_DECL(0, uint64_t);
@@ -853,7 +894,7 @@ __device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                if (sphere_t(v.sph[k], r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
@@ -903,7 +944,7 @@ __device__ __forceinline__ Hit nearest_quad(const DevScene& sc, const BvhView& v
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     const int32_t q = static_cast<int32_t>(threadIdx.x & 3u);
@@ -947,7 +988,7 @@ __device__ __forceinline__ Hit nearest_quad(const DevScene& sc, const BvhView& v
             for (int k = first + q; k < first + cnt; k += 4) {
                 if constexpr (kCount) ++w->spheres;
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t)) {
+                if (sphere_t(v.sph[k], r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < lt || (t == lt && obj < lo)) { lt = t; lo = obj; lp = k; }
                 }
@@ -1049,7 +1090,7 @@ __device__ __forceinline__ Hit nearest_wave(const DevScene& sc, const BvhView& v
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     const int lane = static_cast<int>(threadIdx.x & 63u);
@@ -1097,7 +1138,7 @@ __device__ __forceinline__ Hit nearest_wave(const DevScene& sc, const BvhView& v
             const int k = (mine >> 5) + i;
             if constexpr (kCount) ++w->spheres;
             double t;
-            if (sphere_t(v.sph[k], r, a2, a4, t)) {
+            if (sphere_t(v.sph[k], r, sk, t)) {
                 const int32_t obj = v.obj[k];
                 if (wb_better(t, obj, best)) { best.t = t; best.obj = obj; best.prim = k; }
             }
@@ -1131,11 +1172,11 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
     if (plane_block) return true;
     if (sc.n_spheres == 0) return false;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     if (hint >= 0) {
         if constexpr (kCount) ++w->spheres;
         double t;
-        if (sphere_t(v.sph[hint], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+        if (sphere_t(v.sph[hint], r, sk, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
 #if RT_SEL4
@@ -1174,7 +1215,7 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
                 double t;
-                if (sphere_t(v.sph[k], r, a2, a4, t) && (!has_range || t * t < r2)) return true;
+                if (sphere_t(v.sph[k], r, sk, t) && (!has_range || t * t < r2)) return true;
             }
         }
         if (stk_n == 0) return false;
@@ -1205,11 +1246,11 @@ __device__ __forceinline__ bool occluded_lgrid(const DevScene& sc, const BvhView
     if (plane_block) return true;
     if (sc.n_spheres == 0) return false;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     auto blocks = [&](int32_t k) {
         if constexpr (kCount) ++w->spheres;
         double t;
-        return sphere_t(v.sph[k], r, a2, a4, t) && t * t < r2;
+        return sphere_t(v.sph[k], r, sk, t) && t * t < r2;
     };
     if (hint >= 0 && blocks(hint)) return true;
     for (uint32_t e = g.always_begin; e < g.always_end; ++e)
@@ -1261,13 +1302,13 @@ __device__ __forceinline__ Hit nearest_cgrid(const DevScene& sc, const BvhView& 
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     const DevLightGrid& g = *sc.cgrid;
     float lim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
     auto test = [&](int32_t k) {
         if constexpr (kCount) ++w->spheres;
         double t;
-        if (sphere_t(v.sph[k], r, a2, a4, t)) {
+        if (sphere_t(v.sph[k], r, sk, t)) {
             const int32_t obj = v.obj[k];
             if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = k; lim = t_limit(t); }
         }
@@ -1320,7 +1361,7 @@ __device__ __forceinline__ Hit nearest_camera(const DevScene& sc, const BvhView&
     const bool go = act && !h.nan_t;
     if (sc.n_spheres == 0 || __ballot(go) == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const double a2 = 2.0 * a, a4 = 4.0 * a;
+    const SphK sk = sphere_k(a);
     int32_t* stk = v.stk;
     int sp = 0;
     int32_t cur = sc.bvh_root;
@@ -1348,7 +1389,7 @@ __device__ __forceinline__ Hit nearest_camera(const DevScene& sc, const BvhView&
             for (int k = first; k < first + cnt; ++k) {
                 const DevSphere s = v.sph[k];
                 double t;
-                if (go && sphere_t(s, r, a2, a4, t)) {
+                if (go && sphere_t(s, r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = k; }
                 }

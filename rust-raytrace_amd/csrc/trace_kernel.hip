@@ -370,6 +370,10 @@ constexpr int kSrcGridG = 15;
 // spheres staged in LDS (22) or read through L2 (23).
 constexpr int kSrcCamGridL = 22;
 constexpr int kSrcCamGridG = 23;
+// kSrcBvhL8C whose launches also run the wave-cooperative query (nearest_wave) for
+// queues of <= WfBufs::wave_max rays; its own instantiation, so that the default
+// src-9 kernel carries neither that code's registers nor the clusters' LDS
+constexpr int kSrcBvhL8W = 24;
 
 template <int kSrc>
 struct Src {
@@ -378,13 +382,14 @@ struct Src {
     static constexpr bool cgrid = kSrc == kSrcCamGridL || kSrc == kSrcCamGridG;
     static constexpr bool bvh = kSrc >= kSrcBvhG && !grid && !cgrid;
     static constexpr bool quad = kSrc == kSrcBvh4Q;
+    static constexpr bool waveq = kSrc == kSrcBvhL8W;
     static constexpr bool wide = (kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P) || quad;
     static constexpr bool half = kSrc == kSrcBvhPH || kSrc == kSrcBvhPHC;
-    static constexpr int compact_bits = kSrc == kSrcBvhL8C ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
+    static constexpr int compact_bits = kSrc == kSrcBvhL8C || waveq ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
     static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P || half;
-    static constexpr bool compact = kSrc == kSrcBvhL8C;
+    static constexpr bool compact = kSrc == kSrcBvhL8C || waveq;
     static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
-                                    kSrc == kSrcCamL || quad;
+                                    kSrc == kSrcCamL || quad || waveq;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL || kSrc == kSrcCamGridL;
     static constexpr int nodes = all_lds ? 2 : half ? 3 : prefix ? 1 : 0;
     static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 && !quad) || half ? 8 : 4;   // min waves per SIMD
@@ -426,7 +431,7 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     bytes = (bytes + 15) / 16 * 16;
     if (Src<kSrc>::quad) bytes += static_cast<size_t>(kQuadStack) * kQuadStride * sizeof(uint32_t);
-    if (kSrc == kSrcBvhL8C && sc.cl_slots > 0)           // the wave-cooperative query's clusters and orders
+    if (Src<kSrc>::waveq && sc.cl_slots > 0)             // the wave-cooperative query's clusters and orders
         bytes += cluster_lds_bytes(sc);
     return bytes;
 }
@@ -509,7 +514,7 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
             const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
             v.lstk = reinterpret_cast<uint32_t*>(lds + at) + (threadIdx.x >> 2);
         }
-        if constexpr (kSrc == kSrcBvhL8C) {              // the clusters after the spheres (wave-cooperative query)
+        if constexpr (Src<kSrc>::waveq) {                // the clusters after the spheres (wave-cooperative query)
             if (wave && sc.cl_slots > 0) {
                 const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
                 DevCluster* lc = reinterpret_cast<DevCluster*>(lds + at);
@@ -783,7 +788,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
     // queues of <= wave_max rays (generations >= 1 of a src-9 tree with clusters): the
     // regular kernel runs the wave-cooperative query, `width` rays per wave one after another,
     // width = ceil(n / waves) so that every wave takes at most one chunk
-    const bool wv = kSrc == kSrcBvhL8C && !kCam && k >= 1 && b.wave_max > 0 && n <= b.wave_max;
+    const bool wv = Src<kSrc>::waveq && !kCam && k >= 1 && b.wave_max > 0 && n <= b.wave_max;
     // tail generations: the quad kernel takes queues of <= tail_max rays (and above wave_max
     // when the wave query is on), the regular one the rest (both are launched; the other
     // returns at once)
@@ -843,7 +848,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             tile_rect(fp, b, j >> 6, tx0, ty0, tx1, ty1);
             h = nearest_camera<kCount>(sc, v, r, live, tx0, ty0, tx1, ty1, &w);
         }
-        if constexpr (kSrc == kSrcBvhL8C) {
+        if constexpr (Src<kSrc>::waveq) {
             if (wv) {                                    // workgroup-uniform: every lane on one ray at a time
                 for (uint32_t i = 0; i < width; ++i) {
                     if (!__builtin_amdgcn_readlane(live ? 1 : 0, static_cast<int>(i))) continue;
@@ -1380,6 +1385,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     // does not fit a workgroup (160 KB) the regular kernel alone takes every queue
     const bool quad = kSrcN == kSrcBvhL8C && b.tail_from > 0 && k >= b.tail_from && k >= 1 && sc.bvh4 != nullptr &&
                       staged_bytes<kSrcBvh4Q>(sc) + queue_lds_bytes(b.G) <= 160u * 1024u;
+    // src 9 with the wave-cooperative query on: its own instantiation (kSrcBvhL8W)
+    const bool waveq = kSrcN == kSrcBvhL8C && b.wave_max > 0 && sc.cl_slots > 0;
     WfBufs bn = b;
     if (!quad) bn.tail_from = 0;
     if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
@@ -1400,10 +1407,12 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
         if (sc.has_fresnel) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, true, false);
     } else if (lists) {
         if (quad) { if (sc.has_fresnel) RT_NEARL(kSrcBvh4Q, true); else RT_NEARL(kSrcBvh4Q, false); }
-        if (sc.has_fresnel) RT_NEARL(kSrcN, true); else RT_NEARL(kSrcN, false);
+        if (waveq) { if (sc.has_fresnel) RT_NEARL(kSrcBvhL8W, true); else RT_NEARL(kSrcBvhL8W, false); }
+        else if (sc.has_fresnel) RT_NEARL(kSrcN, true); else RT_NEARL(kSrcN, false);
     } else {
         if (quad) { if (sc.has_fresnel) RT_NEAR(kSrcBvh4Q, false, true); else RT_NEAR(kSrcBvh4Q, false, false); }
-        if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
+        if (waveq) { if (sc.has_fresnel) RT_NEAR(kSrcBvhL8W, false, true); else RT_NEAR(kSrcBvhL8W, false, false); }
+        else if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
     }
 #undef RT_NEARC
 #undef RT_NEARL

@@ -41,3 +41,15 @@ def gpu_ctx():
     ctx = lr.Context(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(autouse=True)
+def _native_fault_trace():
+    """RT_SEGV_BT=1: print the native stack of a SIGSEGV / SIGBUS (tools/segv_bt.c;
+    diagnostic).  Installed before every test, after pytest's faulthandler and after
+    whatever the HIP runtime installs when it starts."""
+    if os.environ.get("RT_SEGV_BT") == "1":
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libsegv_bt.so"))
+        assert lib.segv_bt_install() == 0
+    yield

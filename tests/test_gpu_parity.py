@@ -623,8 +623,10 @@ def test_working_set_budget_splits_chunks_bit_identically(gpu_ctx):
 
 def test_oversized_budget_falls_back_to_smaller_chunks():
     """A budget beyond the device's 288 GB (the whole 16384^2 depth-16 tile in
-    one chunk needs ~0.5 TB): hipMalloc fails, the render halves its chunks
-    until the working set fits, and the image equals the default schedule's.
+    one chunk needs ~0.5 TB): the working set does not fit the free device
+    memory (checked before hipMalloc, which has crashed inside the runtime on
+    requests that size), the render halves its chunks until it fits, and the
+    image equals the default schedule's.
     Own context, closed at the end (its working set is large)."""
     spec = scenes.random_spheres(40, 16384, 16384, 16, seed=11, name="sparse")
     o = lr.render_opts(16384, 16384, max_depth=16, spp=1, algo=lr.RT_ALGO_WAVEFRONT)

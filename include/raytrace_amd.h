@@ -271,7 +271,8 @@ enum rt_kernel_family {
     RT_KF_TALLY = 4,        /* wf_tally */
     RT_KF_CAMERA = 5,       /* wf_nearest, generation 0 (camera rays) */
     RT_KF_SHADOW = 6,       /* wf_shadow: the shadow item lists of a generation */
-    RT_KF_COUNT = 7
+    RT_KF_TAIL = 7,         /* wf_tail: the fused generations >= tail_fuse */
+    RT_KF_COUNT = 8
 };
 int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 
@@ -302,7 +303,11 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * camera view of the tree in LDS / through L2, 3 the camera's view grid), cam_grid_res
  * (the view grid's cells per face side, 0 from the scene's frame size, -1 none;
  * at the next rt_scene_upload), a_queue (1: the nearest-hit chain's stream gets a
- * hardware queue of its own).
+ * hardware queue of its own), tail_fuse (T > 0: generations >= T of a frame on
+ * the src-9 tree whose lights all have light-view grids run as one launch, one
+ * chain per work-item through its remaining bounces; 0 off, -1 auto), tail_shade
+ * (that launch also shades the records of this many generations before T),
+ * tail_width (its chains per wave; 0 spreads them over every wave).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -11,7 +11,7 @@ namespace rtamd {
 
 // Kernel families of the wavefront schedule (rt_ctx_kernel_times indices).
 enum KernelFamily : int8_t {
-    kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCamera = 5, kKfShadow = 6, kKfCount = 7
+    kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCamera = 5, kKfShadow = 6, kKfTail = 7, kKfCount = 8
 };
 
 // Per-launch timing (RT_TIME_KERNELS): begin() records a start event before a
@@ -88,6 +88,10 @@ struct WfStreams {
     int bmerge;           // > 0: generations >= bmerge get no shadow / shading launches of their own;
                           //   one occlusion + one shading launch over all their records follow the
                           //   last nearest-hit launch on stream a (the latency-bound tail)
+    int tail_fuse;        // > 0: generations >= tail_fuse run as one wf_tail launch on stream a
+    int tail_wgs;         //   (that many workgroups, all resident: one per CU), which also shades the
+    int tail_shade;       //   records of generations tail_fuse - tail_shade .. tail_fuse - 1;
+    int tail_width;       //   chains per wave (0: spread over every wave)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -1151,6 +1151,131 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     }
 }
 
+// One chain of the fused tail from generation k on: what wf_nearest
+// (finish_nearest), wf_occlusion (light-view grids) and wf_shade do to it, one
+// generation after the other in registers -- the same operations on the same
+// operands, so the levels and the terminal it writes are the per-generation
+// kernels' bits.  cnt[0][k] / cnt[1][k]: this workgroup's shade records of
+// generation k / rays queued for generation k (for wf_tally).
+template <bool kFresnel, bool kCount>
+__device__ __forceinline__ void tail_chain(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const BvhView& v,
+                                           int k, Ray r, double sig, uint32_t c, uint32_t (*cnt)[kMaxGenerations],
+                                           Work& wn, Work& wsh) {
+    for (;; ++k) {
+        const Hit h = nearest_any<kSrcBvhL8C, kCount>(sc, v, r, &wn);
+        if (h.obj == INT32_MAX) {                                         // raytrace.rs:265, 228-232
+            set_terminal(b, c, end_colour(sc, INT32_MAX), k);
+            return;
+        }
+        const DevMaterial& m = sc.mats[h.obj];
+        if (static_cast<uint32_t>(k) > fp.max_depth) {                    // raytrace.rs:33
+            set_terminal(b, c, end_colour(sc, h.obj), k);
+            return;
+        }
+        const double ptx = r.ox + r.dx * h.t, pty = r.oy + r.dy * h.t, ptz = r.oz + r.dz * h.t;   // ray.cast(t)
+        double nx, ny, nz;
+        hit_normal(sc, v.sph, h.prim, ptx, pty, ptz, nx, ny, nz);
+        const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
+        const Shading sh = shading_flags<kFresnel>(m, sig, nd);
+        if (!sh.diffuse && !sh.specular) {
+            set_terminal(b, c, end_colour(sc, h.obj), k);
+            return;
+        }
+        atomicAdd(&cnt[0][k], 1u);
+        uint32_t mask = 0;                                                // raytrace.rs:39-49
+        for (int l = 0; l < sc.n_lights; ++l) {
+            double lx, ly, lz, r2;
+            (void)light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+            const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+            if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, h.prim, &wsh)) mask |= 1u << l;
+        }
+        const ShadeIn in{ptx, pty, ptz, r.dx, r.dy, r.dz, sig, h.obj, h.prim, c, mask};
+        shade_compute<kFresnel>(sc, b, k, 0, in);                         // the level, or the terminal
+        if (!sh.specular) return;
+        if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }                   // raytrace.rs:58-64
+        const double nsig = (sh.f * sig) * m.ks_sig;
+        r = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
+        sig = nsig;
+        atomicAdd(&cnt[1][k + 1], 1u);
+    }
+}
+
+// The fused tail (WfStreams::tail_fuse = T): generations T .. max_depth + 1 of
+// a chunk in one launch, one chain per work-item (tail_chain), instead of a
+// nearest-hit launch per generation with its shadow and shading launches on
+// the B streams; it also answers the shadows and shading of the records of
+// generations T-D .. T-1 (WfStreams::tail_shade = D), so that no B-stream
+// launch competes with it for the CUs.  For small
+// chunks (one rank's share of a frame), whose late generations are a chain of
+// latency-bound launches: the tail then lasts about as long as the slowest
+// chain's remaining bounces, not the sum over generations of each generation's
+// slowest walk plus a launch each.  Needs the src-9 tree (whole tree + spheres
+// in LDS) and a light-view grid for every light.  gridDim.x workgroups, all
+// resident; workgroup w publishes its counts in region w and zeros in the
+// other regions r = w (mod gridDim.x) of every generation >= T.
+template <bool kFresnel, bool kCount>
+__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int D, int W) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t s_cnt[2][kMaxGenerations];
+    __shared__ uint32_t s_rec[kMaxScan + 1];
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrcBvhL8C>(sc), b.G);
+    for (int i = threadIdx.x; i < 2 * kMaxGenerations; i += kWfThreads) (&s_cnt[0][0])[i] = 0u;
+    region_scan(b.rq() + T * b.G, b.G, ql.scan, ql.wave);      // the chains (Q_T); ends with a barrier
+    // the shade records of generations T-D .. T-1 (consecutive in rs: one scan over D*G regions)
+    const uint32_t M = static_cast<uint32_t>(D) * b.G;
+    if (D > 0) region_scan(b.rs() + (T - D) * b.G, M, s_rec, ql.wave);
+    const uint32_t nch = ql.scan[b.G];
+    const int gens = static_cast<int>(fp.max_depth) + 2;
+    const uint32_t nrec = D > 0 ? s_rec[M] : 0u, nw = gridDim.x * (kWfThreads / 64);
+    const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    // the chains in contiguous runs of cw per wave from the first wave slot up, the records 64
+    // per wave from the last slot down, so that chain waves and record waves are mostly
+    // apart; cw (tuning tail_width; auto: spread over about half of the waves) trades the
+    // slowest chain of a wave against the lanes its finished chains leave idle: 48 per wave
+    // beat 16 / 24 / 32 / 64 on one rank's share of an 8-way C3 frame.  Contiguous runs keep
+    // the queue / record loads and the level / terminal stores coalesced.
+    const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * nch + nw - 1) / nw));
+    const uint32_t rslot = nw - 1u - slot;
+    Work wn, wsh;
+    {                                                          // (every workgroup stages: one per CU)
+        const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
+        __syncthreads();
+        for (uint64_t base = static_cast<uint64_t>(slot) * cw; base < nch; base += static_cast<uint64_t>(nw) * cw) {
+            const uint64_t j = base + lane;
+            if (lane >= cw || j >= nch) continue;
+            const size_t at = region_entry(ql.scan, b.G, b.R, static_cast<uint32_t>(j));
+            const Ray r = load_ray(b, T & 1, at);
+            const double sig = ldn_if<kNtQ>(&b.qf(T & 1, 6)[at]);
+            const uint32_t c = ldn_if<kNtQ>(&b.qpix(T & 1)[at]);
+            tail_chain<kFresnel, kCount>(sc, fp, b, v, T, r, sig, c, s_cnt, wn, wsh);       // its remaining bounces
+        }
+        for (uint64_t base = static_cast<uint64_t>(rslot) * 64u; base < nrec; base += static_cast<uint64_t>(nw) * 64u) {
+            const uint64_t j = base + lane;                    // a record of T-D .. T-1: its shadows and shading
+            if (j >= nrec) continue;
+            const size_t at = static_cast<size_t>(T - D) * b.qcap + region_entry(s_rec, M, b.R, static_cast<uint32_t>(j));
+            ShadeIn in = shade_load(b, at, false);
+            for (int l = 0; l < sc.n_lights; ++l) {
+                double lx, ly, lz, r2;
+                (void)light_dir(sc.lights[l], in.ptx, in.pty, in.ptz, lx, ly, lz, r2);
+                const Ray sray{in.ptx + lx * kEps, in.pty + ly * kEps, in.ptz + lz * kEps, lx, ly, lz};
+                if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, in.ptx, in.pty, in.ptz, in.prim, &wsh))
+                    in.mask |= 1u << l;
+            }
+            shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, in);
+        }
+    }
+    __syncthreads();
+    for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
+        const bool own = rg == blockIdx.x;
+        for (int k = T + static_cast<int>(threadIdx.x); k < gens; k += kWfThreads) {
+            b.rs()[k * b.G + rg] = own ? s_cnt[0][k] : 0u;
+            b.rq()[(k + 1) * b.G + rg] = own ? s_cnt[1][k + 1] : 0u;
+        }
+    }
+    flush_work<kCount>(b, 2, wn);
+    flush_work<kCount>(b, 4, wsh);
+}
+
 // The fold factor of a level is the specular colour of its object times, for
 // FresnelMaterial, the level's Schlick factor (raytrace.rs:63 / 163).  The chain is folded inner-first exactly as the
 // recursion returns (acc = res_k + ks_k * acc); the loads of four levels are
@@ -1369,7 +1494,16 @@ template <int kSrcN, int kSrcO, bool kCount>
 hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws) {
     const dim3 grid(b.G), block(kWfThreads);
     const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
-    hipError_t e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
+    hipError_t e;
+    if (ws.tail_fuse > 0 && k >= ws.tail_fuse) {      // the fused tail: every generation >= T in one launch
+        if (k > ws.tail_fuse) return hipSuccess;
+        if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
+        const size_t lds_t = staged_bytes<kSrcBvhL8C>(sc) + queue_lds_bytes(b.G);
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_shade, ws.tail_width);
+        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_shade, ws.tail_width);
+        return ws.ma ? ws.ma->mark(ws.a, kKfTail) : hipGetLastError();
+    }
+    e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
 #define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR, false>), grid, block, \
                                                staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
@@ -1424,6 +1558,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (!shaded && !b.eager) return hipSuccess;
     // the merged tail: generations >= bmerge are shaded together after the last nearest-hit launch
     if (ws.bmerge > 0 && k >= ws.bmerge) return hipSuccess;
+    // the fused tail also shades the records of generations T-D .. T-1
+    if (ws.tail_fuse > 0 && k >= ws.tail_fuse - ws.tail_shade) return hipSuccess;
     // shadows and shading of generation k: on a b stream once nearest_k is done
     // (generations alternate over the b streams, so consecutive ones overlap too)
     const int bi = k % ws.nb;

@@ -317,6 +317,42 @@ def test_quad_tail_walk_matches_oracle(gpu_ctx, scene):
         check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
+@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan", "fresnel"])
+def test_fused_tail_matches_oracle(gpu_ctx, scene):
+    """The fused tail (tuning tail_fuse = T, trace_kernel.hip wf_tail): every
+    generation >= T of each chain -- nearest hit, light-view grid shadows,
+    Phong sum, reflection -- in one launch, one chain per work-item.  From
+    generation 1 (nearly the whole recursion) and from 4, on ties across
+    leaves, the deepest small tree, NaN planes, Fresnel levels and a C3
+    workload: bit for bit the oracle's image, and the same ray and shadow-ray
+    counts (the tail publishes every generation's queue and record counts).
+    The timed render checks that the tail really ran: one nearest-hit launch
+    for the generations >= T, and no shadow or shading launches of their own
+    for them or for generation T-1 (whose records the tail shades too,
+    tuning tail_shade = 1)."""
+    def fresnel():
+        s = scenes.config3(96, 72)
+        s.max_depth = 10
+        for i in range(0, len(s.objects), 3):
+            s.objects[i]["material"] = scenes.fresnel((0.3, 0.4, 0.5), (0.7, 0.7, 0.7), 30.0, (0.01, 0.01, 0.01), 1.5)
+        return s
+    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene, "config3": lambda: scenes.config3(160, 128),
+         "planes_nan": _nan_plane_scene, "fresnel": fresnel}[scene]()
+    # (the tail answers shadows through light-view grids only: directional lights become point lights far away)
+    s.lights = [l if l["kind"] == "point" else
+                {"kind": "point", "location": tuple(-40.0 * x for x in l["direction"]), "color": l["color"]} for l in s.lights]
+    for T in (1, 4):
+        with _with_tuning(gpu_ctx, tail_fuse=T, tail_shade=1):
+            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+            gpu_ctx.kernel_times()
+            gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
+                                          flags=lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS))
+            kt = gpu_ctx.kernel_times()
+        if T <= s.max_depth + 1:
+            assert kt["nearest"][1] == T - 1 and kt["tail"][1] == 1, (T, kt)     # generations 1 .. T-1, the tail
+            assert kt["occlusion"][1] + kt["shadow"][1] == T - 1, (T, kt)       # generations 0 .. T-2
+
+
 @pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "extreme", "planes_nan"])
 def test_wave_cooperative_query_matches_oracle(gpu_ctx, scene):
     """The wave-cooperative query (one ray per wave, clusters of <= 16 spheres
@@ -517,6 +553,11 @@ def test_kernel_times(gpu_ctx):
     spec = scenes.config3(64, 48)
     gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
     base = dict(max_depth=8, spp=1, algo=lr.RT_ALGO_WAVEFRONT)
+    with _with_tuning(gpu_ctx, tail_fuse=0):               # one launch set per generation (no fused tail)
+        _kernel_times_per_generation(gpu_ctx, base)
+
+
+def _kernel_times_per_generation(gpu_ctx, base):
     plain = gpu_ctx.render(lr.render_opts(64, 48, **base))
     gpu_ctx.kernel_times()
     timed = [gpu_ctx.render(lr.render_opts(64, 48, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS,
@@ -655,7 +696,9 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(fold_split=1), dict(fold_split=4), dict(fold_split=8), dict(fold_split=3, bstreams=1),
                dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3), dict(bmerge=1), dict(bmerge=3),
                dict(bmerge=5, tail_from=1, tail_max=1 << 30), dict(bmerge=2, regions=2048), dict(wave_max=0),
-               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4), dict(cam=3)]:
+               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4), dict(cam=3),
+               dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
+               dict(tail_fuse=4, tail_shade=0), dict(tail_fuse=6, tail_shade=5)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

@@ -303,11 +303,13 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * camera view of the tree in LDS / through L2, 3 the camera's view grid), cam_grid_res
  * (the view grid's cells per face side, 0 from the scene's frame size, -1 none;
  * at the next rt_scene_upload), a_queue (1: the nearest-hit chain's stream gets a
- * hardware queue of its own), tail_fuse (T > 0: generations >= T of a frame on
- * the src-9 tree whose lights all have light-view grids run as one launch, one
- * chain per work-item through its remaining bounces; 0 off, -1 auto), tail_shade
- * (that launch also shades the records of this many generations before T),
- * tail_width (its chains per wave; 0 spreads them over every wave).
+ * hardware queue of its own), tail_fuse (T >= 1: the chains still running at
+ * generation T-1 of a frame on the src-9 tree whose lights all have light-view
+ * grids finish in one launch, one chain per work-item through its remaining
+ * bounces; 0 off, -1 auto), tail_width (that launch's chains per wave, 0
+ * auto), tail_fold (1: it also folds its chains, after the shading streams),
+ * tail_shade (with tail_fold 0: it also shades the records of this many
+ * generations before T-1).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

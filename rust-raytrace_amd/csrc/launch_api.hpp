@@ -88,10 +88,11 @@ struct WfStreams {
     int bmerge;           // > 0: generations >= bmerge get no shadow / shading launches of their own;
                           //   one occlusion + one shading launch over all their records follow the
                           //   last nearest-hit launch on stream a (the latency-bound tail)
-    int tail_fuse;        // > 0: generations >= tail_fuse run as one wf_tail launch on stream a
-    int tail_wgs;         //   (that many workgroups, all resident: one per CU), which also shades the
-    int tail_shade;       //   records of generations tail_fuse - tail_shade .. tail_fuse - 1;
-    int tail_width;       //   chains per wave (0: spread over every wave)
+    int tail_fuse;        // > 0: the chains running at generation tail_fuse - 1 finish in one wf_tail
+    int tail_wgs;         //   launch on stream a (that many workgroups, all resident: one per CU;
+    int tail_width;       //   chains per wave, 0 auto)
+    int tail_fold;        //   1: it folds its chains (after the B streams), the others fold on b[0]
+    int tail_shade;       //   it also shades the records of generations T-1-tail_shade .. T-2 (tail_fold 0)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

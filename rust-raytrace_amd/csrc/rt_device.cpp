@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneTailFuse, kTuneTailShade, kTuneTailWidth, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneTailFold, kTuneTailShade, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,10 +92,12 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // frame size, -1: no grid); takes effect at the next rt_scene_upload
     {"a_queue", 0, 0, 1},                        // 1: the nearest-hit chain's stream CU-masked (a hardware queue of its
                                                  // own, so another context's frame is never queued behind it)
-    {"tail_fuse", -1, -1, 32},                    // > 0: generations >= tail_fuse of a src-9 frame whose lights all have
-                                                 // light-view grids run as one fused launch (wf_tail); 0 off, -1 auto
-    {"tail_shade", 1, 0, 8},                     // ... which also shades the records of the tail_shade generations before it
-    {"tail_width", 0, 0, 64},                    // ... with this many chains per wave (0: spread over every wave)
+    {"tail_fuse", -1, -1, 32},                   // > 0: the chains running at generation tail_fuse - 1 of a src-9 frame whose
+                                                 // lights all have light-view grids finish in one launch (wf_tail); 0 off, -1 auto
+    {"tail_width", 0, 0, 64},                    // ... with this many chains per wave (0: auto)
+    {"tail_fold", 1, 0, 1},                      // ... 1: which also folds them (after the shading streams)
+    {"tail_shade", 1, 0, 8},                     // ... which also shades the records of this many generations before
+                                                 // T-1 (tail_fold 0)
 };
 
 }  // namespace
@@ -1264,16 +1266,19 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             // fused tail (tuning tail_fuse = T): the src-9 tree, light-view grid shadows, the frame-end fold
             {
                 // auto: from generation 4 for chunks of <= 4.5 M pixel slots (one rank's share of a 4- or
-                // 8-way C3 frame: 1.140 -> 1.033 and 0.807 -> 0.747 ms), from 5 up to 9 M (a 2-way share:
-                // 1.725 -> 1.666 ms), off above (the whole C3 frame: 2.933 vs 2.921 ms with T = 7)
+                // 8-way C3 frame), from 5 up to 9 M (a 2-way share), off above (the whole C3 frame: 2.933
+                // vs 2.921 ms with T = 7); with the tail's own fold (tail_fold 1) on one box: 8-way share
+                // 0.855 -> 0.751 ms, 4-way 1.140 -> 1.040, 2-way 1.725 -> 1.642
                 const uint64_t S = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8);
                 int T = static_cast<int>(c->t(kTuneTailFuse));
                 if (T < 0) T = S <= 4500000u ? 4 : S <= 9000000u ? 5 : 0;
                 const bool ok = T >= 1 && static_cast<uint32_t>(T) <= o->max_depth + 1 && src == 9 && c->all_lights_gridded &&
                                 c->t(kTuneGridOcc) != 0 && !b.eager && ws.bmerge == 0 && c->t(kTuneFoldSplit) == 0;
                 ws.tail_fuse = ok ? T : 0;
-                ws.tail_shade = std::min<int>({T, static_cast<int>(c->t(kTuneTailShade)), static_cast<int>(kMaxScan / G)});
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
+                ws.tail_fold = static_cast<int>(c->t(kTuneTailFold));
+                ws.tail_shade = ws.tail_fold ? 0 : std::min<int>({T - 1, static_cast<int>(c->t(kTuneTailShade)),
+                                                                  static_cast<int>(kMaxScan / G)});
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;

@@ -927,8 +927,18 @@ __device__ __forceinline__ ShadeIn shade_load(const WfBufs& b, size_t at, bool m
     return in;
 }
 
-template <bool kFresnel>
-__device__ __forceinline__ void shade_compute(const DevScene& sc, const WfBufs& b, int k, size_t at, const ShadeIn& in) {
+// What a shading leaves for the fused tail: the local colour, whether the hit
+// reflects, its Schlick factor and the normal turned toward the ray.
+struct ShadeOut {
+    Col res;
+    bool specular;
+    double f, nx, ny, nz;
+};
+
+// kTerm = false (the fused tail): a non-specular hit's colour is returned for
+// the caller's in-register fold instead of being written as the chain's terminal.
+template <bool kFresnel, bool kTerm = true>
+__device__ __forceinline__ ShadeOut shade_compute(const DevScene& sc, const WfBufs& b, int k, size_t at, const ShadeIn& in) {
     const double ptx = in.ptx, pty = in.pty, ptz = in.ptz, dx = in.dx, dy = in.dy, dz = in.dz, sig = in.sig;
     const int32_t obj = in.obj;
     const uint32_t c = in.c, mask = in.mask;
@@ -952,12 +962,14 @@ __device__ __forceinline__ void shade_compute(const DevScene& sc, const WfBufs& 
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
         stn(&b.lobj()[st], obj);
         if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
+    } else if (!kTerm) {
     } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
         stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
         stn(&b.ru(2)[at], c | kChainEnd);
     } else {
         set_terminal(b, c, res, k);
     }
+    return ShadeOut{res, specular, sh.f, nx, ny, nz};
 }
 
 template <bool kFresnel>
@@ -1151,131 +1163,61 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     }
 }
 
-// One chain of the fused tail from generation k on: what wf_nearest
-// (finish_nearest), wf_occlusion (light-view grids) and wf_shade do to it, one
-// generation after the other in registers -- the same operations on the same
-// operands, so the levels and the terminal it writes are the per-generation
-// kernels' bits.  cnt[0][k] / cnt[1][k]: this workgroup's shade records of
-// generation k / rays queued for generation k (for wf_tally).
+// The shadow mask of a lit hit at (ptx, pty, ptz) on sphere `prim` through the
+// light-view grids (raytrace.rs:39-49; the host checked every light has one):
+// the operations of wf_occlusion's grid source.
+template <bool kCount>
+__device__ __forceinline__ uint32_t grid_shadow_mask(const DevScene& sc, const BvhView& v, double ptx, double pty,
+                                                     double ptz, int32_t prim, Work& wsh) {
+    uint32_t mask = 0;
+    for (int l = 0; l < sc.n_lights; ++l) {
+        double lx, ly, lz, r2;
+        (void)light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
+        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
+        if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, prim, &wsh)) mask |= 1u << l;
+    }
+    return mask;
+}
+
+// One chain of the fused tail from its shade record of generation T-1 on: the
+// record's shadows and shading (wf_occlusion + wf_shade), then generation by
+// generation what wf_nearest (finish_nearest), wf_occlusion and wf_shade do to
+// it, in registers -- the same operations on the same operands, so the levels
+// it writes are the per-generation kernels' bits.  Returns the chain's
+// terminal colour and sets nlev (the generation it ended in) instead of writing
+// them: the caller folds the chain right away.  cnt[0][k] / cnt[1][k]: this
+// workgroup's shade records of generation k / rays queued for generation k.
 template <bool kFresnel, bool kCount>
-__device__ __forceinline__ void tail_chain(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const BvhView& v,
-                                           int k, Ray r, double sig, uint32_t c, uint32_t (*cnt)[kMaxGenerations],
-                                           Work& wn, Work& wsh) {
-    for (;; ++k) {
+__device__ __forceinline__ Col tail_chain(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const BvhView& v,
+                                          int k, ShadeIn in, int& nlev, uint32_t (*cnt)[kMaxGenerations], Work& wn,
+                                          Work& wsh) {
+    const int k0 = k;
+    for (;;) {
+        in.mask = grid_shadow_mask<kCount>(sc, v, in.ptx, in.pty, in.ptz, in.prim, wsh);
+        const ShadeOut so = shade_compute<kFresnel, false>(sc, b, k, 0, in);     // level k if specular
+        if (!so.specular) { nlev = k; return so.res; }
+        const Ray r = reflect_ray(Ray{in.ptx, in.pty, in.ptz, in.dx, in.dy, in.dz}, in.ptx, in.pty, in.ptz, so.nx, so.ny,
+                                  so.nz);                                   // raytrace.rs:58-64
+        const double sig = (so.f * in.sig) * sc.mats[in.obj].ks_sig;
+        ++k;
+        if (k > k0 + 1) atomicAdd(&cnt[1][k], 1u);                         // (Q_T was counted by wf_nearest)
         const Hit h = nearest_any<kSrcBvhL8C, kCount>(sc, v, r, &wn);
-        if (h.obj == INT32_MAX) {                                         // raytrace.rs:265, 228-232
-            set_terminal(b, c, end_colour(sc, INT32_MAX), k);
-            return;
-        }
+        nlev = k;
+        if (h.obj == INT32_MAX) return end_colour(sc, INT32_MAX);          // raytrace.rs:265, 228-232
         const DevMaterial& m = sc.mats[h.obj];
-        if (static_cast<uint32_t>(k) > fp.max_depth) {                    // raytrace.rs:33
-            set_terminal(b, c, end_colour(sc, h.obj), k);
-            return;
-        }
-        const double ptx = r.ox + r.dx * h.t, pty = r.oy + r.dy * h.t, ptz = r.oz + r.dz * h.t;   // ray.cast(t)
+        if (static_cast<uint32_t>(k) > fp.max_depth) return end_colour(sc, h.obj);    // raytrace.rs:33
+        in.ptx = r.ox + r.dx * h.t; in.pty = r.oy + r.dy * h.t; in.ptz = r.oz + r.dz * h.t;   // ray.cast(t)
         double nx, ny, nz;
-        hit_normal(sc, v.sph, h.prim, ptx, pty, ptz, nx, ny, nz);
-        const double nd = nx * r.dx + ny * r.dy + nz * r.dz;
-        const Shading sh = shading_flags<kFresnel>(m, sig, nd);
-        if (!sh.diffuse && !sh.specular) {
-            set_terminal(b, c, end_colour(sc, h.obj), k);
-            return;
-        }
+        hit_normal(sc, v.sph, h.prim, in.ptx, in.pty, in.ptz, nx, ny, nz);
+        const Shading sh = shading_flags<kFresnel>(m, sig, nx * r.dx + ny * r.dy + nz * r.dz);
+        if (!sh.diffuse && !sh.specular) return end_colour(sc, h.obj);
         atomicAdd(&cnt[0][k], 1u);
-        uint32_t mask = 0;                                                // raytrace.rs:39-49
-        for (int l = 0; l < sc.n_lights; ++l) {
-            double lx, ly, lz, r2;
-            (void)light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
-            const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-            if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, h.prim, &wsh)) mask |= 1u << l;
-        }
-        const ShadeIn in{ptx, pty, ptz, r.dx, r.dy, r.dz, sig, h.obj, h.prim, c, mask};
-        shade_compute<kFresnel>(sc, b, k, 0, in);                         // the level, or the terminal
-        if (!sh.specular) return;
-        if (nd > 0.0) { nx = -nx; ny = -ny; nz = -nz; }                   // raytrace.rs:58-64
-        const double nsig = (sh.f * sig) * m.ks_sig;
-        r = reflect_ray(r, ptx, pty, ptz, nx, ny, nz);
-        sig = nsig;
-        atomicAdd(&cnt[1][k + 1], 1u);
+        in.dx = r.dx; in.dy = r.dy; in.dz = r.dz;
+        in.sig = sig;
+        in.obj = h.obj;
+        in.prim = h.prim;
     }
 }
-
-// The fused tail (WfStreams::tail_fuse = T): generations T .. max_depth + 1 of
-// a chunk in one launch, one chain per work-item (tail_chain), instead of a
-// nearest-hit launch per generation with its shadow and shading launches on
-// the B streams; it also answers the shadows and shading of the records of
-// generations T-D .. T-1 (WfStreams::tail_shade = D), so that no B-stream
-// launch competes with it for the CUs.  For small
-// chunks (one rank's share of a frame), whose late generations are a chain of
-// latency-bound launches: the tail then lasts about as long as the slowest
-// chain's remaining bounces, not the sum over generations of each generation's
-// slowest walk plus a launch each.  Needs the src-9 tree (whole tree + spheres
-// in LDS) and a light-view grid for every light.  gridDim.x workgroups, all
-// resident; workgroup w publishes its counts in region w and zeros in the
-// other regions r = w (mod gridDim.x) of every generation >= T.
-template <bool kFresnel, bool kCount>
-__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int D, int W) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint32_t s_cnt[2][kMaxGenerations];
-    __shared__ uint32_t s_rec[kMaxScan + 1];
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrcBvhL8C>(sc), b.G);
-    for (int i = threadIdx.x; i < 2 * kMaxGenerations; i += kWfThreads) (&s_cnt[0][0])[i] = 0u;
-    region_scan(b.rq() + T * b.G, b.G, ql.scan, ql.wave);      // the chains (Q_T); ends with a barrier
-    // the shade records of generations T-D .. T-1 (consecutive in rs: one scan over D*G regions)
-    const uint32_t M = static_cast<uint32_t>(D) * b.G;
-    if (D > 0) region_scan(b.rs() + (T - D) * b.G, M, s_rec, ql.wave);
-    const uint32_t nch = ql.scan[b.G];
-    const int gens = static_cast<int>(fp.max_depth) + 2;
-    const uint32_t nrec = D > 0 ? s_rec[M] : 0u, nw = gridDim.x * (kWfThreads / 64);
-    const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    // the chains in contiguous runs of cw per wave from the first wave slot up, the records 64
-    // per wave from the last slot down, so that chain waves and record waves are mostly
-    // apart; cw (tuning tail_width; auto: spread over about half of the waves) trades the
-    // slowest chain of a wave against the lanes its finished chains leave idle: 48 per wave
-    // beat 16 / 24 / 32 / 64 on one rank's share of an 8-way C3 frame.  Contiguous runs keep
-    // the queue / record loads and the level / terminal stores coalesced.
-    const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * nch + nw - 1) / nw));
-    const uint32_t rslot = nw - 1u - slot;
-    Work wn, wsh;
-    {                                                          // (every workgroup stages: one per CU)
-        const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
-        __syncthreads();
-        for (uint64_t base = static_cast<uint64_t>(slot) * cw; base < nch; base += static_cast<uint64_t>(nw) * cw) {
-            const uint64_t j = base + lane;
-            if (lane >= cw || j >= nch) continue;
-            const size_t at = region_entry(ql.scan, b.G, b.R, static_cast<uint32_t>(j));
-            const Ray r = load_ray(b, T & 1, at);
-            const double sig = ldn_if<kNtQ>(&b.qf(T & 1, 6)[at]);
-            const uint32_t c = ldn_if<kNtQ>(&b.qpix(T & 1)[at]);
-            tail_chain<kFresnel, kCount>(sc, fp, b, v, T, r, sig, c, s_cnt, wn, wsh);       // its remaining bounces
-        }
-        for (uint64_t base = static_cast<uint64_t>(rslot) * 64u; base < nrec; base += static_cast<uint64_t>(nw) * 64u) {
-            const uint64_t j = base + lane;                    // a record of T-D .. T-1: its shadows and shading
-            if (j >= nrec) continue;
-            const size_t at = static_cast<size_t>(T - D) * b.qcap + region_entry(s_rec, M, b.R, static_cast<uint32_t>(j));
-            ShadeIn in = shade_load(b, at, false);
-            for (int l = 0; l < sc.n_lights; ++l) {
-                double lx, ly, lz, r2;
-                (void)light_dir(sc.lights[l], in.ptx, in.pty, in.ptz, lx, ly, lz, r2);
-                const Ray sray{in.ptx + lx * kEps, in.pty + ly * kEps, in.ptz + lz * kEps, lx, ly, lz};
-                if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, in.ptx, in.pty, in.ptz, in.prim, &wsh))
-                    in.mask |= 1u << l;
-            }
-            shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, in);
-        }
-    }
-    __syncthreads();
-    for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
-        const bool own = rg == blockIdx.x;
-        for (int k = T + static_cast<int>(threadIdx.x); k < gens; k += kWfThreads) {
-            b.rs()[k * b.G + rg] = own ? s_cnt[0][k] : 0u;
-            b.rq()[(k + 1) * b.G + rg] = own ? s_cnt[1][k + 1] : 0u;
-        }
-    }
-    flush_work<kCount>(b, 2, wn);
-    flush_work<kCount>(b, 4, wsh);
-}
-
 // The fold factor of a level is the specular colour of its object times, for
 // FresnelMaterial, the level's Schlick factor (raytrace.rs:63 / 163).  The chain is folded inner-first exactly as the
 // recursion returns (acc = res_k + ks_k * acc); the loads of four levels are
@@ -1319,6 +1261,94 @@ template <bool kFresnel>
 __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, uint32_t p, uint8_t nlev) {   // p: the chain
     const Col acc{ldn_if<kNtFold>(&b.term(0)[p]), ldn_if<kNtFold>(&b.term(1)[p]), ldn_if<kNtFold>(&b.term(2)[p])};
     return fold_levels<kFresnel>(sc, b, p, nlev, acc);
+}
+
+// The fused tail (WfStreams::tail_fuse = T): for a small chunk (one rank's
+// share of a frame), whose late generations are a chain of latency-bound
+// launches, one launch takes every chain still running at generation T-1 from
+// its shade record of T-1 through all its remaining bounces (tail_chain), one
+// chain per work-item, and folds it onto its levels (fold_levels, as wf_fold)
+// and writes its pixel: instead of a nearest-hit launch per generation >= T
+// with its shadow and shading launches, and the frame-end fold.  The launch
+// waits for the B streams (the levels of generations <= T-2 are written); the
+// chains that ended by generation T-1 are folded meanwhile on a B stream
+// (wf_fold over nlev <= T-1; the tail's chains keep nlev = kNlevRunning).  It
+// lasts about as long as the slowest chain's remaining bounces, not the sum
+// over generations of each generation's slowest walk plus a launch each.
+// Needs the src-9 tree (whole tree + spheres in LDS) and a light-view grid for
+// every light.  With tail_fold 0 it also shades the records of the D
+// generations before T-1 (tuning tail_shade), so that no B-stream launch runs
+// alongside it and the frame-end fold finds the B streams done.
+// Chains in contiguous runs of cw per wave (tuning tail_width;
+// auto: spread over about half of the waves; 48 per wave beat 16 / 24 / 32 /
+// 64 on one rank's share of an 8-way C3 frame: the slowest chain of a wave
+// against the lanes its finished chains leave idle), contiguous so that the
+// record loads and level stores stay coalesced.  gridDim.x workgroups, all
+// resident; workgroup w publishes its counts in region w and zeros in the
+// other regions r = w (mod gridDim.x) of every generation >= T.
+template <bool kFresnel, bool kCount>
+__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int W, int fold,
+                                                        int D) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint32_t s_cnt[2][kMaxGenerations];
+    __shared__ double s_srgb[255];
+    __shared__ uint32_t s_rec[kMaxScan + 1];
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrcBvhL8C>(sc), b.G);
+    for (int i = threadIdx.x; i < 2 * kMaxGenerations; i += kWfThreads) (&s_cnt[0][0])[i] = 0u;
+    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
+    region_scan(b.rs() + (T - 1) * b.G, b.G, ql.scan, ql.wave);   // generation T-1's records; ends with a barrier
+    // the records of generations T-1-D .. T-2 (consecutive in rs: one scan over D*G regions), shading only
+    const uint32_t M = static_cast<uint32_t>(D) * b.G;
+    if (D > 0) region_scan(b.rs() + (T - 1 - D) * b.G, M, s_rec, ql.wave);
+    const uint32_t n = ql.scan[b.G], nrec = D > 0 ? s_rec[M] : 0u;
+    const int gens = static_cast<int>(fp.max_depth) + 2;
+    const uint32_t nw = gridDim.x * (kWfThreads / 64);
+    const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * n + nw - 1) / nw));
+    // the shading-only records go to the waves past the chains' when those take them in at most
+    // two rounds, else to every wave (last slot first)
+    const uint32_t chain_waves = static_cast<uint32_t>(min<uint64_t>(nw, (static_cast<uint64_t>(n) + cw - 1) / cw));
+    const bool apart = static_cast<uint64_t>(nw - chain_waves) * 128u >= nrec;
+    const uint32_t rw = apart ? nw - chain_waves : nw;
+    const uint32_t rslot = apart ? (slot >= chain_waves ? slot - chain_waves : 0xFFFFFFFFu) : nw - 1u - slot;
+    Work wn, wsh;
+    const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
+    __syncthreads();
+    const size_t rk = static_cast<size_t>(T - 1) * b.qcap;
+    for (uint64_t base = static_cast<uint64_t>(slot) * cw; base < n; base += static_cast<uint64_t>(nw) * cw) {
+        const uint64_t j = base + lane;
+        if (lane >= cw || j >= n) continue;
+        const size_t at = rk + region_entry(ql.scan, b.G, b.R, static_cast<uint32_t>(j));
+        const ShadeIn in = shade_load(b, at, false);
+        int nlev = 0;
+        const Col term = tail_chain<kFresnel, kCount>(sc, fp, b, v, T - 1, in, nlev, s_cnt, wn, wsh);
+        if (!fold) {                                          // (tail_fold 0: the frame-end wf_fold folds it)
+            set_terminal(b, in.c, term, nlev);
+            continue;
+        }
+        const Col res = average_samples(fold_levels<kFresnel>(sc, b, in.c, nlev, term), fp.spp);
+        const uint32_t p = b.cpix()[in.c];
+        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+    }
+    for (uint64_t base = static_cast<uint64_t>(rslot) * 64u; rslot != 0xFFFFFFFFu && base < nrec;
+         base += static_cast<uint64_t>(rw) * 64u) {
+        const uint64_t j = base + lane;                        // a record of T-1-D .. T-2: its shadows and shading
+        if (j >= nrec) continue;
+        const size_t at = static_cast<size_t>(T - 1 - D) * b.qcap + region_entry(s_rec, M, b.R, static_cast<uint32_t>(j));
+        ShadeIn in = shade_load(b, at, false);
+        in.mask = grid_shadow_mask<kCount>(sc, v, in.ptx, in.pty, in.ptz, in.prim, wsh);
+        (void)shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, in);
+    }
+    __syncthreads();
+    for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
+        const bool own = rg == blockIdx.x;
+        for (int k = T + static_cast<int>(threadIdx.x); k < gens; k += kWfThreads) {
+            b.rs()[k * b.G + rg] = own ? s_cnt[0][k] : 0u;
+            b.rq()[(k + 1) * b.G + rg] = own ? s_cnt[1][k + 1] : 0u;
+        }
+    }
+    flush_work<kCount>(b, 2, wn);
+    flush_work<kCount>(b, 4, wsh);
 }
 
 // Eager fold (WfBufs::eager): the pixels whose chain ended in generation k --
@@ -1497,10 +1527,25 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     hipError_t e;
     if (ws.tail_fuse > 0 && k >= ws.tail_fuse) {      // the fused tail: every generation >= T in one launch
         if (k > ws.tail_fuse) return hipSuccess;
+        // the tail folds its chains (tail_fold): the levels of generations <= T-2 (the B streams) must
+        // be written; otherwise the frame-end fold folds every chain and the tail waits for nothing
+        for (int i = 0; i < ws.nb && ws.tail_fold; ++i) {
+            if (ws.b[i] == ws.a) continue;
+            if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
+        }
+        // the chains that ended by generation T-1, folded on a B stream while the tail runs
+        if (ws.tail_fold && ws.b[0] != ws.a) {
+            if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ws.b[0], ws.near_done[k], 0)) != hipSuccess) return e;
+        }
+        if (ws.tail_fold && (e = launch_fold(sc, fp, b, ws.b[0], ws.b[0] != ws.a ? ws.mb[0] : ws.ma, 0u,
+                                             static_cast<uint32_t>(k - 1))) != hipSuccess)
+            return e;
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
         const size_t lds_t = staged_bytes<kSrcBvhL8C>(sc) + queue_lds_bytes(b.G);
-        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_shade, ws.tail_width);
-        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_shade, ws.tail_width);
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, ws.tail_fold, ws.tail_shade);
+        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, ws.tail_fold, ws.tail_shade);
         return ws.ma ? ws.ma->mark(ws.a, kKfTail) : hipGetLastError();
     }
     e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
@@ -1558,8 +1603,8 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (!shaded && !b.eager) return hipSuccess;
     // the merged tail: generations >= bmerge are shaded together after the last nearest-hit launch
     if (ws.bmerge > 0 && k >= ws.bmerge) return hipSuccess;
-    // the fused tail also shades the records of generations T-D .. T-1
-    if (ws.tail_fuse > 0 && k >= ws.tail_fuse - ws.tail_shade) return hipSuccess;
+    // the fused tail shades the records of generations T-1-D .. T-1 itself
+    if (ws.tail_fuse > 0 && k >= ws.tail_fuse - 1 - ws.tail_shade) return hipSuccess;
     // shadows and shading of generation k: on a b stream once nearest_k is done
     // (generations alternate over the b streams, so consecutive ones overlap too)
     const int bi = k % ws.nb;
@@ -1691,7 +1736,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     const hipStream_t s = ws.a;
     // the chains not folded early (all of them without the split)
-    if (!b.eager && (e = launch_fold(sc, fp, b, s, ws.ma, split_fold(ws, fp) ? ws.fold_split + 1u : 0u, kNlevRunning - 1u)) != hipSuccess)
+    // (the fused tail folded every chain: its own as it ended them, the others on a B stream)
+    if (!b.eager && (ws.tail_fuse == 0 || !ws.tail_fold) &&
+        (e = launch_fold(sc, fp, b, s, ws.ma, split_fold(ws, fp) ? ws.fold_split + 1u : 0u, kNlevRunning - 1u)) != hipSuccess)
         return e;
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
     if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, s)) != hipSuccess) return e;

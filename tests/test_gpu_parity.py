@@ -320,16 +320,18 @@ def test_quad_tail_walk_matches_oracle(gpu_ctx, scene):
 @pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan", "fresnel"])
 def test_fused_tail_matches_oracle(gpu_ctx, scene):
     """The fused tail (tuning tail_fuse = T, trace_kernel.hip wf_tail): every
-    generation >= T of each chain -- nearest hit, light-view grid shadows,
-    Phong sum, reflection -- in one launch, one chain per work-item.  From
-    generation 1 (nearly the whole recursion) and from 4, on ties across
-    leaves, the deepest small tree, NaN planes, Fresnel levels and a C3
-    workload: bit for bit the oracle's image, and the same ray and shadow-ray
-    counts (the tail publishes every generation's queue and record counts).
-    The timed render checks that the tail really ran: one nearest-hit launch
-    for the generations >= T, and no shadow or shading launches of their own
-    for them or for generation T-1 (whose records the tail shades too,
-    tuning tail_shade = 1)."""
+    chain still running at generation T-1 goes from its shade record through
+    all its remaining bounces -- light-view grid shadows, Phong sum,
+    reflection, nearest hit -- in one launch, one chain per work-item, and
+    (tail_fold 1) folds it there, the chains that ended earlier being folded
+    on a B stream meanwhile.  From generation 1 (nearly the whole recursion) and from 4, on
+    ties across leaves, the deepest small tree, NaN planes, Fresnel levels and
+    a C3 workload: bit for bit the oracle's image, and the same ray and
+    shadow-ray counts (the tail publishes every generation's queue and record
+    counts).  The timed render checks that the tail really ran: one tail
+    launch, nearest-hit launches for generations 1 .. T-1 only, shadow and
+    shading launches for 0 .. T-2 (or fewer: tail_shade = D hands the records
+    of D more generations to the tail), one fold."""
     def fresnel():
         s = scenes.config3(96, 72)
         s.max_depth = 10
@@ -341,8 +343,8 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
     # (the tail answers shadows through light-view grids only: directional lights become point lights far away)
     s.lights = [l if l["kind"] == "point" else
                 {"kind": "point", "location": tuple(-40.0 * x for x in l["direction"]), "color": l["color"]} for l in s.lights]
-    for T in (1, 4):
-        with _with_tuning(gpu_ctx, tail_fuse=T, tail_shade=1):
+    for T, fold, D in ((1, 0, 0), (4, 0, 1), (4, 1, 0), (2, 1, 0), (4, 0, 3), (3, 0, 0)):
+        with _with_tuning(gpu_ctx, tail_fuse=T, tail_fold=fold, tail_shade=D):
             check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
             gpu_ctx.kernel_times()
             gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
@@ -350,7 +352,9 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
             kt = gpu_ctx.kernel_times()
         if T <= s.max_depth + 1:
             assert kt["nearest"][1] == T - 1 and kt["tail"][1] == 1, (T, kt)     # generations 1 .. T-1, the tail
-            assert kt["occlusion"][1] + kt["shadow"][1] == T - 1, (T, kt)       # generations 0 .. T-2
+            d = 0 if fold else min(D, T - 1)
+            assert kt["occlusion"][1] + kt["shadow"][1] == T - 1 - d, (T, kt)   # generations 0 .. T-2-d
+            assert kt["fold"][1] == 1, (T, kt)     # the frame-end fold, or (tail_fold) the chains that ended by T-1
 
 
 @pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "extreme", "planes_nan"])
@@ -698,7 +702,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(bmerge=5, tail_from=1, tail_max=1 << 30), dict(bmerge=2, regions=2048), dict(wave_max=0),
                dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4), dict(cam=3),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
-               dict(tail_fuse=4, tail_shade=0), dict(tail_fuse=6, tail_shade=5)]:
+               dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, tail_fold=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

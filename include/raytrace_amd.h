@@ -309,7 +309,8 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * bounces; 0 off, -1 auto), tail_width (that launch's chains per wave, 0
  * auto), tail_fold (1: it also folds its chains, after the shading streams),
  * tail_shade (with tail_fold 0: it also shades the records of this many
- * generations before T-1).
+ * generations before T-1), fold_wgs / shade_wgs (workgroups of a fold / shading
+ * launch: 0 one per region, -1 one per CU, else that many).
  * cu_mask and prio rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -299,6 +299,8 @@ struct WfBufs {
     uint32_t tail_max;              //   <= tail_max rays go to the quad kernel (src 17), the rest to src 9
     uint32_t wave_max;              // src 9, generations >= 1: queues of <= wave_max rays take the
                                     //   wave-cooperative query (one ray per wave at a time, nearest_wave)
+    uint32_t fold_wgs, shade_wgs;   // workgroups of wf_fold / wf_shade launches (0: G); their dealing
+                                    //   spans the launch's grid (grid_slot)
     uint32_t eager;                 // 1: each generation folds the pixels whose chain ended in it
                                     //   (wf_fold_gen on the B streams), no frame-end fold
     uint64_t o_dn, o_rd;            // eager: chain ends found by wf_nearest, their region sizes

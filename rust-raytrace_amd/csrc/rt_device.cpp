@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
     kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
     kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneTailFold, kTuneTailShade, kTuneCount
+    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneTailFold, kTuneTailShade, kTuneFoldWgs, kTuneShadeWgs, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -98,6 +98,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"tail_fold", 1, 0, 1},                      // ... 1: which also folds them (after the shading streams)
     {"tail_shade", 1, 0, 8},                     // ... which also shades the records of this many generations before
                                                  // T-1 (tail_fold 0)
+    {"fold_wgs", 0, -1, 2048},                   // workgroups of a wf_fold launch (0: G regions, -1 auto: one per CU)
+    {"shade_wgs", 0, -1, 2048},                  // workgroups of a wf_shade launch (0: G regions, -1 auto: one per CU)
 };
 
 }  // namespace
@@ -1194,6 +1196,11 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.tail_from = tail_from;
             c->lanes[l].b.tail_max = tail_max;
             c->lanes[l].b.wave_max = wave_max;
+            // (wf_fold at 96 VGPRs and wf_shade at 128 fit one 1024-thread workgroup per CU: -1 launches
+            // one per CU, each dealing over the launch's own grid, instead of G in two dispatch rounds)
+            const int64_t fw = c->t(kTuneFoldWgs), sw = c->t(kTuneShadeWgs);
+            c->lanes[l].b.fold_wgs = fw < 0 ? static_cast<uint32_t>(c->n_cu) : static_cast<uint32_t>(fw);
+            c->lanes[l].b.shade_wgs = sw < 0 ? static_cast<uint32_t>(c->n_cu) : static_cast<uint32_t>(sw);
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));

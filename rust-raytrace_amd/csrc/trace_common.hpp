@@ -140,10 +140,18 @@ __device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, const
     const double disc = b * b - k.a4 * cc;
     if (disc > 0.0) {
         const double sq = sqrt(disc);
-        const double t1 = div_a2(-b - sq, k);
-        if (t1 > 0.0) { t = t1; return true; }
-        const double t2 = div_a2(-b + sq, k);
-        if (t2 > 0.0) { t = t2; return true; }
+        // a2 >= 0 (or NaN): x <= 0 or NaN gives x / a2 <= 0, -0 or NaN, never > 0, so the
+        // division is skipped there (a root behind the origin)
+        const double x1 = -b - sq;
+        if (x1 > 0.0) {
+            const double t1 = div_a2(x1, k);
+            if (t1 > 0.0) { t = t1; return true; }
+        }
+        const double x2 = -b + sq;
+        if (x2 > 0.0) {
+            const double t2 = div_a2(x2, k);
+            if (t2 > 0.0) { t = t2; return true; }
+        }
     }
     return false;
 }

@@ -194,6 +194,14 @@ __device__ __forceinline__ uint32_t wave_slot(const WfBufs& b, uint32_t n) {
     return deal_major(b, n) ? blockIdx.x * (kWfThreads / 64) + wave : wave * b.G + blockIdx.x;
 }
 
+// wave_slot over the launch's own grid (kernels launched with fewer than G
+// workgroups: every one resident at once when the kernel's registers allow
+// only one workgroup per CU); identical to wave_slot when gridDim.x == G.
+__device__ __forceinline__ uint32_t grid_slot(const WfBufs& b, uint32_t n) {
+    const uint32_t wave = threadIdx.x >> 6;
+    return deal_major(b, n) ? blockIdx.x * (kWfThreads / 64) + wave : wave * gridDim.x + blockIdx.x;
+}
+
 // Whether this workgroup's first chunk is below n (workgroup-uniform).
 __device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n, uint32_t width = 64) {
     const uint64_t first = deal_major(b, n) ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
@@ -1136,9 +1144,9 @@ __global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams 
     const size_t rk = static_cast<size_t>(k) * b.qcap;
     // software pipelined: the next chunk's records are loaded (HBM) before this chunk is
     // shaded, so at the kernel's 4 waves per SIMD their latency hides behind the f64 math
-    const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    const uint32_t W = gridDim.x * (kWfThreads / 64), lane = threadIdx.x & 63u;
     const bool lit = sc.n_lights > 0;
-    uint32_t rc = wave_slot(b, n);
+    uint32_t rc = grid_slot(b, n);
     size_t at = 0;
     ShadeIn cur{};
     bool have = false;
@@ -1414,7 +1422,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
     const uint32_t n = s_scan[b.G];
     // software pipelined: the next chunk's chain header (level count, pixel, terminal) is
     // loaded before this chain's levels are folded, one dependent round trip less per chain
-    const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    const uint32_t W = gridDim.x * (kWfThreads / 64), lane = threadIdx.x & 63u;
     struct Head {
         uint32_t c, nlev, p;
         Col term;
@@ -1430,7 +1438,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
         }
         return hd;
     };
-    uint32_t rc = wave_slot(b, n);
+    uint32_t rc = grid_slot(b, n);
     Head cur = head(static_cast<uint64_t>(rc) * 64u + lane);
     for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
         const Head nxt = head(static_cast<uint64_t>(rc + W) * 64u + lane);
@@ -1447,8 +1455,9 @@ hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& 
                        uint32_t lo, uint32_t hi) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
-    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    const dim3 grid(b.fold_wgs > 0 && b.fold_wgs < b.G ? b.fold_wgs : b.G);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 
@@ -1667,8 +1676,9 @@ hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBuf
     }
     if (fused) return hipSuccess;
     if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, sb, sc, fp, b, k, ngen);
-    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, sb, sc, fp, b, k, ngen);
+    const dim3 sgrid(b.shade_wgs > 0 && b.shade_wgs < b.G ? b.shade_wgs : b.G);
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, sgrid, block, 0, sb, sc, fp, b, k, ngen);
+    else hipLaunchKernelGGL(wf_shade<false>, sgrid, block, 0, sb, sc, fp, b, k, ngen);
     return mb ? mb->mark(sb, kKfShade) : hipSuccess;
 }
 

@@ -67,7 +67,8 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"lists0", 0, 0, 1},                         // shadow lists from generation 0
     {"path_group", 0, 0, 64},                    // path kernel: lanes per pixel (0: auto)
     {"cu_mask", 1, 0, 4},                        // b streams CU-masked (own hardware queue): 1 every CU, 2/3/4 only 3/4, 1/2, 1/4 of them
-    {"prio", 0, 0, 1},                           // nearest-hit chain on a high-priority stream
+    {"prio", 1, 0, 1},                           // nearest-hit chain on a high-priority stream (round 4: C3 2.969-2.974
+                                                 // vs 2.983-2.998 ms, 8-way share 0.713 vs 0.741 ms, C4 equal; same box)
     {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
     {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)

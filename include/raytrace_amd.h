@@ -52,9 +52,10 @@
 extern "C" {
 #endif
 
-/* 4: rt_stats gained `chunks` (80 B); rt_abi_version() added.  A caller checks
- * rt_abi_version() == RT_ABI_VERSION of the header it was built against before
- * passing any struct (older callers pass a smaller rt_stats). */
+/* 4: rt_abi_version() added; rt_kernel_family gained RT_KF_TAIL (RT_KF_COUNT 8);
+ * rt_stats unchanged (80 B, `chunks` since ABI 3).  Later additions of functions
+ * only (rt_qtree_nodes) keep the version.  A caller checks rt_abi_version() ==
+ * RT_ABI_VERSION of the header it was built against before passing any struct. */
 #define RT_ABI_VERSION 4
 
 enum rt_status {
@@ -160,6 +161,19 @@ int rt_light_grid_candidates(const rt_scene* scene, int light, int resolution, c
  * the lists against that scan. */
 int rt_view_grid_candidates(const rt_scene* scene, int resolution, const double* dirs, uint32_t n_dirs,
                             int32_t* counts, int32_t* ids, float* nears, size_t cap, int64_t* info);
+/* Diagnostic, host only: the quantised 4-wide sphere tree (DESIGN.md §3.10,
+ * built as rt_scene_upload builds it; leaf_max 0: the upload's leaf size) and
+ * the f32 child boxes it rounds outward.  nodes: 48 B per node (the device
+ * layout, DevQNode4), at most cap_nodes; boxes: per node and child slot
+ * lo x,y,z, hi x,y,z (f32; NaN for an unused slot), at most cap_nodes * 24
+ * floats; sphere_first / sphere_count: per node and slot the leaf's spheres in
+ * leaf order (-1 / 0 for an inner child or unused slot).  info[0..2] = nodes (0:
+ * not representable, the device keeps the other trees), the traversal stack's
+ * worst case, the leaf size.  Replaces nothing in the reference (scene.rs:247-249
+ * scans every object); tests decode the nodes and check every box contains its
+ * f32 box. */
+int rt_qtree_nodes(const rt_scene* scene, int leaf_max, void* nodes, float* boxes, int32_t* sphere_first,
+                   int32_t* sphere_count, size_t cap_nodes, int64_t* info);
 /* Decode an image file as Texture::load does (RGB8, rows top-down).  rgb == NULL: only the size.
  * Formats: uncompressed BMP (24/32 bit) and binary PPM; others -> RT_E_UNSUPPORTED. */
 int rt_texture_load(const char* path, uint32_t* width, uint32_t* height, uint8_t* rgb, size_t cap);
@@ -267,10 +281,10 @@ enum rt_kernel_family {
     RT_KF_NEAREST = 0,      /* wf_nearest, generations >= 1 */
     RT_KF_OCCLUSION = 1,    /* wf_occlusion: every (record, light) pair of a generation */
     RT_KF_SHADE = 2,        /* wf_shade */
-    RT_KF_FOLD = 3,         /* wf_fold, or wf_fold_gen per generation (eager_fold) */
+    RT_KF_FOLD = 3,         /* wf_fold */
     RT_KF_TALLY = 4,        /* wf_tally */
     RT_KF_CAMERA = 5,       /* wf_nearest, generation 0 (camera rays) */
-    RT_KF_SHADOW = 6,       /* wf_shadow: the shadow item lists of a generation */
+    RT_KF_SHADOW = 6,       /* (unused since round 5: the shadow item lists were removed) */
     RT_KF_TAIL = 7,         /* wf_tail: the fused generations >= tail_fuse */
     RT_KF_COUNT = 8
 };
@@ -279,39 +293,25 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
 /* Schedule tuning of a context (A/B measurement; the defaults are the measured
  * best).  Keys (rt_tuning_key(i) for i = 0, 1, ... until NULL):
  * chunk_pixels (wavefront chunk cap, 0: from the working-set budget), bvh_leaf, light_grids, light_grid_res
- * (these three take effect at the next rt_scene_upload), src, src_occ,
- * prefix_kb, prefix4_kb, lanes, stagger_gen, regions, split, bstreams, fuse,
- * lists, cam, deal, spread_below, lists0, path_group, cu_mask, prio, verbose,
- * grid_occ, fuse_from, compact_stack (small trees: 32-bit nearest-hit stack entries),
+ * (these three take effect at the next rt_scene_upload), src, src_occ (the
+ * nearest-hit and shadow sphere sources, trace_kernel.hip kSrc*; an unsupported
+ * pair falls back to the binary tree through L2), prefix_kb (KB of the tree's
+ * top staged in LDS for trees beyond LDS), lanes, stagger_gen, regions, split,
+ * bstreams, cam (generation 0: 3 the camera's view grid, -1 where built, other
+ * values per ray), deal, spread_below, path_group, cu_mask, prio, verbose,
+ * grid_occ, compact_stack (small trees: 32-bit nearest-hit stack entries),
  * half_nodes (trees beyond LDS: binary16 node bounds for the prefix walk),
- * cam_prefix_kb (camera view read through L2: KB of its top staged in LDS),
  * wf_budget_mb (wavefront working set of all chunk lanes, MB; 0: min(80 GB, 85%
  * of the device's free memory); a hipMalloc that still fails halves the chunks),
- * tail_from / tail_max (trees that fit LDS: nearest-hit generations >= tail_from
- * hand queues of <= tail_max rays to a walk with four lanes per ray on the 4-wide
- * tree; tail_from 0 off, -1 auto: 5 for chunks of <= 32 x tail_max pixels;
- * tail_max 0: CUs x 256), eager_fold (1: each generation folds the pixels whose
- * chain ended in it, on the shading streams; 0: one fold after the last generation),
- * fold_split (K > 0: chains that ended by generation K fold on a shading stream
- * during the later generations, the rest after the last one; with one or two
- * shading streams only, ignored with bstreams > 2), bmerge (T > 0: generations >= T
- * get no shadow / shading launches of their own; one occlusion and one shading
- * launch over all their records follow the last nearest-hit launch; -1 auto),
- * wave_max (trees that fit LDS: nearest-hit queues of generations >= 1 holding
- * <= wave_max rays take the wave-cooperative query, one ray per wave over sphere
- * clusters; 0 off, -1 auto), cam (generation 0: 0 per ray, 1 / 2 camera tiles over the
- * camera view of the tree in LDS / through L2, 3 the camera's view grid), cam_grid_res
- * (the view grid's cells per face side, 0 from the scene's frame size, -1 none;
- * at the next rt_scene_upload), a_queue (1: the nearest-hit chain's stream gets a
- * hardware queue of its own), tail_fuse (T >= 1: the chains still running at
- * generation T-1 of a frame on the src-9 tree whose lights all have light-view
- * grids finish in one launch, one chain per work-item through its remaining
- * bounces; 0 off, -1 auto), tail_width (that launch's chains per wave, 0
- * auto), tail_fold (1: it also folds its chains, after the shading streams),
- * tail_shade (with tail_fold 0: it also shades the records of this many
- * generations before T-1), fold_wgs / shade_wgs (workgroups of a fold / shading
- * launch: 0 one per region, -1 one per CU, else that many).
- * cu_mask and prio rebuild the context's streams (after pending work) when changed.
+ * cam_grid_res (the view grid's cells per face side, 0 from the scene's frame
+ * size, -1 none; at the next rt_scene_upload), a_queue (1: the nearest-hit
+ * chain's stream gets a hardware queue of its own), tail_fuse (T >= 1: the
+ * chains still running at generation T-1 of a frame on the src-9 tree whose
+ * lights all have light-view grids finish in one launch, one chain per
+ * work-item through its remaining bounces, folded there; 0 off, -1 auto),
+ * tail_width (that launch's chains per wave, 0 auto), qtree (1: trees beyond
+ * LDS take the quantised 4-wide tree for the nearest hit).
+ * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */
 int rt_ctx_set_tuning(rt_ctx* ctx, const char* key, int64_t value);

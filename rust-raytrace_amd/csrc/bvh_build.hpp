@@ -1,6 +1,7 @@
 // Host-side sphere BVH builder (host_bvh.cpp).
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -37,16 +38,6 @@ int bvh4_stack_need(const Bvh4Result& b4);
 // Depth of a binary tree (its traversal pushes at most one entry per level).
 int bvh_depth(const BvhResult& b2);
 
-// Clusters of a binary tree for the wave-cooperative query (device_layout.hpp,
-// DevCluster): subtrees of <= kClusterMax spheres; perm = the 8 octant orders,
-// each 64 * slots entries.  Empty when there are more than 64 * kClusterSlotsMax.
-struct ClusterResult {
-    std::vector<DevCluster> clusters;
-    std::vector<uint16_t> perm;
-    int slots = 0;
-};
-ClusterResult build_clusters(const BvhResult& b2, size_t n_spheres);
-
 // The binary tree's nodes with binary16 bounds rounded outward (DevBvhNodeH);
 // empty when some bound is not finite or lies outside the half range.
 std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2);
@@ -55,9 +46,11 @@ float half_to_float(uint16_t h);
 bool half_round_down(float v, uint16_t& out);
 bool half_round_up(float v, uint16_t& out);
 
-// Camera view of every node of a binary BVH (DevCamNode) for a camera at
-// `pos` with direction matrix `m` (row-major, camera.rs:57-61).
-std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]);
+// The 4-wide tree with 8-bit child bounds in a per-node frame (DevQNode4),
+// every decoded box containing the f32 child box; empty when some bound is not
+// finite or too large, a node's leaf children lie more than 4094 spheres apart,
+// the tree has 32768 nodes or more, or the root is a leaf.
+std::vector<DevQNode4> quantize_bvh4(const Bvh4Result& b4);
 
 }  // namespace rtamd
 

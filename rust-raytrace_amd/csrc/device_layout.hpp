@@ -70,21 +70,6 @@ struct alignas(16) DevBvhNodeH {
 };
 static_assert(sizeof(DevBvhNodeH) == 32, "half BVH node is 32 B");
 
-// Camera view of one binary BVH node, for the generation-0 tile traversal:
-// every camera ray starts at the camera position, so a child box maps to a
-// conservative rectangle of image-plane coordinates (px, py) -- the (px, py)
-// of main.rs:50-53 / camera.rs:78 -- outside which no camera ray can report a
-// hit inside the box, and to a lower bound on the t of any such hit.  Rects
-// are rounded outward to f32 (+-inf when the box reaches behind the camera
-// plane); tmin is rounded down.  Same index and child pointers as DevBvhNode.
-struct alignas(16) DevCamNode {
-    float r0[4];                    // child 0: px_lo, py_lo, px_hi, py_hi
-    float r1[4];                    // child 1
-    float tmin0, tmin1;
-    int32_t c0, c1;
-};
-static_assert(sizeof(DevCamNode) == 48, "camera node is 48 B");
-
 // 4-wide BVH, plane-major: node i's child boxes and pointers are 7 16-byte
 // planes, plane k at index k * n_nodes + i (lo.x, hi.x, lo.y, hi.y, lo.z,
 // hi.z of the 4 children, then the 4 child pointers).  A wave's lanes reading
@@ -99,6 +84,29 @@ struct alignas(16) DevBvh4Plane {
 };
 constexpr int kBvh4Planes = 7;
 constexpr int32_t kBvh4Empty = INT32_MIN;
+
+// The 4-wide tree with child boxes quantised to 8 bits per bound in a per-node
+// frame (host_bvh.cpp quantize_bvh4): 48 B per node, so C4's whole tree (10k
+// spheres, 1510 nodes) fits one nearest-hit workgroup's LDS share.  Per axis a
+// the frame is a power-of-two step s_a = 2^(e_a - 127) and an origin m_a * s_a
+// (m_a a signed 24-bit integer); child k's bounds are (m_a + lo_a[k]) * s_a and
+// (m_a + hi_a[k]) * s_a, which are exact f32 values (|m_a| + 255 < 2^24, normal
+// range), rounded OUTWARD from the child's f32 box on the host: every decoded
+// box contains the binary tree's f32 box, so the slab test on it culls a subset
+// of what the f32 test culls.  Child refs (u16):
+// < 0x8000 an inner node; 0x8000 | off << 3 | (count - 1) a leaf of spheres
+// [base + off, + count); kQ4Empty an unused slot.
+struct alignas(16) DevQNode4 {
+    int32_t frame[3];               // m_a (low 24 bits, signed) | e_a << 24
+    uint32_t base;                  // first sphere (leaf order) of the node's leaf children
+    uint32_t lo[3];                 // per axis: byte k = child k's lower bound
+    uint32_t hi[3];                 // per axis: byte k = child k's upper bound
+    uint16_t child[4];
+};
+static_assert(sizeof(DevQNode4) == 48, "quantised 4-wide node is 48 B");
+constexpr uint16_t kQ4Empty = 0xFFFF;
+constexpr uint16_t kQ4Leaf = 0x8000;
+constexpr int kQ4Stack = 32;          // nearest_q4's stack entries per lane (host: bvh4_stack_need <= this)
 
 // One skybox face (texture.rs:22-26): RGB8 rows top-down at DevScene::tex + off.
 struct DevTexFace {
@@ -127,23 +135,6 @@ struct DevLgEntry {
     float near;
 };
 
-// Sphere clusters for the wave-cooperative nearest query (nearest_wave): the
-// subtrees of the binary BVH cut where a subtree holds <= kClusterMax spheres
-// (host_bvh.cpp build_clusters).  A cluster's spheres are one contiguous range
-// of the leaf order; its box is the binary tree's f32 box of that subtree
-// (padded and rounded outward, so every hit point the exact test can report
-// lies inside it).  cl_perm[octant][slot]: the clusters in increasing order of
-// their centres along the octant's diagonal (a heuristic near-to-far order),
-// kClusterNone in unused slots; slots = 64 * DevScene::cl_slots.
-constexpr int kClusterMax = 16;
-constexpr int kClusterSlotsMax = 4;       // clusters per lane of the wave
-constexpr uint16_t kClusterNone = 0xFFFF;
-struct alignas(16) DevCluster {
-    float lo[3], hi[3];
-    int32_t first, count;
-};
-static_assert(sizeof(DevCluster) == 32, "cluster is 32 B");
-
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -156,11 +147,9 @@ struct DevScene {
     int32_t n_spheres, n_planes, n_lights, n_bvh;
     const DevBvh4Plane* bvh4;       // the same tree collapsed 4-wide (DevBvh4Plane)
     int32_t bvh4_root, n_bvh4;
-    const DevCamNode* cam_nodes;    // camera view of the binary BVH (null: generation 0 traverses per ray)
     const DevBvhNodeH* bvh_h;       // the binary BVH with binary16 bounds (null: not representable)
     int32_t has_fresnel;            // some object uses FresnelMaterial
-    int32_t pfx2, pfx4;             // prefix sources: nodes of the binary / 4-wide tree staged in LDS (set per render)
-    int32_t pfxc;                   // camera source from L2: camera nodes staged in LDS (set per render)
+    int32_t pfx2;                   // prefix sources: nodes of the binary tree staged in LDS (set per render)
     int32_t needs_path;             // a class only the path kernel implements (IndirectPhong, Transparent,
                                     // AreaLight, DepthOfFieldCamera)
     int32_t skybox;                 // SkyboxBackground (raytrace.rs:234-256; path kernel only)
@@ -179,9 +168,9 @@ struct DevScene {
     const DevLightGrid* cgrid;       // the camera's view grid (camera rays' nearest hit; null: none)
     const uint32_t* cg_off;
     const DevLgEntry* cg_ent;
-    const DevCluster* clusters;      // wave-cooperative nearest query (null: not built)
-    const uint16_t* cl_perm;         // [8][64 * cl_slots]
-    int32_t n_clusters, cl_slots;    // cl_slots = ceil(n_clusters / 64) <= kClusterSlotsMax, 0 = none
+    const DevQNode4* q4;             // the quantised 4-wide tree (null: not representable)
+    int32_t n_q4;                    // its nodes (breadth-first; root = node 0)
+    int32_t pfxq;                    // nodes [0, pfxq) staged in LDS by the quantised-tree source (set per render)
 };
 
 struct FrameParams {
@@ -255,10 +244,10 @@ struct PathStack {
 //   records  shade records, f64 fields [7][levels*qcap] (hit point x,y,z,
 //            incoming direction x,y,z, significance) then u32 fields
 //            [4][levels*qcap] (object id, primitive: sphere >= 0 / ~plane,
-//            chain, occlusion mask: bit l = light l shadowed, bits 24.. = lights
-//            decided).  One region array per generation (generation k at
-//            k*qcap), so the nearest-hit kernels never wait for the shadow /
-//            shading kernels of earlier generations (the other stream);
+//            chain, occlusion mask: bit l = light l shadowed).  One region
+//            array per generation (generation k at k*qcap), so the nearest-hit
+//            kernels never wait for the shadow / shading kernels of earlier
+//            generations (the other stream);
 //   levels   per-level local colour r,g,b and Schlick factor (f64)
 //            [4][levels*capa], then object id (i32) [levels*capa]; [k*capa + c]
 //            for chain c (chain = the entry of the lit camera hit's generation-0
@@ -267,27 +256,20 @@ struct PathStack {
 //   term     terminal colour of each chain [3][capa] (f64), then nlev (u8,
 //            levels pushed) [capa];
 //   rq / rs  [k*G + r]: entries of region r of Q_k / of generation k's records;
-//   oq / ro  shadow item lists (nlists > 0): for generation k and light l the
-//            records whose query toward l needs the sphere traversal; list
-//            n_lights = records with nothing left to trace.  Entry = record
-//            index within generation k; [(k*nlists + list)*qcap + entry] and
-//            region sizes [(k*nlists + list)*G + r];
-//   dn / rd  eager fold only (chain ends found by wf_nearest, their region sizes);
 //   cpix     the chunk pixel of each chain [qcap] (u32).
-// Queue, record and list arrays are G regions of R entries (qcap = G*R); region
-// r is written only by workgroup r of the producing kernel.
+// Queue and record arrays are G regions of R entries (qcap = G*R); region r is
+// written only by workgroup r of the producing kernel.
 struct WfBufs {
     unsigned char* mem;
     unsigned long long* totals;     // [0] nearest queries, [1] shadow queries, [2..3] nearest box / sphere
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
     uint64_t qcap;                  // G * R
-    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_oq, o_ro;   // byte offsets of the sections
+    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix;   // byte offsets of the sections
     uint32_t cap;                   // pixel capacity
     uint32_t capa;                  // qcap rounded up to 64: stride of the per-chain arrays (levels,
                                     // terminals; chain c = generation 0's record entry c)
     uint32_t levels;                // record generations / stack levels (max_depth + 1)
-    uint32_t nlists;                // n_lights + 1, or 0 (no lists: the plain shadow kernel)
     uint32_t G;                     // regions per queue
     uint32_t R;                     // entries per region: ceil(slots / (G * 1024)) * 1024
     uint32_t slots;                 // generation-0 slots of this chunk (8x8 tiles, >= pixels)
@@ -295,16 +277,6 @@ struct WfBufs {
     uint32_t spread_below;          // queues below this many items are dealt workgroup-first regardless
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
-    int32_t tail_from;              // > 0: nearest-hit generations >= this of a src-9 tree: queues of
-    uint32_t tail_max;              //   <= tail_max rays go to the quad kernel (src 17), the rest to src 9
-    uint32_t wave_max;              // src 9, generations >= 1: queues of <= wave_max rays take the
-                                    //   wave-cooperative query (one ray per wave at a time, nearest_wave)
-    uint32_t fold_wgs, shade_wgs;   // workgroups of wf_fold / wf_shade launches (0: G); their dealing
-                                    //   spans the launch's grid (grid_slot)
-    uint32_t eager;                 // 1: each generation folds the pixels whose chain ended in it
-                                    //   (wf_fold_gen on the B streams), no frame-end fold
-    uint64_t o_dn, o_rd;            // eager: chain ends found by wf_nearest, their region sizes
-    uint64_t o_cpix;                // the pixel of each chain
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
@@ -314,7 +286,7 @@ struct WfBufs {
     // records (index = k * qcap + entry): f = 0..2 point, 3..5 direction, 6 significance
     RT_HD uint64_t rn() const { return static_cast<uint64_t>(levels) * qcap; }
     RT_HD double* rf(int f) const { return reinterpret_cast<double*>(mem + o_rec) + f * rn(); }
-    RT_HD uint32_t* ru(int f) const {             // 0 object, 1 primitive, 2 pixel, 3 occlusion
+    RT_HD uint32_t* ru(int f) const {             // 0 object, 1 primitive, 2 chain, 3 occlusion
         return reinterpret_cast<uint32_t*>(reinterpret_cast<double*>(mem + o_rec) + 7 * rn()) + f * rn();
     }
     // levels (index = k * capa + chain): f = 0..2 colour, 3 Schlick factor
@@ -327,19 +299,7 @@ struct WfBufs {
     RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
-    RT_HD uint32_t* oq() const { return reinterpret_cast<uint32_t*>(mem + o_oq); }
-    RT_HD uint32_t* ro() const { return reinterpret_cast<uint32_t*>(mem + o_ro); }
-    // eager fold: chain ends of generation k found by wf_nearest (index = k * qcap + entry):
-    // the pixel and the object whose ambient colour ends it (INT32_MAX: background)
-    RT_HD uint32_t* dpix() const { return reinterpret_cast<uint32_t*>(mem + o_dn); }
-    RT_HD int32_t* dobj() const {
-        return reinterpret_cast<int32_t*>(mem + o_dn) + static_cast<uint64_t>(levels + 1) * qcap;
-    }
-    RT_HD uint32_t* rd() const { return reinterpret_cast<uint32_t*>(mem + o_rd); }
 };
-// eager fold: wf_shade marks a record whose chain ends there (ru(2) = pixel | kChainEnd)
-// and leaves its final colour in rf(0..2) (the hit point is dead by then)
-constexpr uint32_t kChainEnd = 0x80000000u;
 constexpr uint32_t kNlevRunning = 0xFFu;   // WfBufs::nlev of a chain that has not ended yet
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels

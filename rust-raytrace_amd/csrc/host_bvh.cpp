@@ -14,6 +14,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <limits>
 #include <vector>
 
@@ -262,71 +263,71 @@ Bvh4Result collapse_bvh4(const BvhResult& b2) {
     return out;
 }
 
-// Image-plane rectangle of a box seen from the camera.  A camera ray is
-// dir = normalize(M (px, py, 1)) (camera.rs:78), so a world point X it passes
-// through has M^-1 (X - pos) = s (px, py, 1) with s > 0.  When every corner of
-// the box lies strictly in front of the camera plane (third coordinate > 0),
-// the box's image is the convex hull of the corner images (the perspective map
-// keeps segments straight on that side), so their bounding rectangle holds
-// every (px, py) whose ray meets the box.  A relative 1e-5 margin absorbs the
-// rounding of the ray direction and of this projection (far below a pixel).
-namespace {
-void project_box(const float lo[3], const float hi[3], const double pos[3], const double inv[9], float rect[4],
-                 float& tmin) {
-    double r[4] = {HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
-    bool front = true;
-    for (int c = 0; c < 8 && front; ++c) {
-        const double X[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
-        const double d[3] = {X[0] - pos[0], X[1] - pos[1], X[2] - pos[2]};
-        double q[3];
-        for (int i = 0; i < 3; ++i) q[i] = inv[3 * i] * d[0] + inv[3 * i + 1] * d[1] + inv[3 * i + 2] * d[2];
-        const double dn = std::fabs(d[0]) + std::fabs(d[1]) + std::fabs(d[2]);
-        if (!(q[2] > 1e-9 * dn) || !std::isfinite(q[0]) || !std::isfinite(q[1])) { front = false; break; }
-        const double px = q[0] / q[2], py = q[1] / q[2];
-        r[0] = std::min(r[0], px); r[1] = std::min(r[1], py);
-        r[2] = std::max(r[2], px); r[3] = std::max(r[3], py);
-    }
-    if (!front) {
-        rect[0] = rect[1] = -HUGE_VALF;
-        rect[2] = rect[3] = HUGE_VALF;
-    } else {
-        for (int i = 0; i < 2; ++i) rect[i] = down(r[i] - 1e-5 * (1.0 + std::fabs(r[i])));
-        for (int i = 2; i < 4; ++i) rect[i] = up(r[i] + 1e-5 * (1.0 + std::fabs(r[i])));
-    }
-    // distance from the camera to the box: a hit inside it is at t >= this
-    // (unit direction up to rounding; the 1e-6 relative cut covers that)
-    double dd = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        const double v = pos[a] < lo[a] ? lo[a] - pos[a] : (pos[a] > hi[a] ? pos[a] - hi[a] : 0.0);
-        dd += v * v;
-    }
-    const double dist = std::sqrt(dd) * (1.0 - 1e-6);
-    tmin = std::isfinite(dist) ? down(dist) : 0.0f;
-}
-}  // namespace
-
-std::vector<DevCamNode> camera_nodes(const BvhResult& b2, const double pos[3], const double m[9]) {
-    std::vector<DevCamNode> out(b2.nodes.size());
-    // M^-1 by the adjugate
-    const double a = m[0], b = m[1], c = m[2], d = m[3], e = m[4], f = m[5], g = m[6], h = m[7], i = m[8];
-    const double det = a * (e * i - f * h) - b * (d * i - f * g) + c * (d * h - e * g);
-    const double inv[9] = {(e * i - f * h) / det, (c * h - b * i) / det, (b * f - c * e) / det,
-                           (f * g - d * i) / det, (a * i - c * g) / det, (c * d - a * f) / det,
-                           (d * h - e * g) / det, (b * g - a * h) / det, (a * e - b * d) / det};
-    bool ok = std::isfinite(det) && det != 0.0;
-    for (double v : inv) ok = ok && std::isfinite(v);
-    for (size_t k = 0; k < b2.nodes.size(); ++k) {
-        const DevBvhNode& n = b2.nodes[k];
-        DevCamNode& o = out[k];
-        if (ok) {
-            project_box(n.lo0, n.hi0, pos, inv, o.r0, o.tmin0);
-            project_box(n.lo1, n.hi1, pos, inv, o.r1, o.tmin1);
-        } else {                                  // degenerate camera: every box everywhere
-            for (float* r : {o.r0, o.r1}) { r[0] = r[1] = -HUGE_VALF; r[2] = r[3] = HUGE_VALF; }
-            o.tmin0 = o.tmin1 = 0.0f;
+// Quantise the 4-wide tree (DevQNode4).  Per node and axis, the frame step is
+// the smallest power of two s = 2^e (e >= -100) for which the node's f32 box
+// [L, H] spans at most 255 steps from m = floor(L / s) and m fits 24 bits
+// signed; child bounds round outward to whole steps: lo' = floor(lo / s) * s,
+// hi' = ceil(hi / s) * s.  Every quantity is a power-of-two multiple of an f32,
+// so the double arithmetic here is exact, and so is the device's decode
+// fma(q, s, m * s) = (m + q) * s (an integer below 2^24 times a power of two
+// in the normal range).
+std::vector<DevQNode4> quantize_bvh4(const Bvh4Result& b4) {
+    const int32_t N = b4.n_nodes;
+    if (N <= 0 || N >= 0x8000 || b4.root != 0) return {};
+    std::vector<DevQNode4> out(static_cast<size_t>(N));
+    for (int32_t i = 0; i < N; ++i) {
+        DevQNode4& q = out[i];
+        std::memset(&q, 0, sizeof q);
+        const DevBvh4Plane& ch = b4.planes[static_cast<size_t>(6) * N + i];
+        bool used[4];
+        int32_t first_leaf = INT32_MAX;
+        for (int k = 0; k < 4; ++k) {
+            used[k] = ch.i[k] != kBvh4Empty;
+            if (used[k] && ch.i[k] < 0) first_leaf = std::min(first_leaf, (~ch.i[k]) >> 3);
         }
-        o.c0 = n.c0;
-        o.c1 = n.c1;
+        q.base = first_leaf == INT32_MAX ? 0u : static_cast<uint32_t>(first_leaf);
+        for (int k = 0; k < 4; ++k) {
+            if (!used[k]) { q.child[k] = kQ4Empty; continue; }
+            const int32_t c = ch.i[k];
+            if (c >= 0) { q.child[k] = static_cast<uint16_t>(c); continue; }
+            const int32_t off = ((~c) >> 3) - first_leaf, cnt = ((~c) & 7) + 1;
+            if (off > 4094) return {};
+            q.child[k] = static_cast<uint16_t>(kQ4Leaf | (off << 3) | (cnt - 1));
+        }
+        for (int a = 0; a < 3; ++a) {
+            const DevBvh4Plane& P0 = b4.planes[static_cast<size_t>(2 * a) * N + i];
+            const DevBvh4Plane& P1 = b4.planes[static_cast<size_t>(2 * a + 1) * N + i];
+            double L = HUGE_VAL, H = -HUGE_VAL;
+            for (int k = 0; k < 4; ++k) {
+                if (!used[k]) continue;
+                if (!std::isfinite(P0.f[k]) || !std::isfinite(P1.f[k]) || !(P0.f[k] <= P1.f[k])) return {};
+                L = std::min(L, static_cast<double>(P0.f[k]));
+                H = std::max(H, static_cast<double>(P1.f[k]));
+            }
+            if (!(L <= H)) { L = 0.0; H = 0.0; }       // no child (cannot happen for a collapsed node)
+            int e = -100;
+            if (H > L) e = std::max(e, static_cast<int>(std::ceil(std::log2((H - L) / 255.0))) - 1);
+            double m = 0.0, s = 0.0;
+            for (;; ++e) {
+                if (e > 104) return {};
+                s = std::ldexp(1.0, e);
+                m = std::floor(L / s);
+                if (m < -8388608.0 || m > 8388607.0) continue;
+                if (std::ceil(H / s) - m <= 255.0) break;
+            }
+            uint32_t lo = 0, hi = 0;
+            for (int k = 0; k < 4; ++k) {
+                if (!used[k]) continue;
+                const double ql = std::floor(P0.f[k] / s) - m, qh = std::ceil(P1.f[k] / s) - m;
+                if (!(ql >= 0.0 && qh <= 255.0 && ql <= qh)) return {};
+                lo |= static_cast<uint32_t>(ql) << (8 * k);
+                hi |= static_cast<uint32_t>(qh) << (8 * k);
+            }
+            q.frame[a] = static_cast<int32_t>((static_cast<uint32_t>(static_cast<int32_t>(m)) & 0xFFFFFFu) |
+                                              (static_cast<uint32_t>(e + 127) << 24));
+            q.lo[a] = lo;
+            q.hi[a] = hi;
+        }
     }
     return out;
 }
@@ -398,64 +399,6 @@ std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2) {
         }
         h.c0 = n.c0;
         h.c1 = n.c1;
-    }
-    return out;
-}
-
-ClusterResult build_clusters(const BvhResult& b2, size_t n_spheres) {
-    ClusterResult out;
-    if (n_spheres == 0) return out;
-    // (first, count) of every subtree: the builder partitions in place, so a
-    // subtree's spheres are one contiguous range of the leaf order
-    auto range = [&](int32_t ptr, auto&& self) -> std::pair<int32_t, int32_t> {
-        if (ptr < 0) return {(~ptr) >> 3, ((~ptr) & 7) + 1};
-        const auto a = self(b2.nodes[ptr].c0, self), b = self(b2.nodes[ptr].c1, self);
-        return {std::min(a.first, b.first), a.second + b.second};
-    };
-    auto cut = [&](int32_t ptr, const float lo[3], const float hi[3], auto&& self) -> void {
-        const auto r = range(ptr, range);
-        if (ptr < 0 || r.second <= kClusterMax) {
-            DevCluster c{};
-            for (int k = 0; k < 3; ++k) { c.lo[k] = lo[k]; c.hi[k] = hi[k]; }
-            c.first = r.first;
-            c.count = r.second;
-            out.clusters.push_back(c);
-            return;
-        }
-        const DevBvhNode& nd = b2.nodes[ptr];
-        self(nd.c0, nd.lo0, nd.hi0, self);
-        self(nd.c1, nd.lo1, nd.hi1, self);
-    };
-    const float inf = std::numeric_limits<float>::infinity();
-    const float all_lo[3] = {-inf, -inf, -inf}, all_hi[3] = {inf, inf, inf};
-    if (b2.root < 0) {                                   // the whole set is one leaf: one cluster, any ray tests it
-        cut(b2.root, all_lo, all_hi, cut);
-    } else {
-        const DevBvhNode& r = b2.nodes[b2.root];
-        cut(r.c0, r.lo0, r.hi0, cut);
-        cut(r.c1, r.lo1, r.hi1, cut);
-    }
-    const size_t n = out.clusters.size();
-    if (n > static_cast<size_t>(64 * kClusterSlotsMax) || n >= kClusterNone) { out.clusters.clear(); return out; }
-    out.slots = static_cast<int>((n + 63) / 64);
-    const size_t ns = static_cast<size_t>(64) * out.slots;
-    out.perm.assign(8 * ns, kClusterNone);
-    std::vector<uint16_t> ids(n);
-    for (int o = 0; o < 8; ++o) {
-        // octant o: bit a set = the ray's direction component a is negative; clusters
-        // sorted by centre . s (s_a = +1 / -1), so the ones a ray meets first come first
-        const double sx = (o & 1) ? -1.0 : 1.0, sy = (o & 2) ? -1.0 : 1.0, sz = (o & 4) ? -1.0 : 1.0;
-        auto key = [&](uint16_t i) {
-            const DevCluster& c = out.clusters[i];
-            const double cx = 0.5 * (static_cast<double>(c.lo[0]) + c.hi[0]);
-            const double cy = 0.5 * (static_cast<double>(c.lo[1]) + c.hi[1]);
-            const double cz = 0.5 * (static_cast<double>(c.lo[2]) + c.hi[2]);
-            const double k = sx * cx + sy * cy + sz * cz;
-            return std::isfinite(k) ? k : -HUGE_VAL;
-        };
-        for (size_t i = 0; i < n; ++i) ids[i] = static_cast<uint16_t>(i);
-        std::stable_sort(ids.begin(), ids.end(), [&](uint16_t a, uint16_t b) { return key(a) < key(b); });
-        for (size_t i = 0; i < n; ++i) out.perm[o * ns + i] = ids[i];
     }
     return out;
 }

@@ -55,15 +55,11 @@ struct LaunchMarks {
 };
 
 hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mode, hipStream_t stream);
-// Sphere sources (trace_kernel.hip, kSrc*): 0 brute force from HBM/L2, 1 brute
-// force staged in LDS, 2 binary BVH from HBM/L2, 4 binary BVH + spheres in
-// LDS, 7 = 4 held to 64 VGPRs, 10 4-wide BVH + spheres in LDS (64 VGPRs),
-// 11 4-wide BVH from HBM/L2, 12 = 10 with 128 VGPRs.  Supported (nearest,
-// occlusion) pairs: (s, s) for every s, (7, 10), (2, 11).
 // The streams of one wavefront lane: a runs the nearest-hit chain and the
 // fold; the shadow + shading kernels of generation k run on b[k % nb] (b[i] ==
 // a: one in-order stream).  near_done: kMaxGenerations events; b_done: one
-// per b stream; marks may be null.  fuse: shading inside the shadow kernel.
+// per b stream; marks may be null.  Sphere sources and the supported
+// (nearest, shadow) pairs: trace_kernel.hip kSrc* and launch_wavefront.
 constexpr int kMaxBStreams = 4;
 struct WfStreams {
     hipStream_t a;
@@ -73,26 +69,14 @@ struct WfStreams {
     hipEvent_t b_done[kMaxBStreams];
     LaunchMarks* ma;
     LaunchMarks* mb[kMaxBStreams];
-    bool fuse;
-    int cam;            // generation 0: 0 per-ray traversal, 1 camera tiles (LDS), 2 camera tiles (HBM/L2)
-    bool lists0;        // shadow item lists from generation 0 (else from generation 1)
-    int fuse_from;      // generations >= fuse_from shade inside the shadow kernel (one B launch instead of two)
+    int cam;            // generation 0: 0 per-ray traversal of the nearest-hit source, 3 / 4 the camera's view
+                        // grid with the spheres in LDS / through L2
     int grid_occ;       // every light has a light-view grid: shadow kernel without a tree walk,
                         // spheres from LDS (1) or HBM/L2 (2); 0: the general shadow kernel
     hipEvent_t* fold_ev;// recorded once the chunk's pixels are final (null: no event)
-    hipEvent_t* gen_done; // eager fold (WfBufs::eager): kMaxGenerations events, generation k's
-                          //   wf_fold_gen done (the next generation's fold waits for it); split
-                          //   fold: gen_done[K-1] = generation K-1's shading done
-    int fold_split;       // > 0: chains that ended by generation K = fold_split are folded on
-                          //   generation K's b stream (with two b streams), the rest at the end
-    int bmerge;           // > 0: generations >= bmerge get no shadow / shading launches of their own;
-                          //   one occlusion + one shading launch over all their records follow the
-                          //   last nearest-hit launch on stream a (the latency-bound tail)
     int tail_fuse;        // > 0: the chains running at generation tail_fuse - 1 finish in one wf_tail
     int tail_wgs;         //   launch on stream a (that many workgroups, all resident: one per CU;
-    int tail_width;       //   chains per wave, 0 auto)
-    int tail_fold;        //   1: it folds its chains (after the B streams), the others fold on b[0]
-    int tail_shade;       //   it also shades the records of generations T-1-tail_shade .. T-2 (tail_fold 0)
+    int tail_width;       //   chains per wave, 0 auto), which folds them; the others fold on b[0]
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kPathBlock, RT_PATH_WAVES) void path_kernel(DevScen
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     double* s_srgb = reinterpret_cast<double*>(lds);
     for (int i = threadIdx.x; i < 255; i += kPathBlock) s_srgb[i] = fp.srgb[i];
-    BvhView v{nullptr, 0, nullptr, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
+    BvhView v = global_view(sc);
     if constexpr (kNodes == 2) {
         v.lnodes = stage_node_planes<kPathBlock>(sc.bvh, sc.n_bvh, lds + 2048);
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds + 2048 + node_planes_bytes(sc.n_bvh));

@@ -32,63 +32,47 @@ namespace {
 // measured-best settings; nothing is read from the environment,
 // so a render's schedule depends only on the scene, the options and these.
 enum TuneKey : int {
-    kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2,
-    kTunePrefixKb4, kTuneLanes, kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneFuse,
-    kTuneLists, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTuneLists0, kTunePathGroup, kTuneCuMask, kTunePrio,
-    kTuneVerbose, kTuneGridOcc, kTuneFuseFrom, kTuneCompact, kTuneHalf, kTuneCamPrefix, kTuneWfBudgetMb, kTuneTailFrom, kTuneTailMax, kTuneEagerFold, kTuneFoldSplit, kTuneBMerge, kTuneWaveMax, kTuneCamGridRes, kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneTailFold, kTuneTailShade, kTuneFoldWgs, kTuneShadeWgs, kTuneCount
+    kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
+    kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
+    kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCount
 };
 struct TuneDef {
     const char* name;
     int64_t dflt, lo, hi;
 };
-// -1 in src / src_occ / cam / split: chosen per scene
+// -1 in src / src_occ / cam / split: chosen per scene.  Round 5 removed the knobs of
+// variants measured slower and off by default (DESIGN.md §9 keeps their rows): fuse,
+// lists, lists0, fuse_from, prefix4_kb, cam_prefix_kb, tail_from, tail_max, eager_fold,
+// fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs, shade_wgs.
 constexpr TuneDef kTune[kTuneCount] = {
     {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what the working-set budget holds at the depth)
     {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
     {"light_grids", 1, 0, 1},                    // light-view grids for point-light shadow queries
     {"light_grid_res", 0, 0, 4096},              // 0: from the median sphere's angular size
-    {"src", -1, -1, 13},                         // nearest-hit sphere source (trace_kernel.hip kSrc*)
-    {"src_occ", -1, -1, 13},                     // shadow sphere source
+    {"src", -1, -1, 26},                         // nearest-hit sphere source (trace_kernel.hip kSrc*)
+    {"src_occ", -1, -1, 26},                     // shadow sphere source
     // LDS prefixes stay <= 150 KB: with the queue counters (<= 8.4 KB at 2048 regions) a
     // workgroup's LDS then fits gfx950's 160 KB
-    {"prefix_kb", 64, 1, 150},                   // LDS prefix of the binary tree (KB) for trees that do not fit
-    {"prefix4_kb", 0, 0, 150},                   // LDS prefix of the 4-wide tree (0: read through L2)
+    {"prefix_kb", 64, 1, 150},                   // LDS prefix of the binary (or quantised) tree (KB) for trees beyond LDS
     {"lanes", 1, 1, 8},                          // chunk lanes (each its own streams and working set)
     {"stagger_gen", 1, 0, 64},                   // lanes: chunk c+1 starts after this generation of chunk c
     {"regions", 0, 0, 2048},                     // regions per queue (0: 2 x CUs)
     {"split", -1, -1, 1},                        // 0: every wavefront kernel on one in-order stream (-1: per tree)
     {"bstreams", 2, 1, 4},                       // streams for the shadow + shading kernels
-    {"fuse", 0, 0, 1},                           // shading inside the shadow kernel
-    {"lists", 1, 0, 1},                          // shadow item lists (with fuse)
-    {"cam", -1, -1, 3},                          // generation 0: 0 per ray, 1 camera tiles in LDS, 2 from L2, 3 the
-                                                 // camera's view grid
+    {"cam", -1, -1, 3},                          // generation 0: 3 the camera's view grid (-1: where built), else per ray
     {"deal", 1, 0, 1},                           // chunk dealing: 1 workgroup-major, 0 workgroup-first
     {"spread_below", 0, 0, INT32_MAX},           // queues below this size are dealt workgroup-first
-    {"lists0", 0, 0, 1},                         // shadow lists from generation 0
     {"path_group", 0, 0, 64},                    // path kernel: lanes per pixel (0: auto)
     {"cu_mask", 1, 0, 4},                        // b streams CU-masked (own hardware queue): 1 every CU, 2/3/4 only 3/4, 1/2, 1/4 of them
     {"prio", 1, 0, 1},                           // nearest-hit chain on a high-priority stream (round 4: C3 2.969-2.974
                                                  // vs 2.983-2.998 ms, 8-way share 0.713 vs 0.741 ms, C4 equal; same box)
-    {"verbose", 0, 0, 1},                        // print the chosen schedule to stderr
+    {"verbose", 0, 0, 1},                        // print the chosen schedule (and a working set that does not fit) to stderr
     {"grid_occ", 1, 0, 1},                       // shadow kernel without a tree walk when every light has a grid
-    {"fuse_from", 99, 0, 99},                    // generations >= this shade inside the shadow kernel (one B launch)
     {"compact_stack", 1, 0, 1},                  // 32-bit nearest-hit stack entries, 32 of them (src 9; src 6 for half-node trees)
     {"half_nodes", 1, 0, 1},                     // trees beyond LDS: binary16 node bounds for the prefix source (src 5)
-    {"cam_prefix_kb", 64, 0, 120},               // camera nodes from L2 (cam 2): the breadth-first top staged in LDS
     {"wf_budget_mb", 0, 0, INT32_MAX},           // wavefront working set of all lanes together (MB; 0: min(80 GB,
                                                  // 85% of the device's free memory)); chunks are sized to it
-    {"tail_from", -1, -1, 99},                   // nearest-hit generations >= this (src 9 trees) hand queues of <= tail_max
-                                                 // rays to the quad walk; 0 off, -1: 5 for chunks of <= 32 x tail_max slots
-    {"tail_max", 0, 0, INT32_MAX},               // 0: CUs x 256 (one quad-walk round: one workgroup of 256 rays per CU)
-    {"eager_fold", 0, 0, 1},                     // 1: each generation folds the chains that ended in it (B streams;
-                                                 // measured slower: scattered level gathers);
-                                                 // 0: one fold over every chain after the last generation
-    {"fold_split", 0, 0, 32},                    // K > 0: chains that ended by generation K fold on a B stream
-                                                 // during the later generations, the rest after the last one
-    {"bmerge", 0, -1, 32},                       // T > 0: generations >= T shade in one occlusion + one shading
-                                                 // launch after the last nearest-hit launch; 0 off, -1 auto
-    {"wave_max", -1, -1, INT32_MAX},             // src 9, generations >= 1: queues of <= this many rays take the
-                                                 // wave-cooperative query (nearest_wave); 0 off, -1 auto
     {"cam_grid_res", 0, -1, 4096},               // the camera's view grid: cells per face side (0: from the scene's
                                                  // frame size, -1: no grid); takes effect at the next rt_scene_upload
     {"a_queue", 0, 0, 1},                        // 1: the nearest-hit chain's stream CU-masked (a hardware queue of its
@@ -96,11 +80,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"tail_fuse", -1, -1, 32},                   // > 0: the chains running at generation tail_fuse - 1 of a src-9 frame whose
                                                  // lights all have light-view grids finish in one launch (wf_tail); 0 off, -1 auto
     {"tail_width", 0, 0, 64},                    // ... with this many chains per wave (0: auto)
-    {"tail_fold", 1, 0, 1},                      // ... 1: which also folds them (after the shading streams)
-    {"tail_shade", 1, 0, 8},                     // ... which also shades the records of this many generations before
-                                                 // T-1 (tail_fold 0)
-    {"fold_wgs", 0, -1, 2048},                   // workgroups of a wf_fold launch (0: G regions, -1 auto: one per CU)
-    {"shade_wgs", 0, -1, 2048},                  // workgroups of a wf_shade launch (0: G regions, -1 auto: one per CU)
+    {"qtree", 0, 0, 1},                          // 1: trees beyond the f32 tree's LDS budget take the quantised 4-wide
+                                                 // tree (src 25 whole in LDS, 26 LDS prefix + L2) for the nearest hit;
+                                                 // measured slower than binary16 (C4 55.0 vs 50.4 ms, C5 330 vs 307 ms)
 };
 
 }  // namespace
@@ -221,12 +203,10 @@ struct rt_ctx {
     DevScene dsc{};
     bool has_scene = false;
     bool deep_bvh4 = false;          // the 4-wide tree could overflow the traversal stack: binary tree only
-    bool quad_ok = false;            // the quad walk's LDS stack holds the 4-wide tree's deepest walk (compact codes)
     bool short_stack = false;        // binary tree fits the compact nearest-hit stack (16-bit codes, depth <= 32)
     bool short_stack18 = false;      // ... with 18-bit codes (the binary16 prefix source, src 6)
+    bool q4_ok = false;              // the quantised 4-wide tree was built (DevScene::q4)
     bool all_lights_gridded = false; // every light is a point light with a light-view grid
-    int32_t cl_slots = 0;            // the uploaded scene's cluster slots (DevScene::cl_slots: 0 per render
-                                     // when the clusters would not fit the nearest-hit kernel's LDS budget)
     unsigned long long* d_counters = nullptr;
     double* d_srgb = nullptr;         // the 255 sRGB thresholds (path kernel)
     void* d_path = nullptr;           // path kernel recursion stack (PathStack)
@@ -248,7 +228,6 @@ struct rt_ctx {
         hipEvent_t mark = nullptr, done = nullptr;
         std::vector<hipEvent_t> b_done;    // one per sb stream
         std::vector<hipEvent_t> near_done; // per generation: nearest-hit kernel finished (s -> sb)
-        std::vector<hipEvent_t> gen_done;  // per generation: its eager fold finished (sb -> next sb)
         void* mem = nullptr;
         size_t bytes = 0;
         WfBufs b{};
@@ -375,7 +354,6 @@ void drop_lanes(rt_ctx* c) {
         if (L.done) (void)hipEventDestroy(L.done);
         for (hipEvent_t e : L.b_done) if (e) (void)hipEventDestroy(e);
         for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : L.gen_done) if (e) (void)hipEventDestroy(e);
         if (L.s) (void)hipStreamDestroy(L.s);
         for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
     }
@@ -384,11 +362,8 @@ void drop_lanes(rt_ctx* c) {
 
 // Working-set bytes per pixel slot of a chunk (ensure_wf's sections, per slot):
 // two queues, one shade-record array and one level array per lit generation,
-// terminals, shadow item lists, the eager fold's chain-end lists (one per generation).
-uint64_t wf_bytes_per_slot(uint64_t levels, uint64_t nlists) {
-    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + levels * std::max<uint64_t>(1, nlists) * 4 +
-           (levels + 1) * 8 + 4;
-}
+// terminals and level counts, the chain's pixel.
+uint64_t wf_bytes_per_slot(uint64_t levels) { return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + 4; }
 
 // Default working-set budget of a render (all lanes): 85% of what the device
 // has free plus what this context's lanes already hold, at most kWfBudget.
@@ -423,8 +398,6 @@ int ensure_lanes(rt_ctx* c, int n) {
         HIP_TRY(c, hipEventCreateWithFlags(&M.done, hipEventDisableTiming));
         M.near_done.assign(kMaxGenerations, nullptr);
         for (hipEvent_t& e : M.near_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        M.gen_done.assign(kMaxGenerations, nullptr);
-        for (hipEvent_t& e : M.gen_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     return RT_OK;
 }
@@ -432,20 +405,16 @@ int ensure_lanes(rt_ctx* c, int n) {
 // Carve a lane's wavefront working set for chunks of up to `cap` pixels: every
 // queue and shade-record array is G regions of R entries; the shade records
 // have one such array per lit generation (`levels` = max_depth + 1).
-int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels, uint32_t nlists) {
+int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, uint32_t levels) {
     WfBufs& b = L.b;
     const uint64_t q = static_cast<uint64_t>(G) * R;   // queue capacity (>= generation-0 slots)
     const uint64_t capa = align_up(q, 64);               // per-chain arrays (chain = generation-0 record entry)
-    const uint64_t nl = std::max(1u, nlists);
     // section sizes (device_layout.hpp, WfBufs)
     const uint64_t s_queue = 2ull * 8 * q * 8;
     const uint64_t s_rec = static_cast<uint64_t>(levels) * q * (7 * 8 + 4 * 4);
     const uint64_t s_lev = static_cast<uint64_t>(levels) * capa * (4 * 8 + 4);
     const uint64_t s_term = capa * (3 * 8 + 1);
     const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
-    const uint64_t s_oq = static_cast<uint64_t>(levels) * nl * q * 4;
-    const uint64_t s_ro = static_cast<uint64_t>(kMaxGenerations) * nl * G * 4;
-    const uint64_t s_dn = (static_cast<uint64_t>(levels) + 1) * q * 8;
     const uint64_t s_cpix = q * 4;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
@@ -453,10 +422,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_term = off; off = align_up(off + s_term, 256);
     b.o_rq = off; off = align_up(off + s_reg, 256);
     b.o_rs = off; off = align_up(off + s_reg, 256);
-    b.o_oq = off; off = align_up(off + s_oq, 256);
-    b.o_ro = off; off = align_up(off + s_ro, 256);
-    b.o_dn = off; off = align_up(off + s_dn, 256);
-    b.o_rd = off; off = align_up(off + s_reg, 256);
     b.o_cpix = off; off = align_up(off + s_cpix, 256);
     if (off > L.bytes) {
         if (L.mem) {
@@ -470,16 +435,26 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         // beyond it is answered without hipMalloc (the runtime has crashed inside a failing
         // hipMalloc of a few hundred GB, seen with an explicit oversized wf_budget_mb), and a
         // working set that took the last free bytes would leave nothing for the scratch the
-        // runtime allocates per hardware queue at a kernel's first launch there
+        // runtime allocates per hardware queue at a kernel's first launch there.  The free
+        // memory is the device's: other contexts and processes count, so the caller's halving
+        // of the chunks is reported under tuning verbose and in rt_stats.chunks.
         size_t fr = 0, total = 0;
-        if (hipMemGetInfo(&fr, &total) == hipSuccess && (off > fr || fr - off < kRuntimeHeadroom))
+        if (hipMemGetInfo(&fr, &total) == hipSuccess && (off > fr || fr - off < kRuntimeHeadroom)) {
+            if (c->t(kTuneVerbose))
+                std::fprintf(stderr, "rtamd: working set of %llu MB does not fit %llu MB free (less %llu MB headroom): "
+                             "halving the chunk\n", static_cast<unsigned long long>(off >> 20),
+                             static_cast<unsigned long long>(fr >> 20), static_cast<unsigned long long>(kRuntimeHeadroom >> 20));
             return fail(c, RT_E_NOMEM, "wavefront working set of " + std::to_string(off >> 20) + " MB does not fit (" +
                                            std::to_string(fr >> 20) + " MB free)");
+        }
         (void)hipGetLastError();
         const hipError_t e = hipMalloc(&L.mem, off);
         if (e == hipErrorOutOfMemory) {          // the caller retries with smaller chunks
             (void)hipGetLastError();
             L.mem = nullptr;
+            if (c->t(kTuneVerbose))
+                std::fprintf(stderr, "rtamd: hipMalloc of %llu MB failed: halving the chunk\n",
+                             static_cast<unsigned long long>(off >> 20));
             return fail(c, RT_E_NOMEM, "wavefront working set of " + std::to_string(off >> 20) + " MB does not fit");
         }
         if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(wavefront working set)");
@@ -492,7 +467,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.cap = cap;
     b.capa = static_cast<uint32_t>(capa);
     b.levels = levels;
-    b.nlists = nlists;
     b.G = G;
     b.R = R;
     return RT_OK;
@@ -631,6 +605,8 @@ static int view_grid_res(const rt_scene* s, int64_t forced) {
     return std::isfinite(imd) ? static_cast<int>(std::lround(std::clamp(imd * side / 8.0, 16.0, 2048.0))) : 64;
 }
 constexpr size_t kViewGridEntries = size_t{32} << 20;
+// the view grid's list entries: at most 32 M, and about 4096 per sphere (C3 holds 395 per sphere)
+static size_t view_grid_cap(size_t n_spheres) { return std::min(kViewGridEntries, (size_t{1} << 20) + 4096 * n_spheres); }
 
 int rt_view_grid_candidates(const rt_scene* s, int resolution, const double* dirs, uint32_t n_dirs, int32_t* counts,
                             int32_t* ids, float* nears, size_t cap, int64_t* info) {
@@ -653,7 +629,7 @@ int rt_view_grid_candidates(const rt_scene* s, int resolution, const double* dir
                     if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
         }
         const LightGridResult g = build_view_grid(spheres, srad, s->camera.position, 1e-5 * (1.0 + extent),
-                                                  view_grid_res(s, resolution), kViewGridEntries);
+                                                  view_grid_res(s, resolution), view_grid_cap(spheres.size()));
         const DevLightGrid& G = g.grids[0];
         if (info) {
             info[0] = G.R;
@@ -695,6 +671,51 @@ int rt_view_grid_candidates(const rt_scene* s, int resolution, const double* dir
         return RT_OK;
     } catch (const std::length_error& e) {
         return fail(nullptr, RT_E_INVALID, e.what());
+    } catch (const std::exception& e) {
+        return fail(nullptr, RT_E_NOMEM, e.what());
+    }
+}
+
+int rt_qtree_nodes(const rt_scene* s, int leaf_max, void* nodes, float* boxes, int32_t* sphere_first,
+                   int32_t* sphere_count, size_t cap_nodes, int64_t* info) {
+    if (!s || leaf_max < 0 || leaf_max > 8 || (cap_nodes && (!nodes || !boxes || !sphere_first || !sphere_count)))
+        return RT_E_INVALID;
+    try {
+        std::vector<double> sx, sy, sz, srad;
+        double extent = 0.0;
+        for (const rt_object& o : s->objects) {
+            if (o.shape != RT_SHAPE_SPHERE) continue;
+            sx.push_back(o.geom[0]); sy.push_back(o.geom[1]); sz.push_back(o.geom[2]); srad.push_back(o.geom[3]);
+            const double r = std::fabs(o.geom[3]);
+            for (int k = 0; k < 3; ++k)
+                for (double v : {o.geom[k] - r, o.geom[k] + r})
+                    if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
+        }
+        const double pad = 1e-5 * (1.0 + extent);
+        // scene_upload's leaf rule: 2, or 4 when that tree and the spheres would not fit the LDS budget
+        int leaf = leaf_max > 0 ? leaf_max : 2;
+        BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf);
+        if (leaf_max == 0 && bvh.nodes.size() * sizeof(DevBvhNode) + sx.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
+            bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf = 4);
+        const Bvh4Result b4 = collapse_bvh4(bvh);
+        const int need = bvh4_stack_need(b4);
+        const std::vector<DevQNode4> q = need <= kQ4Stack ? quantize_bvh4(b4) : std::vector<DevQNode4>{};
+        if (info) { info[0] = static_cast<int64_t>(q.size()); info[1] = need; info[2] = leaf; }
+        if (q.size() > cap_nodes) return q.empty() ? RT_OK : fail(nullptr, RT_E_INVALID, "node buffer too small");
+        const int32_t N = b4.n_nodes;
+        std::memcpy(nodes, q.data(), q.size() * sizeof(DevQNode4));
+        for (size_t i = 0; i < q.size(); ++i)
+            for (int k = 0; k < 4; ++k) {
+                const int32_t ch = b4.planes[static_cast<size_t>(6) * N + i].i[k];
+                for (int a = 0; a < 3; ++a) {
+                    boxes[(i * 4 + k) * 6 + a] = ch == kBvh4Empty ? NAN : b4.planes[static_cast<size_t>(2 * a) * N + i].f[k];
+                    boxes[(i * 4 + k) * 6 + 3 + a] = ch == kBvh4Empty ? NAN : b4.planes[static_cast<size_t>(2 * a + 1) * N + i].f[k];
+                }
+                const bool leafc = ch != kBvh4Empty && ch < 0;
+                sphere_first[i * 4 + k] = leafc ? (~ch) >> 3 : -1;
+                sphere_count[i * 4 + k] = leafc ? ((~ch) & 7) + 1 : 0;
+            }
+        return RT_OK;
     } catch (const std::exception& e) {
         return fail(nullptr, RT_E_NOMEM, e.what());
     }
@@ -780,17 +801,17 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     // traversal stacks hold 64 entries (trace_common.hpp kBvhStack / kBvh4Stack)
     if (bvh_depth(bvh) > 64) return fail(c, RT_E_UNSUPPORTED, "sphere BVH deeper than the traversal stack");
     c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
-    c->quad_ok = bvh4_stack_need(bvh4) <= 48 && bvh4.n_nodes < 32768 && spheres.size() <= 4096;
     // compact stack (trace_common.hpp kShortStack, stk_entry16): the stack never holds more
     // entries than the deepest inner node's depth; node indices and leaf codes
     // (first << 3 | count - 1) must fit a signed 16-bit field
     c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 32768 && spheres.size() <= 4096;
     c->short_stack18 = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 131072 && spheres.size() <= 16383;
-    const std::vector<DevCamNode> camn = camera_nodes(bvh, s->camera.position, s->camera.matrix);
-    const ClusterResult cls = build_clusters(bvh, spheres.size());
     // binary16 nodes only for trees that do not fit LDS whole (the prefix source reads them)
     const bool big_tree = bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget;
     const std::vector<DevBvhNodeH> hnodes = big_tree ? half_nodes(bvh) : std::vector<DevBvhNodeH>{};
+    // the quantised 4-wide tree (nearest_q4's stack holds kQ4Stack entries), for every tree
+    // (tuning qtree, or src 25 / 26, select it)
+    const std::vector<DevQNode4> qnodes = bvh4_stack_need(bvh4) <= kQ4Stack ? quantize_bvh4(bvh4) : std::vector<DevQNode4>{};
     std::vector<double> r_leaf(spheres.size());
     {
         std::vector<DevSphere> s2(spheres.size());
@@ -805,11 +826,12 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     LightGridResult lg;
     if (c->t(kTuneLgrid) != 0) lg = build_light_grids(spheres, r_leaf, lights, pad, static_cast<int>(c->t(kTuneLgridRes)));
     // the camera's view grid (generation 0, tuning "cam" 3): a cell about 8 x 8 pixels of the
-    // scene's own frame size, im_dist * max(W, H) / 8 cells per face side (tuning "cam_grid_res")
+    // scene's own frame size, im_dist * max(W, H) / 8 cells per face side (tuning "cam_grid_res");
+    // only for scenes the wavefront schedule can render (the path kernel never reads it)
     LightGridResult cg;
-    if (s->camera.kind == RT_CAMERA_SIMPLE && c->t(kTuneCamGridRes) >= 0)
+    if (s->camera.kind == RT_CAMERA_SIMPLE && !needs_path && c->t(kTuneCamGridRes) >= 0)
         cg = build_view_grid(spheres, r_leaf, s->camera.position, pad, view_grid_res(s, c->t(kTuneCamGridRes)),
-                             kViewGridEntries);
+                             view_grid_cap(spheres.size()));
     // One blob: [spheres][sphere_obj][planes][plane_obj][mats][lights][bvh], 256-B aligned pieces.
     size_t off = 0;
     auto place = [&](size_t bytes) { size_t at = off; off = align_up(off + bytes, 256); return at; };
@@ -821,8 +843,8 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_li = place(lights.size() * sizeof(DevLight));
     const size_t o_bvh = place(bvh.nodes.size() * sizeof(DevBvhNode));
     const size_t o_bvh4 = place(bvh4.planes.size() * sizeof(DevBvh4Plane));
-    const size_t o_cam = place(camn.size() * sizeof(DevCamNode));
     const size_t o_bvhh = place(hnodes.size() * sizeof(DevBvhNodeH));
+    const size_t o_q4 = place(qnodes.size() * sizeof(DevQNode4));
     const size_t o_srgbv = place(256 * sizeof(double));
     const size_t o_lg = place(lg.grids.size() * sizeof(DevLightGrid));
     const size_t o_lgoff = place(lg.off.size() * sizeof(uint32_t));
@@ -830,8 +852,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_cg = place(cg.grids.size() * sizeof(DevLightGrid));
     const size_t o_cgoff = place(cg.off.size() * sizeof(uint32_t));
     const size_t o_cgent = place(cg.ent.size() * sizeof(DevLgEntry));
-    const size_t o_cl = place(cls.clusters.size() * sizeof(DevCluster));
-    const size_t o_clp = place(cls.perm.size() * sizeof(uint16_t));
     size_t tex_bytes = 0;
     uint64_t face_off[6] = {0, 0, 0, 0, 0, 0};
     if (skybox)
@@ -848,8 +868,8 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_li, lights.data(), lights.size() * sizeof(DevLight));
     put(o_bvh, bvh.nodes.data(), bvh.nodes.size() * sizeof(DevBvhNode));
     put(o_bvh4, bvh4.planes.data(), bvh4.planes.size() * sizeof(DevBvh4Plane));
-    put(o_cam, camn.data(), camn.size() * sizeof(DevCamNode));
     put(o_bvhh, hnodes.data(), hnodes.size() * sizeof(DevBvhNodeH));
+    put(o_q4, qnodes.data(), qnodes.size() * sizeof(DevQNode4));
     put(o_srgbv, srgb_values_table(), 256 * sizeof(double));
     put(o_lg, lg.grids.data(), lg.grids.size() * sizeof(DevLightGrid));
     put(o_lgoff, lg.off.data(), lg.off.size() * sizeof(uint32_t));
@@ -857,8 +877,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_cg, cg.grids.data(), cg.grids.size() * sizeof(DevLightGrid));
     put(o_cgoff, cg.off.data(), cg.off.size() * sizeof(uint32_t));
     put(o_cgent, cg.ent.data(), cg.ent.size() * sizeof(DevLgEntry));
-    put(o_cl, cls.clusters.data(), cls.clusters.size() * sizeof(DevCluster));
-    put(o_clp, cls.perm.data(), cls.perm.size() * sizeof(uint16_t));
     if (skybox)
         for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
     // every render still reading the old blob (on any stream) must be done before it is overwritten
@@ -888,8 +906,10 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.bvh4 = reinterpret_cast<const DevBvh4Plane*>(base + o_bvh4);
     d.bvh4_root = bvh4.root;
     d.n_bvh4 = bvh4.n_nodes;
-    d.cam_nodes = reinterpret_cast<const DevCamNode*>(base + o_cam);
     d.bvh_h = hnodes.empty() ? nullptr : reinterpret_cast<const DevBvhNodeH*>(base + o_bvhh);
+    d.q4 = qnodes.empty() ? nullptr : reinterpret_cast<const DevQNode4*>(base + o_q4);
+    d.n_q4 = static_cast<int32_t>(qnodes.size());
+    c->q4_ok = !qnodes.empty();
     d.has_fresnel = 0;
     for (const DevMaterial& m : mats) d.has_fresnel |= m.kind == kMatFresnel ? 1 : 0;
     d.needs_path = needs_path ? 1 : 0;
@@ -918,11 +938,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.cgrid = (cg.grids.empty() || cg.grids[0].R <= 0) ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_cg);
     d.cg_off = reinterpret_cast<const uint32_t*>(base + o_cgoff);
     d.cg_ent = reinterpret_cast<const DevLgEntry*>(base + o_cgent);
-    d.clusters = cls.clusters.empty() ? nullptr : reinterpret_cast<const DevCluster*>(base + o_cl);
-    d.cl_perm = reinterpret_cast<const uint16_t*>(base + o_clp);
-    d.n_clusters = static_cast<int32_t>(cls.clusters.size());
-    d.cl_slots = cls.clusters.empty() ? 0 : cls.slots;
-    c->cl_slots = d.cl_slots;
     c->all_lights_gridded = !lights.empty() && lg.grids.size() == lights.size();
     for (const DevLightGrid& g : lg.grids) c->all_lights_gridded = c->all_lights_gridded && g.R > 0;
     c->scene_spp = s->antialias;
@@ -1043,83 +1058,81 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         if (mode == RT_ALGO_WAVEFRONT) {
             const bool fit2 = node_bytes + sph_bytes <= kLdsBudget;
             const bool fit4 = node4_bytes + sph_bytes <= kLdsBudget;
-            // trees too large for LDS: the breadth-first top of each tree in LDS (8, 13)
-            src = fit2 ? 7 : 8;
-            src_occ = fit4 ? 10 : 13;
-            if (!fit2 || !fit4) { src = 8; src_occ = 13; }
-            if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;  // the 4-wide stack could overflow
-            if (src == 7 && src_occ == 10 && c->short_stack && c->t(kTuneCompact) != 0) src = 9;
-            if (src == 8 && c->dsc.bvh_h && c->t(kTuneHalf) != 0) src = 5;
-            if (src == 5 && c->short_stack18 && c->t(kTuneCompact) != 0) src = 6;
-            if (c->t(kTuneSrc) >= 0) {
+            const bool q4_fits = static_cast<size_t>(c->dsc.n_q4) * sizeof(DevQNode4) <= kLdsBudget;
+            const bool compact = c->t(kTuneCompact) != 0;
+            // is (nearest, shadow) source pair (a, o) available for this scene (launch_wavefront's pairs)?
+            auto pair_ok = [&](int a, int o) {
+                if (c->deep_bvh4) return (a == 7 && o == 7 && fit2) || (a == 2 && o == 2);   // the 4-wide stack could overflow
+                switch (a * 100 + o) {
+                case 202: case 211: return true;
+                case 707: case 710: return fit2 && (o == 7 || fit4);
+                case 910: return fit2 && fit4 && c->short_stack;
+                case 511: return c->dsc.bvh_h != nullptr;
+                case 611: return c->dsc.bvh_h != nullptr && c->short_stack18;
+                case 811: return true;
+                case 2511: return c->q4_ok && q4_fits;
+                case 2611: return c->q4_ok;
+                default: return false;
+                }
+            };
+            // Default: both trees whole in LDS with the spheres (measured best at C3), the binary
+            // tree for the nearest hit (compact stack entries where the tree allows) and the 4-wide
+            // tree for shadow rays without a light grid; trees beyond LDS: the binary tree's
+            // breadth-first top in LDS (binary16 bounds where representable, twice the nodes)
+            // and the 4-wide shadow tree through L2; the quantised tree with tuning "qtree".
+            if (fit2 && fit4) {
+                src = c->short_stack && compact ? 9 : 7;
+                src_occ = 10;
+            } else {
+                src = !c->dsc.bvh_h || c->t(kTuneHalf) == 0 ? 8 : c->short_stack18 && compact ? 6 : 5;
+                src_occ = 11;
+                if (c->q4_ok && c->t(kTuneQTree) != 0) src = q4_fits ? 25 : 26;
+            }
+            if (c->deep_bvh4) src_occ = src = fit2 ? 7 : 2;
+            if (c->t(kTuneSrc) >= 0) {                   // forced (A/B measurement, tests)
                 src = static_cast<int>(c->t(kTuneSrc));
                 src_occ = c->t(kTuneSrcOcc) >= 0 ? static_cast<int>(c->t(kTuneSrcOcc)) : src;
             }
-            auto ok = [&](int v) { return v == 2 || v == 4 || v == 7 || v == 8 || (v >= 10 && v <= 13); };
-            const bool pair_ok = ((src == 9 && src_occ == 10 && c->short_stack) ||
-                                  (src == 5 && (src_occ == 13 || src_occ == 11) && c->dsc.bvh_h) ||
-                                  (src == 6 && (src_occ == 13 || src_occ == 11) && c->dsc.bvh_h && c->short_stack18) ||
-                                  (ok(src) && ok(src_occ))) &&
-                                 ((src == src_occ && src != 13) || ((src == 7 || src == 9) && src_occ == 10) ||
-                                  ((src == 5 || src == 6 || src == 8) && (src_occ == 13 || src_occ == 11)) ||
-                                  (src == 2 && src_occ == 11) || (src == 8 && (src_occ == 13 || src_occ == 11)) ||
-                                  (src == 2 && src_occ == 13));
-            const bool fits = !((src == 4 || src == 7 || src == 9) && !fit2) && !((src == 10 || src == 12) && !fit4) &&
-                              !((src_occ == 10 || src_occ == 12) && !fit4);
-            if (!pair_ok || !fits) { src = 2; src_occ = 11; }
-            if (c->deep_bvh4 && src_occ >= 10) src_occ = src = 2;
-            // LDS prefix sizes (tuning "prefix_kb", "prefix4_kb"): measured at C4, 64 KB of binary
-            // nodes for the nearest-hit kernels; the 4-wide shadow tree stays in HBM/L2 by default
-            // (src 11), a prefix there costs more in co-residency than it saves
-            const int kb2 = static_cast<int>(c->t(kTunePrefixKb2)), kb4 = static_cast<int>(c->t(kTunePrefixKb4));
+            if (!pair_ok(src, src_occ)) {               // unsupported or unavailable here: the binary tree through L2
+                src = 2;
+                src_occ = c->deep_bvh4 ? 2 : 11;
+            }
+            // LDS prefix (tuning "prefix_kb"): measured at C4, 64 KB of binary nodes for the nearest-hit kernels
+            const int kb2 = static_cast<int>(c->t(kTunePrefixKb2));
             c->dsc.pfx2 = static_cast<int32_t>(static_cast<size_t>(std::max(kb2, 1)) * 1024 / sizeof(DevBvhNode));
-            c->dsc.pfx4 = static_cast<int32_t>(static_cast<size_t>(std::max(kb4, 1)) * 1024 / (kBvh4Planes * sizeof(DevBvh4Plane)));
-            c->dsc.pfxc = static_cast<int32_t>(static_cast<size_t>(c->t(kTuneCamPrefix)) * 1024 / sizeof(DevCamNode));
-            if (src_occ == 13 && kb4 <= 0) src_occ = 11;
+            c->dsc.pfxq = static_cast<int32_t>(static_cast<size_t>(std::max(kb2, 1)) * 1024 / sizeof(DevQNode4));
         } else {
             src = src_occ = fits_lds ? 1 : 0;
         }
         // tuning "split" 0: every kernel on one in-order stream (A/B measurement);
         // "deal": 1 workgroup-major chunk dealing (default), 0 workgroup-first;
         // "bstreams": streams for the shadow + shading kernels (default 2;
-        // generations alternate over them); "fuse" 1: shading fused into the shadow kernel
+        // generations alternate over them).
         // default: two B streams when the tree is in LDS (C3: 3.30 vs 3.71 ms on one stream);
         // one stream when the nearest-hit walk reads the tree through L2 below its LDS prefix,
         // where the overlapped shadow / shading waves slow that chain more than they hide
-        // (C4 55.2 vs 56.6-57.3 ms, C5 318 vs 330 ms, binary16 nodes)
-        const bool prefix_src = src == 5 || src == 6 || src == 8;
+        // (C4 55.2 vs 56.6-57.3 ms, C5 318 vs 330 ms, binary16 nodes; round 5 with the
+        // high-priority chain: C4 51.9 vs 50.4 ms)
+        const bool prefix_src = src == 5 || src == 6 || src == 8 || src == 26;
         const bool split = c->t(kTuneSplit) < 0 ? !prefix_src : c->t(kTuneSplit) != 0;
         // two b streams (consecutive generations' shadows and shading overlap): measured
         // 3.87 -> 3.78 ms at C3 once the shading runs in its own kernel; three are slower
         const int n_b = std::max(1, std::min(kMaxBStreams, static_cast<int>(c->t(kTuneBStreams))));
-        // (fused shading measured slower once shadow queries went through the light-view
-        // grids: the shading's pow and the per-light atomics then dominate the fused kernel)
-        const bool fuse = c->t(kTuneFuse) != 0;
-        // shadow item lists ("lists" 0: every (record, light) pair goes to the shadow kernel)
-        const uint32_t nlists = (split && fuse && c->t(kTuneLists) != 0 && c->dsc.n_lights > 0 &&
-                                 c->dsc.n_lights <= 24) ? static_cast<uint32_t>(c->dsc.n_lights) + 1u : 0u;
-        // generation 0 by camera tile ("cam" 0: per-ray like the other generations);
-        // only with the binary-tree sources, whose node order the camera view shares
+        // generation 0: the camera's view grid (any sphere source), spheres staged in LDS when they
+        // fit (3), else through L2 (4); the default where built (C3 camera pass 520 -> 327 us, 3.46 ->
+        // 3.26 ms per frame on one box, against the camera-view tile walk it replaced); otherwise
+        // (tuning "cam" other than 3 or -1, or no grid) per ray through the nearest-hit source
         int cam = 0;
-        if (src == 2 || src == 4 || src == 5 || src == 6 || src == 7 || src == 8 || src == 9) {
-            const size_t cam_lds = node_bytes / sizeof(DevBvhNode) * sizeof(DevCamNode) + sph_bytes + 16 * 64 * 4;
-            cam = cam_lds <= kLdsBudget ? 1 : 2;
-            const int ce = static_cast<int>(c->t(kTuneCam));
-            if (ce == 0) cam = 0;
-            else if (ce == 2) cam = 2;
-        }
-        // the camera's view grid (any sphere source): spheres staged in LDS when they fit (3), else through L2 (4);
-        // the default where built (C3 camera pass 520 -> 327 us, 3.46 -> 3.26 ms per frame on one box)
         if ((c->t(kTuneCam) == 3 || (c->t(kTuneCam) < 0 && mode == RT_ALGO_WAVEFRONT)) && c->dsc.cgrid)
             cam = static_cast<size_t>(c->dsc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) <= kLdsBudget ? 3 : 4;
         const uint32_t wg_major = c->t(kTuneDeal) != 0 ? 1u : 0u;
         if (c->t(kTuneVerbose))
-            std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d lists %u deep4 %d short_stack %d split %d pfx %d/%d\n",
-                         src, src_occ, cam, nlists, c->deep_bvh4 ? 1 : 0, c->short_stack ? 1 : 0, split ? 1 : 0,
-                         c->dsc.pfx2, c->dsc.pfx4);
+            std::fprintf(stderr, "rtamd: wavefront src %d occ %d cam %d deep4 %d short_stack %d split %d pfx %d/%d\n",
+                         src, src_occ, cam, c->deep_bvh4 ? 1 : 0, c->short_stack ? 1 : 0, split ? 1 : 0, c->dsc.pfx2,
+                         c->dsc.pfxq);
         // Chunks of whole rows, multiples of 8 (the generation-0 8x8 tiles), sized so
         // the lanes' working sets (ensure_wf: queues, one shade-record array and one
-        // level array per lit generation, terminals, shadow lists) fit the budget:
+        // level array per lit generation, terminals) fit the budget:
         // tuning "wf_budget_mb", else min(80 GB, 85% of the free device memory)
         // (hipMemGetInfo), e.g. C4's 8192^2 frame in one chunk at depth 8 (62.8 vs
         // 63.9 ms as two) and C5 in 7 at depth 16.  Balanced: a frame slightly over
@@ -1133,7 +1146,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         if (cap_px == 0) {
             const uint64_t budget = c->t(kTuneWfBudgetMb) > 0 ? static_cast<uint64_t>(c->t(kTuneWfBudgetMb)) << 20
                                                                : default_wf_budget(c);
-            cap_px = std::max<uint64_t>(1, budget / static_cast<uint64_t>(lanes_req) / wf_bytes_per_slot(levels, nlists));
+            cap_px = std::max<uint64_t>(1, budget / static_cast<uint64_t>(lanes_req) / wf_bytes_per_slot(levels));
         }
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));
@@ -1159,55 +1172,17 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             R = (slots + G * kWfThreads - 1) / (G * kWfThreads) * kWfThreads;
             for (int l = 0; l < n_lanes && rc2 == RT_OK; ++l) {
                 if (split && (rc2 = ensure_bstreams(c, c->lanes[l], n_b)) != RT_OK) return rc2;
-                rc2 = ensure_wf(c, c->lanes[l], cap, G, R, static_cast<uint32_t>(levels), nlists);
+                rc2 = ensure_wf(c, c->lanes[l], cap, G, R, static_cast<uint32_t>(levels));
             }
             if (rc2 == RT_OK) break;
             if (rc2 != RT_E_NOMEM || chunk_rows <= 8) return rc2;
             for (auto& L : c->lanes) drop_lane_memory(L);      // retry with half the pixels per chunk
             cap_px = std::max<uint64_t>(1, static_cast<uint64_t>(chunk_rows) * o->tile_w / 2);
         }
-        // the quad walk for the late generations' small queues (trace_kernel.hip kSrcBvh4Q):
-        // by default for chunks small enough that those queues fit one round of it
-        const uint32_t tail_max = c->t(kTuneTailMax) > 0 ? static_cast<uint32_t>(c->t(kTuneTailMax))
-                                                         : static_cast<uint32_t>(c->n_cu) * 256u;
-        int tail_from = static_cast<int>(c->t(kTuneTailFrom));
-        // (auto: from generation 5 in chunks of <= 32 x tail_max slots, e.g. one rank's
-        // share of an 8-way C3 frame: 0.943 -> 0.879 ms; a 4-way share, whose
-        // generations 5 and 6 still hold more rays than that, measured 2% slower)
-        if (tail_from < 0) tail_from = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8) <= 32ull * tail_max ? 5 : 0;
-        if (src != 9 || !c->quad_ok) tail_from = 0;
-        // the wave-cooperative query for the late generations' small queues (src 9 with
-        // clusters whose LDS copy keeps the nearest-hit kernel at two workgroups per CU)
-        c->dsc.cl_slots = c->cl_slots;
-        {
-            const size_t cl_bytes = static_cast<size_t>(c->dsc.n_clusters) * sizeof(DevCluster) +
-                                    static_cast<size_t>(8) * 64 * c->cl_slots * sizeof(uint16_t);
-            // (axis-pair nodes 56 B each, spheres + ids, clusters, region scan and counters of G regions)
-            const size_t total = (node_bytes / sizeof(DevBvhNode) * 56 + 15) / 16 * 16 + (sph_bytes + 15) / 16 * 16 +
-                                 (cl_bytes + 15) / 16 * 16 + (static_cast<size_t>(G) + 64) * 4;
-            if (total > 80 * 1024) c->dsc.cl_slots = 0;
-        }
-        const int64_t wave_t = c->t(kTuneWaveMax);
-        // (auto: off -- measured slower than the quad walk on the tail of an 8-way C3 share: a ray that
-        // misses tests every cluster box it crosses, 60-78 vs 43 us per launch)
-        const uint32_t wave_max = src != 9 || c->dsc.cl_slots == 0 ? 0u
-                                  : wave_t >= 0 ? static_cast<uint32_t>(wave_t) : 0u;
-        if (wave_max == 0) c->dsc.cl_slots = 0;         // (the clusters are staged only for that query)
         for (int l = 0; l < n_lanes; ++l) {
-            c->lanes[l].b.tail_from = tail_from;
-            c->lanes[l].b.tail_max = tail_max;
-            c->lanes[l].b.wave_max = wave_max;
-            // (wf_fold at 96 VGPRs and wf_shade at 128 fit one 1024-thread workgroup per CU: -1 launches
-            // one per CU, each dealing over the launch's own grid, instead of G in two dispatch rounds)
-            const int64_t fw = c->t(kTuneFoldWgs), sw = c->t(kTuneShadeWgs);
-            c->lanes[l].b.fold_wgs = fw < 0 ? static_cast<uint32_t>(c->n_cu) : static_cast<uint32_t>(fw);
-            c->lanes[l].b.shade_wgs = sw < 0 ? static_cast<uint32_t>(c->n_cu) : static_cast<uint32_t>(sw);
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
-            // eager fold: chain ids (< qcap, which the 8-row tiles and 1024-entry regions round up
-            // past the pixel count) carry the kChainEnd flag in bit 31
-            c->lanes[l].b.eager = c->t(kTuneEagerFold) != 0 && c->lanes[l].b.qcap < kChainEnd ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
         // rt_render copies each chunk's rows as soon as that chunk's fold is done (the fold
@@ -1257,46 +1232,26 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.mb[i] = timed ? (split ? &marks_b[i] : &marks) : nullptr;
             }
             ws.near_done = L.near_done.data();
-            ws.gen_done = L.gen_done.data();
-            ws.fold_split = static_cast<int>(c->t(kTuneFoldSplit));
-            // merged tail (tuning bmerge): only with the grid-only shadow kernel, unfused shading and the
-            // frame-end fold, and when one region scan covers the merged generations' regions
-            {
-                int T = static_cast<int>(c->t(kTuneBMerge));
-                if (T < 0) T = 0;                                  // auto: off until measured
-                const bool ok = T >= 1 && static_cast<uint32_t>(T) <= o->max_depth && split && !fuse && nlists == 0 &&
-                                !b.eager && c->all_lights_gridded && c->t(kTuneGridOcc) != 0 &&
-                                c->t(kTuneFuseFrom) > static_cast<int64_t>(o->max_depth) &&
-                                static_cast<uint64_t>(o->max_depth + 1 - T) * G <= static_cast<uint64_t>(kMaxScan) &&
-                                c->t(kTuneFoldSplit) == 0;
-                ws.bmerge = ok ? T : 0;
-            }
-            // fused tail (tuning tail_fuse = T): the src-9 tree, light-view grid shadows, the frame-end fold
+            // fused tail (tuning tail_fuse = T): the src-9 tree and light-view grid shadows
             {
                 // auto: from generation 4 for chunks of <= 4.5 M pixel slots (one rank's share of a 4- or
                 // 8-way C3 frame), from 5 up to 9 M (a 2-way share), off above (the whole C3 frame: 2.933
-                // vs 2.921 ms with T = 7); with the tail's own fold (tail_fold 1) on one box: 8-way share
-                // 0.855 -> 0.751 ms, 4-way 1.140 -> 1.040, 2-way 1.725 -> 1.642
+                // vs 2.921 ms with T = 7); with the tail's own fold on one box: 8-way share 0.855 -> 0.751
+                // ms, 4-way 1.140 -> 1.040, 2-way 1.725 -> 1.642
                 const uint64_t S = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8);
                 int T = static_cast<int>(c->t(kTuneTailFuse));
                 if (T < 0) T = S <= 4500000u ? 4 : S <= 9000000u ? 5 : 0;
                 const bool ok = T >= 1 && static_cast<uint32_t>(T) <= o->max_depth + 1 && src == 9 && c->all_lights_gridded &&
-                                c->t(kTuneGridOcc) != 0 && !b.eager && ws.bmerge == 0 && c->t(kTuneFoldSplit) == 0;
+                                c->t(kTuneGridOcc) != 0;
                 ws.tail_fuse = ok ? T : 0;
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
-                ws.tail_fold = static_cast<int>(c->t(kTuneTailFold));
-                ws.tail_shade = ws.tail_fold ? 0 : std::min<int>({T - 1, static_cast<int>(c->t(kTuneTailShade)),
-                                                                  static_cast<int>(kMaxScan / G)});
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;
-            ws.fuse = fuse;
             ws.cam = cam;
-            ws.lists0 = c->t(kTuneLists0) != 0;
+            ws.fold_ev = c->n_bands == 0 ? nullptr : &c->band_ev[ci];
             // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
             // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
-            ws.fuse_from = static_cast<int>(c->t(kTuneFuseFrom));
-            ws.fold_ev = c->n_bands == 0 ? nullptr : &c->band_ev[ci];
             ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
                               ? (static_cast<size_t>(c->dsc.n_spheres) * sizeof(DevSphere) <= 64 * 1024 ? 1 : 2)
                               : 0;

@@ -271,12 +271,6 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
 // exactness" has the argument in full.
 constexpr float kBoxTol = 1e-5f;
 constexpr int kBvhStack = 64;      // host builder bounds the depth (median splits past depth 40)
-#ifndef RT_SEL4
-#define RT_SEL4 0
-#endif
-#ifndef RT_PUSH_BRANCHLESS
-#define RT_PUSH_BRANCHLESS 0
-#endif
 constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst case (bvh4_stack_need) against it
 
 // f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
@@ -286,20 +280,6 @@ constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst c
 struct RayBox {
     float ix, iy, iz, nox, noy, noz;
 };
-
-// The near-plane selectors of a ray for the plane-major 4-wide nodes: the
-// near slab bound of axis a is plane 2a (lo) when the ray's 1/d_a >= 0, else
-// plane 2a + 1 (hi), and the far bound the other one.  fma with a fixed 1/d
-// and -o/d is monotone in the coordinate, so fma(near) = min(fma(lo),
-// fma(hi)) and fma(far) = max(...) exactly: the same intervals as
-// box_hit's, with 6 fewer min/max per child box.  Offsets in planes.
-struct Sel4 {
-    int32_t x, y, z;             // 0 or n4 (hi plane of the axis is the near one)
-};
-
-__device__ __forceinline__ Sel4 make_sel4(const RayBox& rb, int32_t n4) {
-    return Sel4{rb.ix < 0.0f ? n4 : 0, rb.iy < 0.0f ? n4 : 0, rb.iz < 0.0f ? n4 : 0};
-}
 
 __device__ __forceinline__ float inv_dir(double d) {
     float f = static_cast<float>(d);
@@ -379,18 +359,24 @@ struct BvhView {
     const int32_t* obj;
     const DevBvh4Plane* p4;      // 4-wide tree planes (LDS or HBM), stride n4
     int32_t n4;
-    const DevBvh4Plane* p4l;     // prefix sources: planes of 4-wide nodes [0, nl4) in LDS, stride nl4
-    int32_t nl4;
-    const DevCamNode* cn;        // camera view of the binary tree (LDS or HBM)
-    int32_t* stk;                // this wave's LDS traversal stack (camera sources)
     const DevBvhNodeH* hpnodes;  // half-node prefix source: nodes [0, nl) in LDS (binary16 bounds)
     const DevBvhNodeH* hgnodes;  // ... and the whole half-node tree in HBM/L2
-    const DevCamNode* cng;       // camera nodes [ncl, n) are read here, [0, ncl) from cn (LDS)
-    int32_t ncl;
-    uint32_t* lstk;              // quad source: this ray's LDS stack (entry i at lstk[i * kQuadStride])
-    const DevCluster* cl;        // wave-cooperative query: the clusters and their octant orders (LDS)
-    const uint16_t* clp;
+    const DevQNode4* q4l;        // quantised 4-wide tree: nodes [0, nq) in LDS, the rest from q4g (HBM/L2)
+    const DevQNode4* q4g;
+    int32_t nq;
 };
+
+// The view of the scene's trees and spheres in HBM (what a source does not stage in LDS).
+__device__ __forceinline__ BvhView global_view(const DevScene& sc) {
+    BvhView v{};
+    v.gnodes = sc.bvh;
+    v.sph = sc.spheres;
+    v.obj = sc.sphere_obj;
+    v.p4 = sc.bvh4;
+    v.n4 = sc.n_bvh4;
+    v.q4g = sc.q4;
+    return v;
+}
 
 // LDS copy of binary nodes [0, n), AXIS-PAIR-MAJOR: for axis a the lo_a
 // bounds of the two children of node i as one pair at L[(2a) * n + i] and
@@ -584,14 +570,11 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     }
 }
 
-// nearest_bvh with the inner-node step written branch-light (RT_NEAR_BL=1):
+// nearest_bvh with the inner-node step written branch-light:
 // a wave descends inner nodes in one tight loop whose only divergent
 // statement is the masked push of the far child, then tests its leaf, then
 // pops past the entries the current best rules out.  Same visiting order,
 // culling and result as nearest_bvh.
-#ifndef RT_NEAR_BL
-#define RT_NEAR_BL 1
-#endif
 template <bool kCount = false, int kNodes = 0, int kReg = 0, int kCompactBits = 0>
 __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
@@ -749,53 +732,19 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     }
 }
 
-// The part of a shadow query (raytrace.rs:41-49, see occluded_brute) that
-// needs no traversal: the planes (a NaN plane hit with a range means lit, any
-// plane hit without one or with t*t < r2 means shadowed) and then the sphere
-// the query starts on (`hint`, -1 for none).  Returns 0 = lit, 1 = shadowed,
-// 2 = undecided: only the spheres' any-hit traversal can tell, with the
-// planes and the hint left out (they cannot change the answer any more).
-__device__ __forceinline__ int shadow_prefilter(const DevScene& sc, const DevSphere* S, const Ray& r, bool has_range,
-                                                double r2, int32_t hint) {
-    bool plane_block = false;
-    for (int i = 0; i < sc.n_planes; ++i) {
-        double t;
-        if (!plane_t(sc.planes[i], r, t)) continue;
-        if (!has_range) return 1;
-        if (t != t) return 0;
-        plane_block |= t * t < r2;
-    }
-    if (plane_block) return 1;
-    if (sc.n_spheres == 0) return 0;
-    if (hint >= 0) {
-        const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-        double t;
-        if (sphere_t(S[hint], r, sphere_k(a), t) && (!has_range || t * t < r2)) return 1;
-    }
-    return 2;
-}
-
 // ---- 4-wide BVH --------------------------------------------------------
-// One node visit tests the 4 child boxes (same conservative slab test).  The
-// nearest query continues with the nearest hit child and pushes the others
-// far-to-near with their entry t; the shadow query takes them in slot order.
-// Misses are marked by the child pointer (kBvh4Empty), never by t, so a box
+// One node visit tests the 4 child boxes (same conservative slab test); the
+// shadow query takes the hit children in slot order.  Misses are marked by the child pointer (kBvh4Empty), never by t, so a box
 // hit at t = +inf is still visited.
 struct Node4Hits {
     float t[4];
     int32_t c[4];
 };
 
-// kPrefix: nodes below v.nl4 (the breadth-first top of the tree) are read from
-// the LDS copy, the rest from HBM/L2.
-template <bool kPrefix = false>
 __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, const RayBox& rb, float tlim) {
     // axis by axis (as box_hit, same operations), so only two planes are live at a time
-    int32_t N = v.n4;
+    const int32_t N = v.n4;
     const DevBvh4Plane* P = v.p4 + node;
-    if constexpr (kPrefix) {
-        if (node < v.nl4) { N = v.nl4; P = v.p4l + node; }
-    }
     float tn[4], tf[4];
     {
         const DevBvh4Plane lo = P[0], hi = P[N];
@@ -837,336 +786,112 @@ __device__ __forceinline__ Node4Hits node4_test(const BvhView& v, int32_t node, 
     return o;
 }
 
-// node4_test with the ray's near/far planes chosen by Sel4 (same result).
-__device__ __forceinline__ Node4Hits node4_test_sel(const BvhView& v, int32_t node, const RayBox& rb, const Sel4& sel,
-                                                    float tlim) {
-    const int32_t N = v.n4;
-    const DevBvh4Plane* P = v.p4 + node;
-    const DevBvh4Plane nx = P[sel.x], fx = P[N - sel.x];
-    const DevBvh4Plane ny = P[2 * N + sel.y], fy = P[3 * N - sel.y];
-    const DevBvh4Plane nz = P[4 * N + sel.z], fz = P[5 * N - sel.z];
-    const DevBvh4Plane ch = P[6 * N];
-    Node4Hits o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float tn = fmaxf(fmaxf(slab_t(nx.f[k], rb.ix, rb.nox), slab_t(ny.f[k], rb.iy, rb.noy)),
-                               slab_t(nz.f[k], rb.iz, rb.noz));
-        const float tf = fminf(fminf(slab_t(fx.f[k], rb.ix, rb.nox), slab_t(fy.f[k], rb.iy, rb.noy)),
-                               slab_t(fz.f[k], rb.iz, rb.noz));
-        const float n = widen_lo(tn);
-        const float f = widen_hi(tf);
-        const bool hit = n <= f && f >= 0.0f && n <= tlim && ch.i[k] != kBvh4Empty;
-        o.t[k] = hit ? n : __builtin_inff();
-        o.c[k] = hit ? ch.i[k] : kBvh4Empty;
-    }
-    return o;
-}
+// ---- quantised 4-wide tree (DevQNode4) -----------------------------------------
+// Scene::intersect (scene.rs:247-249) through the 4-wide tree whose child boxes
+// are 8-bit multiples of a per-node power-of-two step (host_bvh.cpp
+// quantize_bvh4).  A bound decodes exactly: fma(q, s, m * s) = (m + q) * s is an
+// f32 value (|m + q| < 2^24, s a power of two in the normal range), and it lies
+// outside the f32 child box (rounded outward), so the slab test below is the
+// f32 tree's test on a box that contains that one: it culls a subset of what
+// the f32 test culls.  The nearest hit child is
+// entered first, the other hit children pushed far-to-near (64-bit entries:
+// the entry t and the node index, or kQ4LeafTag | first << 3 | count - 1);
+// leaves get the exact f64 test and the winner is the lexicographic (t,
+// object id) minimum over every tested sphere, as for the binary tree.
+// kAll: every node in LDS (ds reads); else nodes [0, nq) from LDS and the rest
+// through L2 by one flat load (the same 48-B layout on both sides).
+constexpr uint32_t kQ4LeafTag = 0x80000000u;
 
-__device__ __forceinline__ void cas4(Node4Hits& h, int i, int j) {
-    const bool sw = h.t[j] < h.t[i];
-    const float ti = h.t[i], tj = h.t[j];
-    const int32_t ci = h.c[i], cj = h.c[j];
-    h.t[i] = sw ? tj : ti; h.t[j] = sw ? ti : tj;
-    h.c[i] = sw ? cj : ci; h.c[j] = sw ? ci : cj;
-}
+__device__ __forceinline__ float q4_step(int32_t f) { return __uint_as_float((static_cast<uint32_t>(f) >> 24) << 23); }
+__device__ __forceinline__ float q4_byte(uint32_t w, int k) { return static_cast<float>((w >> (8 * k)) & 0xFFu); }
 
-// 5-comparator sorting network on entry t (misses carry t = +inf).
-__device__ __forceinline__ void sort4(Node4Hits& n) {
-    cas4(n, 0, 1); cas4(n, 2, 3); cas4(n, 0, 2); cas4(n, 1, 3); cas4(n, 1, 2);
-}
-
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
+template <bool kCount = false, bool kAll = true>
+__device__ __forceinline__ Hit nearest_q4(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
     if (h.nan_t || sc.n_spheres == 0) return h;
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    RT_STACK_DECL(0, uint64_t);
-    int32_t cur = sc.bvh4_root;
+    const bool fx = rb.ix < 0.0f, fy = rb.iy < 0.0f, fz = rb.iz < 0.0f;     // near slab bound = hi
+    RT_STACK_DECL_N(0, uint64_t, kQ4Stack);
+    rt_keep_in_scratch(stk_m);
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    uint32_t cur = 0;                                            // the root: inner node 0
     for (;;) {
-        if (cur >= 0) {
-            Node4Hits n = node4_test(v, cur, rb, tlim);
+        while (cur < kQ4LeafTag) {
+            DevQNode4 nd;
+            if constexpr (kAll) nd = v.q4l[cur];
+            else nd = *(static_cast<int32_t>(cur) < v.nq ? v.q4l + cur : v.q4g + cur);
+            const float sx = q4_step(nd.frame[0]), sy = q4_step(nd.frame[1]), sz = q4_step(nd.frame[2]);
+            const float ox = static_cast<float>((nd.frame[0] << 8) >> 8) * sx;      // m * s, exact
+            const float oy = static_cast<float>((nd.frame[1] << 8) >> 8) * sy;
+            const float oz = static_cast<float>((nd.frame[2] << 8) >> 8) * sz;
+            const uint32_t nxw = fx ? nd.hi[0] : nd.lo[0], fxw = fx ? nd.lo[0] : nd.hi[0];
+            const uint32_t nyw = fy ? nd.hi[1] : nd.lo[1], fyw = fy ? nd.lo[1] : nd.hi[1];
+            const uint32_t nzw = fz ? nd.hi[2] : nd.lo[2], fzw = fz ? nd.lo[2] : nd.hi[2];
+            float t[4];
+            uint32_t c[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float tn = fmaxf(fmaxf(slab_t(__builtin_fmaf(q4_byte(nxw, k), sx, ox), rb.ix, rb.nox),
+                                             slab_t(__builtin_fmaf(q4_byte(nyw, k), sy, oy), rb.iy, rb.noy)),
+                                       slab_t(__builtin_fmaf(q4_byte(nzw, k), sz, oz), rb.iz, rb.noz));
+                const float tf = fminf(fminf(slab_t(__builtin_fmaf(q4_byte(fxw, k), sx, ox), rb.ix, rb.nox),
+                                             slab_t(__builtin_fmaf(q4_byte(fyw, k), sy, oy), rb.iy, rb.noy)),
+                                       slab_t(__builtin_fmaf(q4_byte(fzw, k), sz, oz), rb.iz, rb.noz));
+                const float n = widen_lo(tn);
+                const uint32_t ref = nd.child[k];
+                const bool hit = fmaxf(n, 0.0f) <= fminf(widen_hi(tf), tlim) && ref != kQ4Empty;
+                t[k] = hit ? n : __builtin_inff();
+                c[k] = !hit ? kNone
+                       : ref < kQ4Leaf ? ref
+                                       : kQ4LeafTag | ((nd.base + ((ref >> 3) & 0xFFFu)) << 3) | (ref & 7u);
+            }
             if constexpr (kCount) w->boxes += 4;
-            // near-to-far: continue with the nearest hit child, push the others
-            // far-first so they pop in order (the order decides how soon the
-            // best hit starts culling)
-            sort4(n);
+            // near-to-far: misses (t = +inf, c = kNone) sort last
+#define RT_Q4CAS(i, j)                                                              \
+            {                                                                       \
+                const bool sw = t[j] < t[i];                                        \
+                const float ti = t[i]; const uint32_t ci = c[i];                    \
+                t[i] = sw ? t[j] : ti; c[i] = sw ? c[j] : ci;                       \
+                t[j] = sw ? ti : t[j]; c[j] = sw ? ci : c[j];                       \
+            }
+            RT_Q4CAS(0, 1) RT_Q4CAS(2, 3) RT_Q4CAS(0, 2) RT_Q4CAS(1, 3) RT_Q4CAS(1, 2)
+#undef RT_Q4CAS
 #pragma unroll
             for (int k = 3; k >= 1; --k)
-                if (n.c[k] != kBvh4Empty) stk_push(stk_entry(n.c[k], n.t[k]));
-            if (n.c[0] != kBvh4Empty) { cur = n.c[0]; continue; }
-        } else {
-            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
+                if (c[k] != kNone) stk_push(stk_entry(static_cast<int32_t>(c[k]), t[k]));
+            cur = c[0];
+        }
+        if (cur != kNone) {
+            const int first = static_cast<int>((cur & ~kQ4LeafTag) >> 3), cnt = static_cast<int>(cur & 7u) + 1;
             if constexpr (kCount) w->spheres += cnt;
             for (int k = first; k < first + cnt; ++k) {
-                double t;
-                if (sphere_t(v.sph[k], r, sk, t)) {
+                double tt;
+                if (sphere_t(v.sph[k], r, sk, tt)) {
                     const int32_t obj = v.obj[k];
-                    if (t < h.t || (t == h.t && obj < h.obj)) {
-                        h.t = t; h.obj = obj; h.prim = k;
-                        tlim = t_limit(t);
+                    if (tt < h.t || (tt == h.t && obj < h.obj)) {
+                        h.t = tt; h.obj = obj; h.prim = k;
+                        tlim = t_limit(tt);
                     }
                 }
             }
         }
-        for (;;) {                  // pop, skipping entries the current best rules out
-            if (stk_n == 0) return h;
-            const uint64_t e = stk_pop();
-            cur = stk_node(e);
-            if (stk_t(e) <= tlim) break;
-        }
-    }
-}
-
-// Quad-cooperative walk of the 4-wide tree in LDS (the small queues of the
-// late generations, where the launch lasts as long as its slowest walk): the
-// four lanes of a quad carry the same ray, lane q tests child slot q of each
-// node, and the quad exchanges the four entry distances through DPP
-// quad_perm moves.  Every lane then takes the same decisions: continue with
-// the nearest hit child (ties: lowest slot), push the other hit children
-// far-first onto the ray's stack in LDS (each lane writes its own entry), and
-// pop past the entries the current best rules out.  Leaf spheres are dealt
-// over the quad (lane q tests first + q, first + q + 4) and the quad's best
-// (t, object) merges into the ray's best: the same lexicographic minimum the
-// sequential loop finds (nearest_bvh4), so the winner does not depend on the
-// split.  Compact 16-bit stack entries (trees of <= 4096 spheres, host
-// checked); `stk` is the ray's LDS stack, entry i at stk[i * kQuadStride].
-constexpr int kQuadStack = 48;                       // entries per ray (host: bvh4_stack_need <= this)
-constexpr int kQuadStride = kWfThreads / 4;          // rays per workgroup
-template <int kPerm>
-__device__ __forceinline__ int32_t quad_mov(int32_t x) { return __builtin_amdgcn_mov_dpp(x, kPerm, 0xF, 0xF, false); }
-template <int kPerm>
-__device__ __forceinline__ float quad_mov(float x) { return __int_as_float(quad_mov<kPerm>(__float_as_int(x))); }
-template <int kPerm>
-__device__ __forceinline__ double quad_mov(double x) {
-    const int64_t u = __double_as_longlong(x);
-    const int32_t lo = quad_mov<kPerm>(static_cast<int32_t>(u)), hi = quad_mov<kPerm>(static_cast<int32_t>(u >> 32));
-    return __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
-}
-constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kQuadXor3 = 0x1B;   // quad_perm [1,0,3,2], [2,3,0,1], [3,2,1,0]
-
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_quad(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
-    Hit h = nearest_planes(sc, r);
-    if (h.nan_t || sc.n_spheres == 0) return h;
-    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const SphK sk = sphere_k(a);
-    const RayBox rb = make_raybox(r);
-    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    const int32_t q = static_cast<int32_t>(threadIdx.x & 3u);
-    const int32_t N = v.n4;
-    const Sel4 sel = make_sel4(rb, N);
-    uint32_t* const stk = v.lstk;
-    int sp = 0;
-    constexpr int32_t kNone = INT32_MIN;
-    int32_t cur = sc.bvh4_root;
-    for (;;) {
-        while (cur >= 0) {
-            const float* P = reinterpret_cast<const float*>(v.p4 + cur) + q;      // plane k: P[4 * k * N]
-            const float tn = fmaxf(fmaxf(slab_t(P[4 * sel.x], rb.ix, rb.nox), slab_t(P[4 * (2 * N + sel.y)], rb.iy, rb.noy)),
-                                   slab_t(P[4 * (4 * N + sel.z)], rb.iz, rb.noz));
-            const float tf = fminf(fminf(slab_t(P[4 * (N - sel.x)], rb.ix, rb.nox), slab_t(P[4 * (3 * N - sel.y)], rb.iy, rb.noy)),
-                                   slab_t(P[4 * (5 * N - sel.z)], rb.iz, rb.noz));
-            const int32_t c = reinterpret_cast<const int32_t*>(P)[4 * 6 * N];
-            if constexpr (kCount) w->boxes += c != kBvh4Empty ? 1u : 0u;
-            const float n = widen_lo(tn), f = widen_hi(tf);
-            const bool hit = n <= f && f >= 0.0f && n <= tlim && c != kBvh4Empty;
-            const float t = hit ? n : __builtin_inff();
-            const float t1 = quad_mov<kQuadXor1>(t), t2 = quad_mov<kQuadXor2>(t), t3 = quad_mov<kQuadXor3>(t);
-            const int32_t c1 = quad_mov<kQuadXor1>(c), c2 = quad_mov<kQuadXor2>(c), c3 = quad_mov<kQuadXor3>(c);
-            const int32_t q1 = q ^ 1, q2 = q ^ 2, q3 = q ^ 3;
-            // this lane's rank among the quad's entries (t, slot), and the nearest one
-            const int rank = (t1 < t || (t1 == t && q1 < q)) + (t2 < t || (t2 == t && q2 < q)) + (t3 < t || (t3 == t && q3 < q));
-            const int hits = (t < __builtin_inff()) + (t1 < __builtin_inff()) + (t2 < __builtin_inff()) + (t3 < __builtin_inff());
-            float bt = t;
-            int32_t bq = q, bc = c;
-            if (t1 < bt || (t1 == bt && q1 < bq)) { bt = t1; bq = q1; bc = c1; }
-            if (t2 < bt || (t2 == bt && q2 < bq)) { bt = t2; bq = q2; bc = c2; }
-            if (t3 < bt || (t3 == bt && q3 < bq)) { bt = t3; bq = q3; bc = c3; }
-            if (hit && rank > 0) stk[(sp + hits - 1 - rank) * kQuadStride] = stk_entry_c<16>(c, t);
-            sp += hits > 0 ? hits - 1 : 0;
-            cur = hits > 0 ? bc : kNone;
-        }
-        if (cur != kNone) {
-            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
-            double lt = __builtin_inf();
-            int32_t lo = INT32_MAX, lp = -1;
-            for (int k = first + q; k < first + cnt; k += 4) {
-                if constexpr (kCount) ++w->spheres;
-                double t;
-                if (sphere_t(v.sph[k], r, sk, t)) {
-                    const int32_t obj = v.obj[k];
-                    if (t < lt || (t == lt && obj < lo)) { lt = t; lo = obj; lp = k; }
-                }
-            }
-            {
-                const double ot = quad_mov<kQuadXor1>(lt);
-                const int32_t oo = quad_mov<kQuadXor1>(lo), op = quad_mov<kQuadXor1>(lp);
-                if (ot < lt || (ot == lt && oo < lo)) { lt = ot; lo = oo; lp = op; }
-            }
-            {
-                const double ot = quad_mov<kQuadXor2>(lt);
-                const int32_t oo = quad_mov<kQuadXor2>(lo), op = quad_mov<kQuadXor2>(lp);
-                if (ot < lt || (ot == lt && oo < lo)) { lt = ot; lo = oo; lp = op; }
-            }
-            if (lt < h.t || (lt == h.t && lo < h.obj)) {
-                h.t = lt; h.obj = lo; h.prim = lp;
-                tlim = t_limit(lt);
-            }
-        }
         cur = kNone;
-        while (sp > 0) {
-            --sp;
-            const uint32_t e = stk[sp * kQuadStride];
-            if (stk_t_c<16>(e) <= tlim) { cur = stk_node_c<16>(e); break; }
+        while (stk_n > 0) {
+            const uint64_t e = stk_pop();
+            if (stk_t(e) <= tlim) { cur = static_cast<uint32_t>(stk_node(e)); break; }
         }
         if (cur == kNone) return h;
     }
-}
-
-// ---- wave-cooperative nearest query ------------------------------------------
-// For the small queues of the late generations, whose launches last as long as
-// their slowest walk: ONE ray (wave-uniform) per wave at a time, every lane
-// working on it.  Lane l tests the boxes of the clusters in slots j*64 + l of
-// the ray's octant order (DevCluster: subtrees of <= 16 spheres, one contiguous
-// sphere range each); then, batch by batch, the next four clusters whose box
-// the ray enters no later than the current t limit are dealt over the four
-// 16-lane rows, lane i of a row testing sphere first + i with the exact f64
-// quadratic.  After each batch the wave's best t tightens the limit, and
-// clusters whose box starts beyond it are dropped (the culling argument of the
-// BVH walk).  The result is the (t, object id)
-// minimum over every sphere tested, the same lexicographic minimum the linear
-// scan finds (scene.rs:247-249).  Every lane must call it with the same ray
-// and no lane masked off (the cross-lane moves read every lane).
-template <int kCtrl>
-__device__ __forceinline__ int32_t dpp_i32(int32_t x) { return __builtin_amdgcn_mov_dpp(x, kCtrl, 0xF, 0xF, false); }
-constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
-
-__device__ __forceinline__ float rl_f32(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
-__device__ __forceinline__ double rl_f64(double x, int l) {
-    const int64_t u = __double_as_longlong(x);
-    const int32_t lo = __builtin_amdgcn_readlane(static_cast<int32_t>(u), l);
-    const int32_t hi = __builtin_amdgcn_readlane(static_cast<int32_t>(u >> 32), l);
-    return __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
-}
-__device__ __forceinline__ Ray rl_ray(const Ray& r, int l) {
-    return Ray{rl_f64(r.ox, l), rl_f64(r.oy, l), rl_f64(r.oz, l), rl_f64(r.dx, l), rl_f64(r.dy, l), rl_f64(r.dz, l)};
-}
-
-// min over the wave's 64 lanes (each 16-lane row by DPP, then the four rows)
-__device__ __forceinline__ float wave_min_f32(float x) {
-    x = fminf(x, __int_as_float(dpp_i32<kDppXor1>(__float_as_int(x))));
-    x = fminf(x, __int_as_float(dpp_i32<kDppXor2>(__float_as_int(x))));
-    x = fminf(x, __int_as_float(dpp_i32<kDppHalfMirror>(__float_as_int(x))));
-    x = fminf(x, __int_as_float(dpp_i32<kDppMirror>(__float_as_int(x))));
-    return fminf(fminf(rl_f32(x, 0), rl_f32(x, 16)), fminf(rl_f32(x, 32), rl_f32(x, 48)));
-}
-
-struct WaveBest {
-    double t;
-    int32_t obj, prim;
-};
-__device__ __forceinline__ bool wb_better(double t, int32_t o, const WaveBest& b) { return t < b.t || (t == b.t && o < b.obj); }
-template <int kCtrl>
-__device__ __forceinline__ void wb_step(WaveBest& b) {
-    const int64_t u = __double_as_longlong(b.t);
-    const int32_t lo = dpp_i32<kCtrl>(static_cast<int32_t>(u)), hi = dpp_i32<kCtrl>(static_cast<int32_t>(u >> 32));
-    const double ot = __longlong_as_double((static_cast<int64_t>(hi) << 32) | static_cast<uint32_t>(lo));
-    const int32_t oo = dpp_i32<kCtrl>(b.obj), op = dpp_i32<kCtrl>(b.prim);
-    if (wb_better(ot, oo, b)) { b.t = ot; b.obj = oo; b.prim = op; }
-}
-// the lexicographic (t, object) minimum over the wave (wave-uniform result)
-__device__ __forceinline__ WaveBest wave_best(WaveBest b) {
-    wb_step<kDppXor1>(b);
-    wb_step<kDppXor2>(b);
-    wb_step<kDppHalfMirror>(b);
-    wb_step<kDppMirror>(b);
-    WaveBest r{rl_f64(b.t, 0), __builtin_amdgcn_readlane(b.obj, 0), __builtin_amdgcn_readlane(b.prim, 0)};
-#pragma unroll
-    for (int row = 1; row < 4; ++row) {
-        const double t = rl_f64(b.t, 16 * row);
-        const int32_t o = __builtin_amdgcn_readlane(b.obj, 16 * row), p = __builtin_amdgcn_readlane(b.prim, 16 * row);
-        if (wb_better(t, o, r)) { r.t = t; r.obj = o; r.prim = p; }
-    }
-    return r;
-}
-
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_wave(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
-    Hit h = nearest_planes(sc, r);
-    if (h.nan_t || sc.n_spheres == 0) return h;
-    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const SphK sk = sphere_k(a);
-    const RayBox rb = make_raybox(r);
-    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
-    const int lane = static_cast<int>(threadIdx.x & 63u);
-    const int oct = (rb.ix < 0.0f ? 1 : 0) | (rb.iy < 0.0f ? 2 : 0) | (rb.iz < 0.0f ? 4 : 0);
-    const int S = sc.cl_slots, NS = 64 * S;
-    // per slot: the cluster's entry t (NaN: missed, never <= tlim) and (first << 5 | count)
-    float te[kClusterSlotsMax];
-    int32_t pk[kClusterSlotsMax];
-    uint64_t m[kClusterSlotsMax];
-#pragma unroll
-    for (int j = 0; j < kClusterSlotsMax; ++j) {
-        te[j] = __builtin_nanf("");
-        pk[j] = 0;
-        m[j] = 0;
-        if (j < S) {
-            const uint16_t cid = v.clp[oct * NS + j * 64 + lane];
-            if (cid != kClusterNone) {
-                const DevCluster c = v.cl[cid];
-                float tn;
-                if constexpr (kCount) w->boxes += 1;
-                if (box_hit(c.lo, c.hi, rb, tlim, tn)) { te[j] = fmaxf(tn, 0.0f); pk[j] = (c.first << 5) | c.count; }
-            }
-            m[j] = __ballot(te[j] <= tlim);
-        }
-    }
-    WaveBest best{__builtin_huge_val(), INT32_MAX, 0};
-    const int q = lane >> 4, i = lane & 15;
-    for (;;) {
-        // the next four clusters in slot order (wave-uniform, scalar)
-        int32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        int got = 0;
-#pragma unroll
-        for (int j = 0; j < kClusterSlotsMax; ++j) {
-            while (m[j] != 0 && got < 4) {
-                const int l = __builtin_ctzll(m[j]);
-                m[j] &= m[j] - 1;
-                const int32_t val = __builtin_amdgcn_readlane(pk[j], l);
-                if (got == 0) s0 = val; else if (got == 1) s1 = val; else if (got == 2) s2 = val; else s3 = val;
-                ++got;
-            }
-        }
-        if (got == 0) break;
-        const int32_t mine = q == 0 ? s0 : q == 1 ? s1 : q == 2 ? s2 : s3;
-        if (q < got && i < (mine & 31)) {
-            const int k = (mine >> 5) + i;
-            if constexpr (kCount) ++w->spheres;
-            double t;
-            if (sphere_t(v.sph[k], r, sk, t)) {
-                const int32_t obj = v.obj[k];
-                if (wb_better(t, obj, best)) { best.t = t; best.obj = obj; best.prim = k; }
-            }
-        }
-        // the wave's best t so far bounds every cluster still worth testing
-        tlim = fminf(tlim, wave_min_f32(best.obj != INT32_MAX ? t_limit(best.t) : __builtin_inff()));
-#pragma unroll
-        for (int j = 0; j < kClusterSlotsMax; ++j)
-            if (j < S) m[j] &= __ballot(te[j] <= tlim);
-    }
-    const WaveBest wb = wave_best(best);
-    if (wb.obj != INT32_MAX && (wb.t < h.t || (wb.t == h.t && wb.obj < h.obj))) { h.t = wb.t; h.obj = wb.obj; h.prim = wb.prim; }
-    return h;
 }
 
 // `hint`: a sphere (leaf-order index, or -1) tested before the traversal: the
 // sphere the shadow ray starts on, which occludes it whenever the light is
 // behind that surface.  Any-hit: testing one sphere early cannot change the
 // answer (and the planes, with the NaN rule, are decided before it).
-template <bool kCount = false, bool kPrefix = false>
+template <bool kCount = false>
 __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                               double r2, int32_t hint, Work* w = nullptr) {
     bool plane_block = false;
@@ -1187,9 +912,6 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
         if (sphere_t(v.sph[hint], r, sk, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
-#if RT_SEL4
-    const Sel4 sel = make_sel4(rb, v.n4);
-#endif
     const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
     // pushes are unconditional stores at the stack top (junk when nothing is
     // pushed; the next push overwrites it): no branch per child
@@ -1199,22 +921,13 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
     for (;;) {
         if (cur >= 0) {
             // slot order (measured: near-to-far sorting costs more than it saves here)
-#if RT_SEL4
-            const Node4Hits n = node4_test_sel(v, cur, rb, sel, tlim);
-#else
-            const Node4Hits n = node4_test<kPrefix>(v, cur, rb, tlim);
-#endif
+            const Node4Hits n = node4_test(v, cur, rb, tlim);
             if constexpr (kCount) w->boxes += 4;
             int32_t next = kBvh4Empty;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const bool hk = n.c[k] != kBvh4Empty;
-#if RT_PUSH_BRANCHLESS
-                stk_m[stk_n] = next;
-                stk_n += (hk && next != kBvh4Empty) ? 1 : 0;
-#else
                 if (hk && next != kBvh4Empty) stk_m[stk_n++] = next;
-#endif
                 next = hk ? n.c[k] : next;
             }
             if (next != kBvh4Empty) { cur = next; continue; }
@@ -1347,65 +1060,6 @@ __device__ __forceinline__ Hit nearest_cgrid(const DevScene& sc, const BvhView& 
         test(en.sph);
     }
     return h;
-}
-
-// ---- generation 0: camera rays by 8x8 tile -----------------------------
-// Every camera ray starts at the camera, so the wave's 64 rays of one pixel
-// tile share a rectangle of image-plane coordinates [tx0, tx1] x [ty0, ty1]
-// (the px, py of main.rs:50-53).  The wave walks the camera view of the binary
-// BVH (DevCamNode) with ONE wave-uniform stack in LDS: a child is entered when
-// its image rectangle overlaps the tile's and some lane's current best t is
-// not below the child's distance bound.  The tree is only a filter; every
-// lane tests every sphere of an entered leaf with the exact f64 quadratic and
-// keeps the (t, object id) minimum, so the result is the linear scan's
-// ("BVH exactness": a reported hit point lies in its padded box,
-// hence its image in the box's rectangle, hence its pixel's (px, py) within
-// the tile's rectangle).  Lanes with `act` = false (no pixel, or a NaN plane
-// hit, which wins outright) only ride along.
-template <bool kCount = false>
-__device__ __forceinline__ Hit nearest_camera(const DevScene& sc, const BvhView& v, const Ray& r, bool act, float tx0,
-                                              float ty0, float tx1, float ty1, Work* w = nullptr) {
-    Hit h = nearest_planes(sc, r);
-    const bool go = act && !h.nan_t;
-    if (sc.n_spheres == 0 || __ballot(go) == 0) return h;
-    const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
-    const SphK sk = sphere_k(a);
-    int32_t* stk = v.stk;
-    int sp = 0;
-    int32_t cur = sc.bvh_root;
-    for (;;) {
-        if (cur >= 0) {
-            const DevCamNode n = *(cur < v.ncl ? v.cn + cur : v.cng + cur);   // wave-uniform: LDS part or L2
-            if constexpr (kCount) w->boxes += go ? 2 : 0;
-            const bool o0 = !(n.r0[2] < tx0 || n.r0[0] > tx1 || n.r0[3] < ty0 || n.r0[1] > ty1);
-            const bool o1 = !(n.r1[2] < tx0 || n.r1[0] > tx1 || n.r1[3] < ty0 || n.r1[1] > ty1);
-            // a lane can still gain from a child unless its best t is below the child's bound
-            const bool e0 = __ballot(go && o0 && !(static_cast<double>(n.tmin0) > h.t)) != 0;
-            const bool e1 = __ballot(go && o1 && !(static_cast<double>(n.tmin1) > h.t)) != 0;
-            const int32_t c0 = __builtin_amdgcn_readfirstlane(n.c0), c1 = __builtin_amdgcn_readfirstlane(n.c1);
-            if (e0 && e1) {
-                const bool first0 = __builtin_amdgcn_readfirstlane(n.tmin0 <= n.tmin1);   // nearer child first
-                stk[sp++] = first0 ? c1 : c0;
-                cur = first0 ? c0 : c1;
-                continue;
-            }
-            if (e0) { cur = c0; continue; }
-            if (e1) { cur = c1; continue; }
-        } else {
-            const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
-            if constexpr (kCount) w->spheres += go ? cnt : 0;
-            for (int k = first; k < first + cnt; ++k) {
-                const DevSphere s = v.sph[k];
-                double t;
-                if (go && sphere_t(s, r, sk, t)) {
-                    const int32_t obj = v.obj[k];
-                    if (t < h.t || (t == h.t && obj < h.obj)) { h.t = t; h.obj = obj; h.prim = k; }
-                }
-            }
-        }
-        if (sp == 0) return h;
-        cur = __builtin_amdgcn_readfirstlane(stk[--sp]);
-    }
 }
 
 // The surface normal the reference's intersect() returned for the winner:

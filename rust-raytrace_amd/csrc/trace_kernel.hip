@@ -194,14 +194,6 @@ __device__ __forceinline__ uint32_t wave_slot(const WfBufs& b, uint32_t n) {
     return deal_major(b, n) ? blockIdx.x * (kWfThreads / 64) + wave : wave * b.G + blockIdx.x;
 }
 
-// wave_slot over the launch's own grid (kernels launched with fewer than G
-// workgroups: every one resident at once when the kernel's registers allow
-// only one workgroup per CU); identical to wave_slot when gridDim.x == G.
-__device__ __forceinline__ uint32_t grid_slot(const WfBufs& b, uint32_t n) {
-    const uint32_t wave = threadIdx.x >> 6;
-    return deal_major(b, n) ? blockIdx.x * (kWfThreads / 64) + wave : wave * gridDim.x + blockIdx.x;
-}
-
 // Whether this workgroup's first chunk is below n (workgroup-uniform).
 __device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n, uint32_t width = 64) {
     const uint64_t first = deal_major(b, n) ? static_cast<uint64_t>(blockIdx.x) * (kWfThreads / 64) : blockIdx.x;
@@ -266,27 +258,6 @@ __device__ __forceinline__ bool slot_pixel(const WfBufs& b, const FrameParams& f
     return lx < fp.tile_w && ly < fp.rows;
 }
 
-// Image-plane rectangle (f32, rounded outward) of the live pixels of
-// generation-0 tile `tile`: px grows with x and py with the frame row, which
-// grows with the local row for any band layout (camera_ray's mapping).
-__device__ __forceinline__ void tile_rect(const FrameParams& fp, const WfBufs& b, uint32_t tile, float& tx0, float& ty0,
-                                          float& tx1, float& ty1) {
-    const uint32_t xa = (tile % b.tiles_x) * 8u, la = (tile / b.tiles_x) * 8u;
-    const uint32_t xb = min(xa + 7u, fp.tile_w - 1u), lb = min(la + 7u, fp.rows - 1u);
-    auto row = [&](uint32_t l) {
-        const uint32_t lr = fp.row0 + l;
-        return fp.y0 + ((lr / fp.band) * fp.band_stride + fp.band_phase) * fp.band + lr % fp.band;
-    };
-    // jitter in [0, 1) (random) or 0.5 (centre): x + j is monotone in both
-    const double j0 = fp.jitter ? 0.0 : 0.5, j1 = fp.jitter ? 1.0 : 0.5;
-    const double px0 = ((static_cast<double>(fp.x0 + xa) + j0) - fp.hw) * fp.scale;
-    const double px1 = ((static_cast<double>(fp.x0 + xb) + j1) - fp.hw) * fp.scale;
-    const double py0 = ((static_cast<double>(row(la)) + j0) - fp.hh) * fp.scale;
-    const double py1 = ((static_cast<double>(row(lb)) + j1) - fp.hh) * fp.scale;
-    tx0 = __double2float_rd(px0); tx1 = __double2float_ru(px1);
-    ty0 = __double2float_rd(py0); ty1 = __double2float_ru(py1);
-}
-
 // Streaming accesses (queues, shade records, levels): each word is written once
 // and read once by a later launch, so they bypass L2 allocation (nontemporal)
 // and leave it to the BVH / sphere lines the traversals re-read.
@@ -346,29 +317,16 @@ __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
 // Sphere sources of the wavefront intersection kernels.
 constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
-constexpr int kSrcBvhG = 2;         // binary BVH from HBM/L2
-constexpr int kSrcBvhL = 4;         // binary BVH + spheres in LDS
-constexpr int kSrcBvhL8 = 7;        // kSrcBvhL held to 64 VGPRs: two 1024-thread workgroups per CU
+constexpr int kSrcBvhG = 2;         // binary BVH from HBM/L2 (trees too deep for the 4-wide stack)
+constexpr int kSrcBvhL8 = 7;        // binary BVH + spheres in LDS, 64 VGPRs: two 1024-thread workgroups per CU
 constexpr int kSrcBvhL8C = 9;       // kSrcBvhL8 with compact 32-bit stack entries (small trees, depth <= kShortStack)
-// The 4-wide tree + spheres in LDS walked by quads of lanes (nearest_quad),
-// the rays' stacks in LDS: one workgroup per CU (up to 128 VGPRs), for the
-// small queues of the late generations, whose launches last as long as their
-// slowest walk (WfBufs::tail_from / tail_max)
-constexpr int kSrcBvh4Q = 17;
-constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs
-constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs
-constexpr int kSrcBvh4L4 = 12;      // kSrcBvh4L with 128 VGPRs (one workgroup per CU)
-// Trees too large for LDS: the breadth-first top of the tree (DevScene::pfx2 /
-// pfx4 nodes, chosen by the host) in LDS, the rest and the spheres from HBM/L2
-// (64 VGPRs).
+constexpr int kSrcBvh4L = 10;       // 4-wide BVH + spheres in LDS, 64 VGPRs (shadow queries without a light grid)
+constexpr int kSrcBvh4G = 11;       // 4-wide BVH + spheres from HBM/L2, 64 VGPRs (idem)
+// Trees too large for LDS: the breadth-first top of the binary tree (DevScene::pfx2
+// nodes, chosen by the host) in LDS, the rest and the spheres from HBM/L2 (64 VGPRs).
 constexpr int kSrcBvhP = 8;         // binary BVH, LDS prefix
 constexpr int kSrcBvhPH = 5;        // binary BVH with binary16 bounds (DevBvhNodeH), LDS prefix of twice the nodes
 constexpr int kSrcBvhPHC = 6;       // kSrcBvhPH with compact 32-bit stack entries (18-bit codes: <= 16383 spheres)
-constexpr int kSrcBvh4P = 13;       // 4-wide BVH, LDS prefix
-// Generation 0 only: camera rays by 8x8 tile, a wave-uniform traversal of the
-// binary BVH's camera view (DevCamNode) with exact per-lane leaf tests.
-constexpr int kSrcCamL = 20;        // camera nodes + spheres in LDS
-constexpr int kSrcCamG = 21;        // camera nodes + spheres from HBM/L2
 // Shadow kernel when every light is a point light with a light-view grid: no
 // tree walk at all (so no traversal stack in scratch and no register spills),
 // spheres from LDS or HBM/L2.
@@ -378,81 +336,69 @@ constexpr int kSrcGridG = 15;
 // spheres staged in LDS (22) or read through L2 (23).
 constexpr int kSrcCamGridL = 22;
 constexpr int kSrcCamGridG = 23;
-// kSrcBvhL8C whose launches also run the wave-cooperative query (nearest_wave) for
-// queues of <= WfBufs::wave_max rays; its own instantiation, so that the default
-// src-9 kernel carries neither that code's registers nor the clusters' LDS
-constexpr int kSrcBvhL8W = 24;
+// The quantised 4-wide tree (DevQNode4, nearest_q4), spheres from HBM/L2 (64 VGPRs): every
+// node in LDS (25, trees of <= ~1500 nodes such as C4's) or the breadth-first top
+// DevScene::pfxq nodes in LDS and the rest through L2 (26, C5); tuning qtree, off by default
+constexpr int kSrcQ4 = 25;
+constexpr int kSrcQ4P = 26;
 
 template <int kSrc>
 struct Src {
-    static constexpr bool cam = kSrc == kSrcCamL || kSrc == kSrcCamG;
     static constexpr bool grid = kSrc == kSrcGridL || kSrc == kSrcGridG;
     static constexpr bool cgrid = kSrc == kSrcCamGridL || kSrc == kSrcCamGridG;
-    static constexpr bool bvh = kSrc >= kSrcBvhG && !grid && !cgrid;
-    static constexpr bool quad = kSrc == kSrcBvh4Q;
-    static constexpr bool waveq = kSrc == kSrcBvhL8W;
-    static constexpr bool wide = (kSrc >= kSrcBvh4L && kSrc <= kSrcBvh4P) || quad;
+    static constexpr bool q4 = kSrc == kSrcQ4 || kSrc == kSrcQ4P;
+    static constexpr bool bvh = kSrc >= kSrcBvhG && !grid && !cgrid && !q4;
+    static constexpr bool wide = kSrc == kSrcBvh4L || kSrc == kSrcBvh4G;
     static constexpr bool half = kSrc == kSrcBvhPH || kSrc == kSrcBvhPHC;
-    static constexpr int compact_bits = kSrc == kSrcBvhL8C || waveq ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
-    static constexpr bool prefix = kSrc == kSrcBvhP || kSrc == kSrcBvh4P || half;
-    static constexpr bool compact = kSrc == kSrcBvhL8C || waveq;
-    static constexpr bool all_lds = kSrc == kSrcBvhL || kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L || kSrc == kSrcBvh4L4 ||
-                                    kSrc == kSrcCamL || quad || waveq;
+    static constexpr int compact_bits = kSrc == kSrcBvhL8C ? 16 : kSrc == kSrcBvhPHC ? 18 : 0;
+    static constexpr bool prefix = kSrc == kSrcBvhP || half;
+    static constexpr bool all_lds = kSrc == kSrcBvhL8 || kSrc == kSrcBvhL8C || kSrc == kSrcBvh4L;
     static constexpr bool sph_lds = kSrc == kSrcLds || all_lds || kSrc == kSrcGridL || kSrc == kSrcCamGridL;
     static constexpr int nodes = all_lds ? 2 : half ? 3 : prefix ? 1 : 0;
-    static constexpr int waves = (kSrc >= kSrcBvhL8 && kSrc != kSrcBvh4L4 && !quad) || half ? 8 : 4;   // min waves per SIMD
+    static constexpr int waves = kSrc >= kSrcBvhL8 || half ? 8 : 4;   // min waves per SIMD
 };
-
-// Per-wave traversal stack of the camera sources (wave-uniform entries).
-constexpr int kCamStack = 64;
 
 // Nodes of the LDS prefix of a prefix source.
 template <int kSrc>
 __host__ __device__ inline int32_t prefix_nodes(const DevScene& sc) {
     if (kSrc == kSrcBvhP) return min(sc.n_bvh, sc.pfx2);
     if (Src<kSrc>::half) return min(sc.n_bvh, 2 * sc.pfx2);     // same LDS bytes, 32-B nodes
-    if (kSrc == kSrcBvh4P) return min(sc.n_bvh4, sc.pfx4);
+    if (kSrc == kSrcQ4P) return min(sc.n_q4, sc.pfxq);
+    if (kSrc == kSrcQ4) return sc.n_q4;
     return 0;
-}
-
-__host__ __device__ inline size_t cluster_lds_bytes(const DevScene& sc) {
-    return (static_cast<size_t>(sc.n_clusters) * sizeof(DevCluster) + static_cast<size_t>(8) * 64 * sc.cl_slots * sizeof(uint16_t) +
-            15) / 16 * 16;
 }
 
 // LDS layout of the intersection kernels: [staged data][region scan, G + 1][wave sums, 16][counter].
 template <int kSrc>
 __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
     size_t bytes = 0;
+    if (Src<kSrc>::q4) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevQNode4);
     if (kSrc == kSrcLds || kSrc == kSrcGridL) bytes = static_cast<size_t>(sc.n_spheres) * sizeof(DevSphere);
     if (kSrc == kSrcCamGridL) bytes = static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
     if (kSrc == kSrcBvhP) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNode);
     if (Src<kSrc>::half) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * sizeof(DevBvhNodeH);
-    if (kSrc == kSrcBvh4P) bytes = static_cast<size_t>(prefix_nodes<kSrc>(sc)) * kBvh4Planes * sizeof(DevBvh4Plane);
-    if (Src<kSrc>::prefix) return (bytes + 15) / 16 * 16;
-    if (Src<kSrc>::cam) bytes = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
-    if (kSrc == kSrcCamG) bytes += static_cast<size_t>(min(sc.n_bvh, sc.pfxc)) * sizeof(DevCamNode);
-    if (Src<kSrc>::nodes > 0)
-        bytes += Src<kSrc>::cam    ? static_cast<size_t>(sc.n_bvh) * sizeof(DevCamNode)
-                 : Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane)
-                                   : node_planes_bytes(sc.n_bvh);
+    if (Src<kSrc>::nodes == 2)
+        bytes = Src<kSrc>::wide ? static_cast<size_t>(sc.n_bvh4) * kBvh4Planes * sizeof(DevBvh4Plane) : node_planes_bytes(sc.n_bvh);
     if (Src<kSrc>::bvh && Src<kSrc>::sph_lds) bytes += static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t));
-    bytes = (bytes + 15) / 16 * 16;
-    if (Src<kSrc>::quad) bytes += static_cast<size_t>(kQuadStack) * kQuadStride * sizeof(uint32_t);
-    if (Src<kSrc>::waveq && sc.cl_slots > 0)             // the wave-cooperative query's clusters and orders
-        bytes += cluster_lds_bytes(sc);
-    return bytes;
+    return (bytes + 15) / 16 * 16;
 }
 
-// Stage what the source keeps in LDS (the whole tree and the spheres); returns
-// the view the queries use.  wave: a src-9 launch that runs the wave-cooperative
-// query (nearest_wave) stages the spheres and the clusters, not the tree.
+// Stage what the source keeps in LDS (the whole tree and the spheres, or the
+// top of the tree); returns the view the queries use.
 template <int kSrc>
-__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds, bool wave = false) {
+__device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
-    BvhView v{nullptr, 0, nullptr, sc.bvh, sc.spheres, sc.sphere_obj, sc.bvh4, sc.n_bvh4, nullptr, 0, sc.cam_nodes, nullptr};
+    BvhView v = global_view(sc);
     size_t off = 0;
-    if constexpr (kSrc == kSrcBvhP) {
+    if constexpr (Src<kSrc>::q4) {
+        const int32_t nl = prefix_nodes<kSrc>(sc);
+        uint4* ln = reinterpret_cast<uint4*>(lds);
+        const uint4* gn = reinterpret_cast<const uint4*>(sc.q4);
+        for (int i = threadIdx.x; i < 3 * nl; i += T) ln[i] = gn[i];
+        v.q4l = reinterpret_cast<const DevQNode4*>(lds);
+        v.nq = nl;
+        return v;
+    } else if constexpr (kSrc == kSrcBvhP) {
         DevBvhNode* ln = reinterpret_cast<DevBvhNode*>(lds);
         const int32_t nl = prefix_nodes<kSrc>(sc);
         for (int i = threadIdx.x; i < nl; i += T) ln[i] = sc.bvh[i];
@@ -467,25 +413,6 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.hgnodes = sc.bvh_h;
         v.nl = nl;
         return v;
-    } else if constexpr (kSrc == kSrcBvh4P) {
-        DevBvh4Plane* lp = reinterpret_cast<DevBvh4Plane*>(lds);
-        const int32_t nl = prefix_nodes<kSrc>(sc);
-        for (int i = threadIdx.x; i < kBvh4Planes * nl; i += T) lp[i] = sc.bvh4[(i / nl) * sc.n_bvh4 + i % nl];
-        v.p4l = lp;
-        v.nl4 = nl;
-        return v;
-    }
-    if constexpr (Src<kSrc>::cam) {
-        v.stk = reinterpret_cast<int32_t*>(lds) + (threadIdx.x >> 6) * kCamStack;
-        off = static_cast<size_t>(kWfThreads / 64) * kCamStack * sizeof(int32_t);
-        // every camera node in LDS (kSrcCamL), or the breadth-first top pfxc of them (kSrcCamG)
-        const int32_t nl = Src<kSrc>::nodes > 0 ? sc.n_bvh : min(sc.n_bvh, sc.pfxc);
-        DevCamNode* lc = reinterpret_cast<DevCamNode*>(lds + off);
-        for (int i = threadIdx.x; i < nl; i += T) lc[i] = sc.cam_nodes[i];
-        v.cn = lc;
-        v.ncl = nl;
-        v.cng = sc.cam_nodes;
-        off += static_cast<size_t>(nl) * sizeof(DevCamNode);
     } else if constexpr (kSrc == kSrcLds || kSrc == kSrcGridL) {
         DevSphere* ls = reinterpret_cast<DevSphere*>(lds);
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) ls[i] = sc.spheres[i];
@@ -498,17 +425,14 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.sph = ls;
         v.obj = lo;
         return v;
-    } else if constexpr (kSrc == kSrcCamGridG) {
-        return v;
-    } else if constexpr (Src<kSrc>::nodes > 0 && Src<kSrc>::wide) {
+    } else if constexpr (Src<kSrc>::nodes == 2 && Src<kSrc>::wide) {
         DevBvh4Plane* lp = reinterpret_cast<DevBvh4Plane*>(lds);
         const int n = kBvh4Planes * sc.n_bvh4;
         for (int i = threadIdx.x; i < n; i += T) lp[i] = sc.bvh4[i];
         v.p4 = lp;
         off = static_cast<size_t>(n) * sizeof(DevBvh4Plane);
-    } else if constexpr (Src<kSrc>::nodes > 0) {
-        if (!wave) v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
-        else v.lnodes = reinterpret_cast<const float2*>(lds);
+    } else if constexpr (Src<kSrc>::nodes == 2) {
+        v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
         v.nl = sc.n_bvh;
         off = node_planes_bytes(sc.n_bvh);
     }
@@ -518,52 +442,29 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         for (int i = threadIdx.x; i < sc.n_spheres; i += T) { ls[i] = sc.spheres[i]; lo[i] = sc.sphere_obj[i]; }
         v.sph = ls;
         v.obj = lo;
-        if constexpr (Src<kSrc>::quad) {                 // the rays' stacks after the spheres
-            const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
-            v.lstk = reinterpret_cast<uint32_t*>(lds + at) + (threadIdx.x >> 2);
-        }
-        if constexpr (Src<kSrc>::waveq) {                // the clusters after the spheres (wave-cooperative query)
-            if (wave && sc.cl_slots > 0) {
-                const size_t at = (off + static_cast<size_t>(sc.n_spheres) * (sizeof(DevSphere) + sizeof(int32_t)) + 15) / 16 * 16;
-                DevCluster* lc = reinterpret_cast<DevCluster*>(lds + at);
-                for (int i = threadIdx.x; i < sc.n_clusters; i += T) lc[i] = sc.clusters[i];
-                uint16_t* lp = reinterpret_cast<uint16_t*>(lc + sc.n_clusters);
-                const int np = 8 * 64 * sc.cl_slots;
-                for (int i = threadIdx.x; i < np; i += T) lp[i] = sc.cl_perm[i];
-                v.cl = lc;
-                v.clp = lp;
-            }
-        }
     }
     return v;
 }
 
-// register entries on top of the compact stack (A/B builds: EXTRA=-DRT_COMPACT_REG=n)
-#ifndef RT_COMPACT_REG
-#define RT_COMPACT_REG 0
-#endif
+// Scene::intersect of one ray through the source's structure (scene.rs:247-249).
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
     if constexpr (Src<kSrc>::cgrid) return nearest_cgrid<kCount>(sc, v, r, w);
-    else if constexpr (Src<kSrc>::quad) return nearest_quad<kCount>(sc, v, r, w);
-    else if constexpr (Src<kSrc>::wide) return nearest_bvh4<kCount>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::q4) return nearest_q4<kCount, kSrc == kSrcQ4>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2 && RT_NEAR_BL)
-        return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact ? RT_COMPACT_REG : 0, Src<kSrc>::compact_bits>(sc, v, r, w);
-#ifndef RT_BL_PREFIX
-#define RT_BL_PREFIX 1
-#endif
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2)
+        return nearest_bvh_bl<kCount, 2, 0, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2, Src<kSrc>::compact_bits>(sc, v, r, w);
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix && RT_BL_PREFIX) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
-    else if constexpr (Src<kSrc>::bvh) return nearest_bvh<kCount, Src<kSrc>::nodes, Src<kSrc>::prefix ? 2 : 0>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh) return nearest_bvh_bl<kCount, 0, 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);
 }
 
 template <int kSrc, bool kCount>
 __device__ __forceinline__ bool occluded_any(const DevScene& sc, const BvhView& v, const Ray& r, bool has_range,
                                              double r2, int32_t hint, Work* w) {
-    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount, Src<kSrc>::prefix>(sc, v, r, has_range, r2, hint, w);
+    if constexpr (Src<kSrc>::wide) return occluded_bvh4<kCount>(sc, v, r, has_range, r2, hint, w);
     else if constexpr (Src<kSrc>::bvh) return occluded_bvh<kCount, Src<kSrc>::nodes, 0>(sc, v, r, has_range, r2, hint, w);
     else return occluded_brute<kCount>(sc, v.sph, r, has_range, r2, w);
 }
@@ -625,16 +526,12 @@ __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t c, Col co
 }
 
 // LDS of a queue kernel after its staged data.
-constexpr int kMaxFusedLights = 24;         // shadow lists / fused shading: the light count lives in occ bits 24..31
-constexpr int kOccCount = 24;
-constexpr int kCntDone = 2 + kMaxFusedLights + 1;     // eager fold: chain ends of this workgroup
-constexpr int kQueueCounters = kCntDone + 1;
+constexpr int kQueueCounters = 2;           // this workgroup's shade records and reflection rays
 
 struct QueueLds {
     uint32_t* scan;     // G + 1
     uint32_t* wave;     // 16
-    uint32_t* count;    // shade records, reflection rays, then one per shadow item list, then chain
-                        // ends (eager fold), appended by this workgroup
+    uint32_t* count;    // shade records, reflection rays appended by this workgroup
 };
 
 __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
@@ -643,8 +540,6 @@ __device__ __forceinline__ QueueLds queue_lds(unsigned char* at, uint32_t G) {
 }
 
 __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + kWfThreads / 64 + kQueueCounters) * 4u; }
-
-
 
 // What follows a nearest hit (all 64 lanes call it; `live` lanes carry a
 // query): a miss or a cut-off ends the chain at once (terminal colour; a
@@ -655,7 +550,7 @@ __host__ __device__ inline size_t queue_lds_bytes(uint32_t G) { return (G + 1 + 
 // pixel cpix[c]); its records, reflection rays, levels and terminal carry c
 // (`p` is the pixel for kCam, the chain otherwise), so the levels and
 // terminals of a generation are written in about the order of its records.
-template <bool kCam, bool kFresnel, bool kLists>
+template <bool kCam, bool kFresnel>
 __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FrameParams& fp, const WfBufs& b,
                                                const DevSphere* sph, int k, bool live, const Ray& r, double sig,
                                                uint32_t p, const Hit& h, uint32_t* counts, size_t obase, size_t rbase) {
@@ -663,7 +558,7 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
     double ptx = 0.0, pty = 0.0, ptz = 0.0, nsig = 0.0;
     Ray rr{};
     // a chain that ends here without lighting: background (end_obj INT32_MAX) or the
-    // object's ambient colour; eager fold: queued for this generation's wf_fold_gen
+    // object's ambient colour
     bool ends = false;
     int32_t end_obj = INT32_MAX;
     if (live) {
@@ -696,46 +591,13 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
             }
         }
     }
-    if (kCam && ends) {                                    // no levels: the final pixel now
-        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, average_samples(end_colour(sc, end_obj), fp.spp));
-        ends = false;
-    }
-    if (b.eager) {                                         // workgroup-uniform
-        const uint32_t ds = lds_append(&counts[kCntDone], ends);
-        if (ends) {
-            stn(&b.dpix()[static_cast<size_t>(k) * b.qcap + obase + ds], p);
-            stn(&b.dobj()[static_cast<size_t>(k) * b.qcap + obase + ds], end_obj);
-        }
-    } else if (ends) {
-        set_terminal(b, p, end_colour(sc, end_obj), k);
+    if (ends) {
+        if constexpr (kCam)                                // no levels: the final pixel now
+            write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, average_samples(end_colour(sc, end_obj), fp.spp));
+        else
+            set_terminal(b, p, end_colour(sc, end_obj), k);
     }
     const uint32_t slot = lds_append(&counts[0], shade);
-    uint32_t occ = 0u;
-    if constexpr (kLists) {
-        // shadow lists: decide what needs no traversal here (planes, the own
-        // sphere) and queue each undecided (record, light) pair in light l's list
-        const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-        const size_t rk = static_cast<size_t>(k) * b.nlists;
-        uint32_t decided = 0u;
-        for (uint32_t l = 0; l < L; ++l) {
-            bool want = false;
-            if (shade) {
-                double lx, ly, lz, r2;
-                const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
-                const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-                const int d = shadow_prefilter(sc, sph, sray, has_range, r2, h.prim);
-                occ |= d == 1 ? 1u << l : 0u;
-                decided += d != 2 ? 1u : 0u;
-                want = d == 2;
-            }
-            const uint32_t qs = lds_append(&counts[2 + l], want);
-            if (want) stn_if<2>(&b.oq()[(rk + l) * b.qcap + obase + qs], static_cast<uint32_t>(obase) + slot);
-        }
-        occ |= decided << kOccCount;
-        const bool none = shade && decided == L;           // nothing to trace: shade directly from the list
-        const uint32_t qs = lds_append(&counts[2 + L], none);
-        if (none) stn_if<2>(&b.oq()[(rk + L) * b.qcap + obase + qs], static_cast<uint32_t>(obase) + slot);
-    }
     const uint32_t chain = kCam ? static_cast<uint32_t>(obase) + slot : p;   // (slot valid when shade)
     if (shade) {
         const size_t at = rbase + slot;
@@ -745,7 +607,7 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         stn(&b.ru(0)[at], static_cast<uint32_t>(h.obj));
         stn(&b.ru(1)[at], static_cast<uint32_t>(h.prim));
         stn(&b.ru(2)[at], chain);
-        stn(&b.ru(3)[at], occ);
+        stn(&b.ru(3)[at], 0u);
         if constexpr (kCam) {
             stn(&b.cpix()[chain], p);
             b.nlev()[chain] = kNlevRunning;                   // set_terminal gives the level count
@@ -770,7 +632,7 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
 // its reflection ray (raytrace.rs:58-64) to Q_{k+1} right here: the next
 // generation depends only on the hit, never on the shadow rays or the Phong
 // sum, so those run on the other stream, off the critical path.
-template <int kSrc, bool kCam, bool kCount, bool kFresnel, bool kLists>
+template <int kSrc, bool kCam, bool kCount, bool kFresnel>
 __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 #ifndef RT_NEAR_PRIO
@@ -790,42 +652,21 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         region_scan(b.rq() + k * b.G, b.G, ql.scan, ql.wave);
         n = ql.scan[b.G];
     }
-    // quad walk: 16 rays per wave; chunks of 16 rays when every wave takes at most one
-    // (a workgroup then appends <= 256 entries), else 64-ray chunks in four passes
-    constexpr bool kQuad = Src<kSrc>::quad;
-    // queues of <= wave_max rays (generations >= 1 of a src-9 tree with clusters): the
-    // regular kernel runs the wave-cooperative query, `width` rays per wave one after another,
-    // width = ceil(n / waves) so that every wave takes at most one chunk
-    const bool wv = Src<kSrc>::waveq && !kCam && k >= 1 && b.wave_max > 0 && n <= b.wave_max;
-    // tail generations: the quad kernel takes queues of <= tail_max rays (and above wave_max
-    // when the wave query is on), the regular one the rest (both are launched; the other
-    // returns at once)
-    if (!kCam && b.tail_from > 0 && k >= b.tail_from &&
-        (n <= b.tail_max && !(b.wave_max > 0 && n <= b.wave_max)) != kQuad)
-        return;
-    const uint32_t wwidth = max(1u, min(64u, (n + b.G * (kWfThreads / 64) - 1) / (b.G * (kWfThreads / 64))));
-    const uint32_t width = kQuad && n <= b.G * (kWfThreads / 4) ? 16u : wv ? wwidth : 64u;
-    if (!wg_has_work(b, n, width)) {           // nothing dealt here: publish empty regions, free the CU
+    if (!wg_has_work(b, n)) {                  // nothing dealt here: publish empty regions, free the CU
         if (threadIdx.x == 0) {
             b.rs()[k * b.G + blockIdx.x] = 0;
             b.rq()[(k + 1) * b.G + blockIdx.x] = 0;
-            if (b.eager) b.rd()[k * b.G + blockIdx.x] = 0;
         }
-        if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = 0;
         return;
     }
-    const BvhView v = stage_lds<kSrc>(sc, lds, wv);
+    const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();                                       // publishes the LDS staging and counters
     RT_STAMP_AT(st1);
     acc[0] = st1 - st0;
     Work w;
     const size_t obase = static_cast<size_t>(blockIdx.x) * b.R;
     const size_t rbase = static_cast<size_t>(k) * b.qcap + obase;
-    for (uint32_t rt_c = wave_slot(b, n), rt_w = b.G * (kWfThreads / 64); static_cast<uint64_t>(rt_c) * width < n;
-         rt_c += rt_w)
-    for (uint32_t sub = 0; sub < (kQuad ? width / 16u : 1u); ++sub) {
-        const uint32_t j = kQuad ? rt_c * width + sub * 16u + ((threadIdx.x & 63u) >> 2)
-                                 : ((threadIdx.x & 63u) < width ? rt_c * width + (threadIdx.x & 63u) : 0xFFFFFFFFu);
+    RT_FOR_CHUNKS(b, n, j) {
         RT_STAMP_AT(st0);
         [[maybe_unused]] const uint32_t visits0 = w.boxes;
         Ray r{};
@@ -851,27 +692,9 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
             }
         }
         RT_STAMP_AT(st1);
-        if constexpr (Src<kSrc>::cam) {                 // whole wave: one pixel tile
-            float tx0, ty0, tx1, ty1;
-            tile_rect(fp, b, j >> 6, tx0, ty0, tx1, ty1);
-            h = nearest_camera<kCount>(sc, v, r, live, tx0, ty0, tx1, ty1, &w);
-        }
-        if constexpr (Src<kSrc>::waveq) {
-            if (wv) {                                    // workgroup-uniform: every lane on one ray at a time
-                for (uint32_t i = 0; i < width; ++i) {
-                    if (!__builtin_amdgcn_readlane(live ? 1 : 0, static_cast<int>(i))) continue;
-                    const Hit hi = nearest_wave<kCount>(sc, v, rl_ray(r, static_cast<int>(i)), &w);
-                    if ((threadIdx.x & 63u) == i) h = hi;
-                }
-            } else if (live) {
-                h = nearest_any<kSrc, kCount>(sc, v, r, &w);
-            }
-        } else if (live) {
-            if constexpr (!Src<kSrc>::cam) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
-        }
+        if (live) h = nearest_any<kSrc, kCount>(sc, v, r, &w);
         RT_STAMP_AT(st2);
-        finish_nearest<kCam, kFresnel, kLists>(sc, fp, b, v.sph, k, live && (!kQuad || (threadIdx.x & 3u) == 0), r, sig, p, h,
-                                               ql.count, obase, rbase);
+        finish_nearest<kCam, kFresnel>(sc, fp, b, v.sph, k, live, r, sig, p, h, ql.count, obase, rbase);
         RT_STAMP_AT(st3);
 #if RT_STAMP
         acc[1] += st1 - st0; acc[2] += st2 - st1; acc[3] += st3 - st2; acc[4] += 1;
@@ -900,22 +723,15 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         for (int off = 32; off > 0; off >>= 1) ws += __shfl_xor(ws, off, 64);
         if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamp2[k][1 + q], ws);
     }
-
 #endif
     __syncthreads();
     if (threadIdx.x == 0) {
         b.rs()[k * b.G + blockIdx.x] = ql.count[0];
         b.rq()[(k + 1) * b.G + blockIdx.x] = ql.count[1];
-        if (b.eager) b.rd()[k * b.G + blockIdx.x] = ql.count[kCntDone];
     }
-    if (kLists && threadIdx.x < b.nlists) b.ro()[(k * b.nlists + threadIdx.x) * b.G + blockIdx.x] = ql.count[2 + threadIdx.x];
     flush_work<kCount>(b, 2, w);
 }
 
-// The Phong sum of shade record `at` of generation k (raytrace.rs:31-56) with
-// the shadow mask of its lights: a specular hit pushes the level's local
-// colour (its reflection ray was already queued by wf_nearest); any other hit
-// ends the chain with it.
 // A shade record's fields (loaded ahead of its shading by wf_shade).
 struct ShadeIn {
     double ptx, pty, ptz, dx, dy, dz, sig;
@@ -943,10 +759,14 @@ struct ShadeOut {
     double f, nx, ny, nz;
 };
 
-// kTerm = false (the fused tail): a non-specular hit's colour is returned for
-// the caller's in-register fold instead of being written as the chain's terminal.
+// The Phong sum of one shade record of generation k (raytrace.rs:31-56) with
+// the shadow mask of its lights (bit l set: light l shadowed): a specular hit
+// pushes the level's local colour (its reflection ray was already queued by
+// wf_nearest); any other hit ends the chain with it.  kTerm = false (the fused
+// tail): a non-specular hit's colour is returned for the caller's in-register
+// fold instead of being written as the chain's terminal.
 template <bool kFresnel, bool kTerm = true>
-__device__ __forceinline__ ShadeOut shade_compute(const DevScene& sc, const WfBufs& b, int k, size_t at, const ShadeIn& in) {
+__device__ __forceinline__ ShadeOut shade_compute(const DevScene& sc, const WfBufs& b, int k, const ShadeIn& in) {
     const double ptx = in.ptx, pty = in.pty, ptz = in.ptz, dx = in.dx, dy = in.dy, dz = in.dz, sig = in.sig;
     const int32_t obj = in.obj;
     const uint32_t c = in.c, mask = in.mask;
@@ -970,58 +790,22 @@ __device__ __forceinline__ ShadeOut shade_compute(const DevScene& sc, const WfBu
         stn(&b.lf(0)[st], res.r); stn(&b.lf(1)[st], res.g); stn(&b.lf(2)[st], res.b);
         stn(&b.lobj()[st], obj);
         if (kFresnel && m.kind == kMatFresnel) stn(&b.lf(3)[st], sh.f);
-    } else if (!kTerm) {
-    } else if (b.eager) {               // the chain ends here: wf_fold_gen of generation k folds it
-        stn(&b.rf(0)[at], res.r); stn(&b.rf(1)[at], res.g); stn(&b.rf(2)[at], res.b);
-        stn(&b.ru(2)[at], c | kChainEnd);
-    } else {
+    } else if (kTerm) {
         set_terminal(b, c, res, k);
     }
     return ShadeOut{res, specular, sh.f, nx, ny, nz};
 }
 
-template <bool kFresnel>
-__device__ __forceinline__ void shade_record(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t mask) {
-    ShadeIn in = shade_load(b, at, false);
-    in.mask = mask;
-    shade_compute<kFresnel>(sc, b, k, at, in);
-}
-
-// Fused shadow + shading: each (record, light) item adds its shadow bit and
-// one to the record's finished-light count (bits kOccCount..) in a single
-// atomic; the item that completes the count shades the record with the
-// final mask.  Needs n_lights <= kMaxFusedLights.
-
-// Record the answer of shadow query (record at, light l); kShade: the query
-// that completes the record's light count shades it.
-template <bool kShade, bool kFresnel>
-__device__ __forceinline__ void occlusion_done(const DevScene& sc, const WfBufs& b, int k, size_t at, uint32_t l,
-                                               uint32_t L, bool occluded) {
-    if constexpr (kShade) {
-        const uint32_t inc = (occluded ? 1u << l : 0u) + (1u << kOccCount);
-        const uint32_t now = atomicAdd(&b.ru(3)[at], inc) + inc;
-        if ((now >> kOccCount) == L) shade_record<kFresnel>(sc, b, k, at, now & ((1u << kOccCount) - 1u));
-    } else {
-        if (occluded) atomicOr(&b.ru(3)[at], 1u << l);
-    }
-}
-
 // The shadow queries of every shade record of generation k (raytrace.rs:39-49):
 // one work-item per (record, light) pair -- the lights of one hit are
-// independent queries -- setting bit l of the record's occlusion mask
-// (kShade: and shading the record once its last light is done).
-// ngen > 1 (the merged tail, WfStreams::bmerge): the records of generations
-// k .. k + ngen - 1 as one item list (their region sizes are consecutive in rs,
-// and record entry = generation * qcap + region * R + offset either way).
-template <int kSrc, bool kCount, bool kShade, bool kFresnel>
-__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k,
-                                                                            int ngen) {
+// independent queries -- setting bit l of the record's occlusion mask.
+template <int kSrc, bool kCount>
+__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(DevScene sc, FrameParams fp, WfBufs b, int k) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t M = b.G * static_cast<uint32_t>(ngen);
-    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), M);
-    region_scan(b.rs() + k * b.G, M, ql.scan, ql.wave);
+    const QueueLds ql = queue_lds(lds + staged_bytes<kSrc>(sc), b.G);
+    region_scan(b.rs() + k * b.G, b.G, ql.scan, ql.wave);
     const uint32_t L = static_cast<uint32_t>(sc.n_lights);
-    const uint32_t nrec = ql.scan[M], n = nrec * L;
+    const uint32_t nrec = ql.scan[b.G], n = nrec * L;
     if (!wg_has_work(b, n)) return;
     const BvhView v = stage_lds<kSrc>(sc, lds);
     __syncthreads();
@@ -1033,7 +817,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
     const uint32_t W = b.G * (kWfThreads / 64), lane = threadIdx.x & 63u;
     auto item_at = [&](uint32_t qi, uint32_t& l) {
         l = qi / nrec;
-        return rk + region_entry(ql.scan, M, b.R, qi - l * nrec);
+        return rk + region_entry(ql.scan, b.G, b.R, qi - l * nrec);
     };
     uint32_t rc = wave_slot(b, n), lc = 0;
     size_t atc = 0;
@@ -1073,100 +857,37 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
             occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
                            ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
                            : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
-        occlusion_done<kShade, kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, l, L, occluded);
+        if (occluded) atomicOr(&b.ru(3)[at], 1u << l);
     }
     flush_work<kCount>(b, 4, w);
 }
 
-// The shadow lists of generation k: item i of list l < n_lights is the
-// any-hit sphere traversal of (record, light l) -- planes and the record's own
-// sphere were already decided by wf_nearest -- and the query that completes a
-// record's light count shades it; list n_lights holds the records that need
-// no traversal, shaded directly.  Lists are laid end to end, each starting on
-// a 64-item boundary so a wave's chunk belongs to one list (light-major).
-template <int kSrc, bool kCount, bool kFresnel>
-__global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_shadow(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint32_t NL = b.nlists, L = NL - 1u;
-    uint32_t* scans = reinterpret_cast<uint32_t*>(lds + staged_bytes<kSrc>(sc));   // NL x (G + 1)
-    __shared__ uint32_t s_wave[kWfThreads / 64];
-    __shared__ uint32_t s_start[kMaxFusedLights + 2];
-    for (uint32_t l = 0; l < NL; ++l)
-        region_scan(b.ro() + (k * NL + l) * b.G, b.G, scans + l * (b.G + 1), s_wave);
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (uint32_t l = 0; l < NL; ++l) { s_start[l] = acc; acc += (scans[l * (b.G + 1) + b.G] + 63u) & ~63u; }
-        s_start[NL] = acc;
-    }
-    __syncthreads();
-    const uint32_t n = s_start[NL];
-    if (!wg_has_work(b, n)) return;
-    const BvhView v = stage_lds<kSrc>(sc, lds);
-    __syncthreads();
-    DevScene ss = sc;                                  // the traversal part only: planes decided upstream
-    ss.n_planes = 0;
-    Work w;
-    const size_t rk = static_cast<size_t>(k) * b.qcap;
-    RT_FOR_CHUNKS(b, n, qi) {
-        if (qi >= n) continue;
-        uint32_t l = 0;
-        while (l + 1 < NL && qi >= s_start[l + 1]) ++l;          // wave-uniform: chunks never straddle lists
-        const uint32_t j = qi - s_start[l];
-        const uint32_t* sl = scans + l * (b.G + 1);
-        if (j >= sl[b.G]) continue;                               // padding of the list's last chunk
-        const size_t at = rk + ldn_if<2>(&b.oq()[(static_cast<size_t>(k) * NL + l) * b.qcap + region_entry(sl, b.G, b.R, j)]);
-        if (l == L) {                                             // nothing to trace
-            shade_record<kFresnel>(sc, b, k, at, b.ru(3)[at] & ((1u << kOccCount) - 1u));
-            continue;
-        }
-        const double ptx = ldn_if<3>(&b.rf(0)[at]), pty = ldn_if<3>(&b.rf(1)[at]), ptz = ldn_if<3>(&b.rf(2)[at]);
-        double lx, ly, lz, r2;
-        const bool has_range = light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
-        const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        const bool occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
-                                  ? occluded_lgrid<kCount>(ss, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, -1, &w)
-                                  : occluded_any<kSrc, kCount>(ss, v, sray, has_range, r2, -1, &w);
-        occlusion_done<true, kFresnel>(sc, b, k, at, l, L, occluded);
-    }
-    flush_work<kCount>(b, 4, w);
-}
-
-// The Phong sum of every shade record of generation k (scenes without lights,
-// or with more lights than the fused kernel's count field holds).
-// (ngen > 1: generations k .. k + ngen - 1 as one list, as in wf_occlusion.)
+// The Phong sum of every shade record of generation k.
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k, int ngen) {
-    __shared__ uint32_t s_scan[kMaxScan + 1];
+__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
+    __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
-    const uint32_t M = b.G * static_cast<uint32_t>(ngen);
-    region_scan(b.rs() + k * b.G, M, s_scan, s_wave);
-    const uint32_t n = s_scan[M];
+    region_scan(b.rs() + k * b.G, b.G, s_scan, s_wave);
+    const uint32_t n = s_scan[b.G];
     const size_t rk = static_cast<size_t>(k) * b.qcap;
     // software pipelined: the next chunk's records are loaded (HBM) before this chunk is
     // shaded, so at the kernel's 4 waves per SIMD their latency hides behind the f64 math
     const uint32_t W = gridDim.x * (kWfThreads / 64), lane = threadIdx.x & 63u;
     const bool lit = sc.n_lights > 0;
-    uint32_t rc = grid_slot(b, n);
-    size_t at = 0;
+    uint32_t rc = wave_slot(b, n);
     ShadeIn cur{};
     bool have = false;
     if (static_cast<uint64_t>(rc) * 64u + lane < n) {
-        at = rk + region_entry(s_scan, M, b.R, rc * 64u + lane);
-        cur = shade_load(b, at, lit);
+        cur = shade_load(b, rk + region_entry(s_scan, b.G, b.R, rc * 64u + lane), lit);
         have = true;
     }
     for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
         const uint64_t jn = static_cast<uint64_t>(rc + W) * 64u + lane;
-        size_t at_n = 0;
         ShadeIn nxt{};
         const bool have_n = jn < n;
-        if (have_n) {
-            at_n = rk + region_entry(s_scan, M, b.R, static_cast<uint32_t>(jn));
-            nxt = shade_load(b, at_n, lit);
-        }
-        if (have) shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, cur);
+        if (have_n) nxt = shade_load(b, rk + region_entry(s_scan, b.G, b.R, static_cast<uint32_t>(jn)), lit);
+        if (have) shade_compute<kFresnel>(sc, b, k, cur);
         cur = nxt;
-        at = at_n;
         have = have_n;
     }
 }
@@ -1202,7 +923,7 @@ __device__ __forceinline__ Col tail_chain(const DevScene& sc, const FrameParams&
     const int k0 = k;
     for (;;) {
         in.mask = grid_shadow_mask<kCount>(sc, v, in.ptx, in.pty, in.ptz, in.prim, wsh);
-        const ShadeOut so = shade_compute<kFresnel, false>(sc, b, k, 0, in);     // level k if specular
+        const ShadeOut so = shade_compute<kFresnel, false>(sc, b, k, in);        // level k if specular
         if (!so.specular) { nlev = k; return so.res; }
         const Ray r = reflect_ray(Ray{in.ptx, in.pty, in.ptz, in.dx, in.dy, in.dz}, in.ptx, in.pty, in.ptz, so.nx, so.ny,
                                   so.nz);                                   // raytrace.rs:58-64
@@ -1284,10 +1005,7 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
 // lasts about as long as the slowest chain's remaining bounces, not the sum
 // over generations of each generation's slowest walk plus a launch each.
 // Needs the src-9 tree (whole tree + spheres in LDS) and a light-view grid for
-// every light.  With tail_fold 0 it also shades the records of the D
-// generations before T-1 (tuning tail_shade), so that no B-stream launch runs
-// alongside it and the frame-end fold finds the B streams done.
-// Chains in contiguous runs of cw per wave (tuning tail_width;
+// every light.  Chains in contiguous runs of cw per wave (tuning tail_width;
 // auto: spread over about half of the waves; 48 per wave beat 16 / 24 / 32 /
 // 64 on one rank's share of an 8-way C3 frame: the slowest chain of a wave
 // against the lanes its finished chains leave idle), contiguous so that the
@@ -1295,30 +1013,19 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
 // resident; workgroup w publishes its counts in region w and zeros in the
 // other regions r = w (mod gridDim.x) of every generation >= T.
 template <bool kFresnel, bool kCount>
-__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int W, int fold,
-                                                        int D) {
+__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int W) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t s_cnt[2][kMaxGenerations];
     __shared__ double s_srgb[255];
-    __shared__ uint32_t s_rec[kMaxScan + 1];
     const QueueLds ql = queue_lds(lds + staged_bytes<kSrcBvhL8C>(sc), b.G);
     for (int i = threadIdx.x; i < 2 * kMaxGenerations; i += kWfThreads) (&s_cnt[0][0])[i] = 0u;
     for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
     region_scan(b.rs() + (T - 1) * b.G, b.G, ql.scan, ql.wave);   // generation T-1's records; ends with a barrier
-    // the records of generations T-1-D .. T-2 (consecutive in rs: one scan over D*G regions), shading only
-    const uint32_t M = static_cast<uint32_t>(D) * b.G;
-    if (D > 0) region_scan(b.rs() + (T - 1 - D) * b.G, M, s_rec, ql.wave);
-    const uint32_t n = ql.scan[b.G], nrec = D > 0 ? s_rec[M] : 0u;
+    const uint32_t n = ql.scan[b.G];
     const int gens = static_cast<int>(fp.max_depth) + 2;
     const uint32_t nw = gridDim.x * (kWfThreads / 64);
     const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * n + nw - 1) / nw));
-    // the shading-only records go to the waves past the chains' when those take them in at most
-    // two rounds, else to every wave (last slot first)
-    const uint32_t chain_waves = static_cast<uint32_t>(min<uint64_t>(nw, (static_cast<uint64_t>(n) + cw - 1) / cw));
-    const bool apart = static_cast<uint64_t>(nw - chain_waves) * 128u >= nrec;
-    const uint32_t rw = apart ? nw - chain_waves : nw;
-    const uint32_t rslot = apart ? (slot >= chain_waves ? slot - chain_waves : 0xFFFFFFFFu) : nw - 1u - slot;
     Work wn, wsh;
     const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
     __syncthreads();
@@ -1330,22 +1037,9 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
         const ShadeIn in = shade_load(b, at, false);
         int nlev = 0;
         const Col term = tail_chain<kFresnel, kCount>(sc, fp, b, v, T - 1, in, nlev, s_cnt, wn, wsh);
-        if (!fold) {                                          // (tail_fold 0: the frame-end wf_fold folds it)
-            set_terminal(b, in.c, term, nlev);
-            continue;
-        }
         const Col res = average_samples(fold_levels<kFresnel>(sc, b, in.c, nlev, term), fp.spp);
         const uint32_t p = b.cpix()[in.c];
         write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
-    }
-    for (uint64_t base = static_cast<uint64_t>(rslot) * 64u; rslot != 0xFFFFFFFFu && base < nrec;
-         base += static_cast<uint64_t>(rw) * 64u) {
-        const uint64_t j = base + lane;                        // a record of T-1-D .. T-2: its shadows and shading
-        if (j >= nrec) continue;
-        const size_t at = static_cast<size_t>(T - 1 - D) * b.qcap + region_entry(s_rec, M, b.R, static_cast<uint32_t>(j));
-        ShadeIn in = shade_load(b, at, false);
-        in.mask = grid_shadow_mask<kCount>(sc, v, in.ptx, in.pty, in.ptz, in.prim, wsh);
-        (void)shade_compute<kFresnel>(sc, b, static_cast<int>(at / b.qcap), at, in);
     }
     __syncthreads();
     for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
@@ -1359,44 +1053,6 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
     flush_work<kCount>(b, 4, wsh);
 }
 
-// Eager fold (WfBufs::eager): the pixels whose chain ended in generation k --
-// shade records wf_shade marked kChainEnd (their final colour in rf(0..2)) and
-// the misses / cut-offs wf_nearest listed (dpix, dobj) -- folded through their
-// levels k-1 .. 0 exactly as wf_fold does, and written.  Runs on the B stream of
-// generation k after its shading and after generation k-1's wf_fold_gen (so
-// every level below k is written), off the nearest-hit chain: the frame ends
-// with the last generation's shading instead of a fold over every pixel.
-template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FrameParams fp, WfBufs b, int k) {
-    __shared__ uint32_t s_scan[2][kMaxRegions + 1];
-    __shared__ uint32_t s_wave[kWfThreads / 64];
-    __shared__ double s_srgb[255];
-    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
-    region_scan(b.rs() + k * b.G, b.G, s_scan[0], s_wave);     // (past the cut-off: all zero)
-    region_scan(b.rd() + k * b.G, b.G, s_scan[1], s_wave);     // also publishes s_srgb
-    const uint32_t nr = s_scan[0][b.G], n = nr + s_scan[1][b.G];
-    const size_t rk = static_cast<size_t>(k) * b.qcap;
-    RT_FOR_CHUNKS(b, n, j) {
-        if (j >= n) continue;
-        uint32_t c;                                            // the chain
-        Col acc;
-        if (j < nr) {
-            const size_t at = rk + region_entry(s_scan[0], b.G, b.R, j);
-            const uint32_t pf = ldn(&b.ru(2)[at]);
-            if (!(pf & kChainEnd)) continue;                   // specular: its chain goes on
-            c = pf & ~kChainEnd;
-            acc = Col{ldn(&b.rf(0)[at]), ldn(&b.rf(1)[at]), ldn(&b.rf(2)[at])};
-        } else {
-            const size_t at = rk + region_entry(s_scan[1], b.G, b.R, j - nr);
-            c = ldn(&b.dpix()[at]);
-            acc = end_colour(sc, ldn(&b.dobj()[at]));
-        }
-        const Col res = average_samples(fold_levels<kFresnel>(sc, b, c, k, acc), fp.spp);
-        const uint32_t p = b.cpix()[c];
-        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
-    }
-}
-
 // One chain per work-item: the chains of the chunk are generation 0's shade
 // records (chain c = record entry c), dealt densely over G workgroups through
 // the region scan of generation 0's record counts, 64 consecutive chains to a
@@ -1408,10 +1064,9 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold_gen(DevScene sc, FramePara
 // pixel cpix[c].  The quantisation table is staged in LDS: the binary search
 // indexes it with a different entry per lane, which from __constant__ memory
 // costs nine dependent vector loads per channel.
-// Only chains of lo <= nlev <= hi: the split fold (tuning fold_split = K) folds
-// the chains that ended by generation K on a B stream while the later
-// generations run (every level and terminal they need is written by then),
-// and the rest after the last generation.
+// Only chains of lo <= nlev <= hi: with the fused tail, the chains that ended
+// by generation T-1 fold on a B stream while the tail runs (every level and
+// terminal they need is written by then); the tail folds its own.
 template <bool kFresnel>
 __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
     __shared__ double s_srgb[255];
@@ -1438,7 +1093,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
         }
         return hd;
     };
-    uint32_t rc = grid_slot(b, n);
+    uint32_t rc = wave_slot(b, n);
     Head cur = head(static_cast<uint64_t>(rc) * 64u + lane);
     for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
         const Head nxt = head(static_cast<uint64_t>(rc + W) * 64u + lane);
@@ -1450,14 +1105,12 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
     }
 }
 
-template <bool kUnused = false>
 hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& b, hipStream_t s, LaunchMarks* m,
                        uint32_t lo, uint32_t hi) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    const dim3 grid(b.fold_wgs > 0 && b.fold_wgs < b.G ? b.fold_wgs : b.G);
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
-    else hipLaunchKernelGGL((wf_fold<false>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 
@@ -1510,176 +1163,83 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
     return hipGetLastError();
 }
 
+// The shadow queries and the shading of generation k on b stream sb (after its
+// nearest-hit launch).
 template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
-                          hipStream_t sb, LaunchMarks* mb, bool lists, int ngen = 1);
-
-// The split fold applies with B streams of their own (at most two: the fold of
-// generation K waits for K's stream and, through gen_done[K-1], for the other
-// one, so every generation <= K has been shaded only when those two streams
-// carry all of them) and 1 <= K <= max_depth.
-inline bool split_fold(const WfStreams& ws, const FrameParams& fp) {
-    return ws.fold_split >= 1 && static_cast<uint32_t>(ws.fold_split) <= fp.max_depth && ws.b[0] != ws.a && ws.nb <= 2;
-}
-
-template <int kSrcO, bool kCount>
-hipError_t launch_merged_tail(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const WfStreams& ws) {
-    const int k0 = ws.bmerge, ngen = static_cast<int>(fp.max_depth) + 1 - ws.bmerge;
-    if (ngen <= 0) return hipSuccess;
-    return launch_shading<kSrcO, kCount>(sc, fp, b, k0, ws, ws.a, ws.ma, false, ngen);
+                          hipStream_t sb, LaunchMarks* mb) {
+    const dim3 grid(b.G), block(kWfThreads);
+    hipError_t e;
+    if (sc.n_lights > 0) {
+        if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+#define RT_OCC(S) hipLaunchKernelGGL((wf_occlusion<S, kCount>), grid, block, staged_bytes<S>(sc) + queue_lds_bytes(b.G), \
+                                     sb, sc, fp, b, k)
+        if (ws.grid_occ == 1) RT_OCC(kSrcGridL);
+        else if (ws.grid_occ == 2) RT_OCC(kSrcGridG);
+        else RT_OCC(kSrcO);
+#undef RT_OCC
+        if (mb && (e = mb->mark(sb, kKfOcclusion)) != hipSuccess) return e;
+    }
+    if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
+    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, grid, block, 0, sb, sc, fp, b, k);
+    else hipLaunchKernelGGL(wf_shade<false>, grid, block, 0, sb, sc, fp, b, k);
+    return mb ? mb->mark(sb, kKfShade) : hipSuccess;
 }
 
 template <int kSrcN, int kSrcO, bool kCount>
 hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws) {
     const dim3 grid(b.G), block(kWfThreads);
-    const size_t lds_n = staged_bytes<kSrcN>(sc) + queue_lds_bytes(b.G);
     hipError_t e;
     if (ws.tail_fuse > 0 && k >= ws.tail_fuse) {      // the fused tail: every generation >= T in one launch
         if (k > ws.tail_fuse) return hipSuccess;
-        // the tail folds its chains (tail_fold): the levels of generations <= T-2 (the B streams) must
-        // be written; otherwise the frame-end fold folds every chain and the tail waits for nothing
-        for (int i = 0; i < ws.nb && ws.tail_fold; ++i) {
+        // the tail folds its chains: the levels of generations <= T-2 (the B streams) must be written
+        for (int i = 0; i < ws.nb; ++i) {
             if (ws.b[i] == ws.a) continue;
             if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
         }
         // the chains that ended by generation T-1, folded on a B stream while the tail runs
-        if (ws.tail_fold && ws.b[0] != ws.a) {
+        if (ws.b[0] != ws.a) {
             if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(ws.b[0], ws.near_done[k], 0)) != hipSuccess) return e;
         }
-        if (ws.tail_fold && (e = launch_fold(sc, fp, b, ws.b[0], ws.b[0] != ws.a ? ws.mb[0] : ws.ma, 0u,
-                                             static_cast<uint32_t>(k - 1))) != hipSuccess)
+        if ((e = launch_fold(sc, fp, b, ws.b[0], ws.b[0] != ws.a ? ws.mb[0] : ws.ma, 0u, static_cast<uint32_t>(k - 1))) !=
+            hipSuccess)
             return e;
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
         const size_t lds_t = staged_bytes<kSrcBvhL8C>(sc) + queue_lds_bytes(b.G);
-        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, ws.tail_fold, ws.tail_shade);
-        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, ws.tail_fold, ws.tail_shade);
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width);
+        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width);
         return ws.ma ? ws.ma->mark(ws.a, kKfTail) : hipGetLastError();
     }
     e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;
-#define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR, false>), grid, block, \
-                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
-#define RT_NEARL(S, FR) hipLaunchKernelGGL((wf_nearest<S, false, kCount, FR, true>), grid, block, \
-                                           staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
-    // shadow lists from generation 1 on (generation 0 feeds every (record, light) pair to the plain shadow kernel)
-#define RT_NEARC(S, FR, L) hipLaunchKernelGGL((wf_nearest<S, true, kCount, FR, L>), grid, block, \
-                                              staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, bn, k)
-    const bool lists = b.nlists != 0 && (k >= 1 || ws.lists0);
-    // generations >= b.tail_from of an all-LDS compact-stack tree: the quad kernel is
-    // launched before the regular one and takes the queue when it holds <= b.tail_max
-    // rays (decided on the device, where the size is); when the quad kernel's LDS
-    // does not fit a workgroup (160 KB) the regular kernel alone takes every queue
-    const bool quad = kSrcN == kSrcBvhL8C && b.tail_from > 0 && k >= b.tail_from && k >= 1 && sc.bvh4 != nullptr &&
-                      staged_bytes<kSrcBvh4Q>(sc) + queue_lds_bytes(b.G) <= 160u * 1024u;
-    // src 9 with the wave-cooperative query on: its own instantiation (kSrcBvhL8W)
-    const bool waveq = kSrcN == kSrcBvhL8C && b.wave_max > 0 && sc.cl_slots > 0;
-    WfBufs bn = b;
-    if (!quad) bn.tail_from = 0;
-    if (k == 0 && ws.cam == 1) {                 // camera rays by tile (camera view of the BVH)
-        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamL, true, true); else RT_NEARC(kSrcCamL, false, true); }
-        else if (sc.has_fresnel) RT_NEAR(kSrcCamL, true, true); else RT_NEAR(kSrcCamL, true, false);
-    } else if (k == 0 && ws.cam == 2) {
-        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamG, true, true); else RT_NEARC(kSrcCamG, false, true); }
-        else if (sc.has_fresnel) RT_NEAR(kSrcCamG, true, true); else RT_NEAR(kSrcCamG, true, false);
-    } else if (k == 0 && ws.cam == 3) {          // the camera's view grid, spheres in LDS
-        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamGridL, true, true); else RT_NEARC(kSrcCamGridL, false, true); }
-        else if (sc.has_fresnel) RT_NEAR(kSrcCamGridL, true, true); else RT_NEAR(kSrcCamGridL, true, false);
+#define RT_NEAR(S, CAM, FR) hipLaunchKernelGGL((wf_nearest<S, CAM, kCount, FR>), grid, block, \
+                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G), ws.a, sc, fp, b, k)
+    if (k == 0 && ws.cam == 3) {                 // the camera's view grid, spheres in LDS
+        if (sc.has_fresnel) RT_NEAR(kSrcCamGridL, true, true); else RT_NEAR(kSrcCamGridL, true, false);
     } else if (k == 0 && ws.cam == 4) {          // ... spheres through L2
-        if (lists) { if (sc.has_fresnel) RT_NEARC(kSrcCamGridG, true, true); else RT_NEARC(kSrcCamGridG, false, true); }
-        else if (sc.has_fresnel) RT_NEAR(kSrcCamGridG, true, true); else RT_NEAR(kSrcCamGridG, true, false);
-    } else if (k == 0 && lists) {
-        if (sc.has_fresnel) RT_NEARC(kSrcN, true, true); else RT_NEARC(kSrcN, false, true);
+        if (sc.has_fresnel) RT_NEAR(kSrcCamGridG, true, true); else RT_NEAR(kSrcCamGridG, true, false);
     } else if (k == 0) {
         if (sc.has_fresnel) RT_NEAR(kSrcN, true, true); else RT_NEAR(kSrcN, true, false);
-    } else if (lists) {
-        if (quad) { if (sc.has_fresnel) RT_NEARL(kSrcBvh4Q, true); else RT_NEARL(kSrcBvh4Q, false); }
-        if (waveq) { if (sc.has_fresnel) RT_NEARL(kSrcBvhL8W, true); else RT_NEARL(kSrcBvhL8W, false); }
-        else if (sc.has_fresnel) RT_NEARL(kSrcN, true); else RT_NEARL(kSrcN, false);
     } else {
-        if (quad) { if (sc.has_fresnel) RT_NEAR(kSrcBvh4Q, false, true); else RT_NEAR(kSrcBvh4Q, false, false); }
-        if (waveq) { if (sc.has_fresnel) RT_NEAR(kSrcBvhL8W, false, true); else RT_NEAR(kSrcBvhL8W, false, false); }
-        else if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
+        if (sc.has_fresnel) RT_NEAR(kSrcN, false, true); else RT_NEAR(kSrcN, false, false);
     }
-#undef RT_NEARC
-#undef RT_NEARL
 #undef RT_NEAR
-    (void)lds_n;
     e = ws.ma ? ws.ma->mark(ws.a, k == 0 ? kKfCamera : kKfNearest) : hipSuccess;
     if (e != hipSuccess) return e;
-    const bool shaded = static_cast<uint32_t>(k) <= fp.max_depth;     // no shade records past the cut-off
-    if (!shaded && !b.eager) return hipSuccess;
-    // the merged tail: generations >= bmerge are shaded together after the last nearest-hit launch
-    if (ws.bmerge > 0 && k >= ws.bmerge) return hipSuccess;
-    // the fused tail shades the records of generations T-1-D .. T-1 itself
-    if (ws.tail_fuse > 0 && k >= ws.tail_fuse - 1 - ws.tail_shade) return hipSuccess;
+    if (static_cast<uint32_t>(k) > fp.max_depth) return hipSuccess;    // no shade records past the cut-off
+    // the fused tail shades the records of generation T-1 itself
+    if (ws.tail_fuse > 0 && k >= ws.tail_fuse - 1) return hipSuccess;
     // shadows and shading of generation k: on a b stream once nearest_k is done
     // (generations alternate over the b streams, so consecutive ones overlap too)
     const int bi = k % ws.nb;
     const hipStream_t sb = ws.b[bi];
-    LaunchMarks* mb = ws.mb[bi];
     if (sb != ws.a) {
         if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(sb, ws.near_done[k], 0)) != hipSuccess) return e;
     }
-    if (shaded && (e = launch_shading<kSrcO, kCount>(sc, fp, b, k, ws, sb, mb, lists)) != hipSuccess) return e;
-    if (!b.eager) {
-        if (!split_fold(ws, fp) || sb == ws.a) return hipSuccess;
-        // split fold: the chains that ended by generation K, once the shading of K and K-1 is done
-        if (k == ws.fold_split - 1 && (e = hipEventRecord(ws.gen_done[k], sb)) != hipSuccess) return e;
-        if (k != ws.fold_split) return hipSuccess;
-        if (ws.b[(k - 1) % ws.nb] != sb && (e = hipStreamWaitEvent(sb, ws.gen_done[k - 1], 0)) != hipSuccess) return e;
-        return launch_fold(sc, fp, b, sb, mb, 0u, static_cast<uint32_t>(k));
-    }
-    // eager fold of the chains that ended in generation k, after generation k-1's fold
-    // (on another b stream: every level below k is then written)
-    if (k > 0 && ws.b[(k - 1) % ws.nb] != sb && (e = hipStreamWaitEvent(sb, ws.gen_done[k - 1], 0)) != hipSuccess) return e;
-    if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL(wf_fold_gen<true>, grid, block, 0, sb, sc, fp, b, k);
-    else hipLaunchKernelGGL(wf_fold_gen<false>, grid, block, 0, sb, sc, fp, b, k);
-    if (mb && (e = mb->mark(sb, kKfFold)) != hipSuccess) return e;
-    if (sb != ws.a && (e = hipEventRecord(ws.gen_done[k], sb)) != hipSuccess) return e;
-    return hipGetLastError();
-}
-
-// The shadow queries and the shading of generation k on b stream sb (after its
-// nearest-hit launch).
-template <int kSrcO, bool kCount>
-hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
-                          hipStream_t sb, LaunchMarks* mb, bool lists, int ngen) {
-    const dim3 grid(b.G), block(kWfThreads);
-    hipError_t e;
-    if (lists) {                                 // shadow lists (planes and own sphere decided upstream)
-        if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-        const size_t lds_s = staged_bytes<kSrcO>(sc) + static_cast<size_t>(b.nlists) * (b.G + 1) * 4u;
-        if (sc.has_fresnel) hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, true>), grid, block, lds_s, sb, sc, fp, b, k);
-        else hipLaunchKernelGGL((wf_shadow<kSrcO, kCount, false>), grid, block, lds_s, sb, sc, fp, b, k);
-        return mb ? mb->mark(sb, kKfShadow) : hipSuccess;
-    }
-    const bool fused = sc.n_lights > 0 && sc.n_lights <= kMaxFusedLights && (ws.fuse || k >= ws.fuse_from);
-    if (sc.n_lights > 0) {
-        const size_t lds_o = staged_bytes<kSrcO>(sc) + queue_lds_bytes(b.G);
-        if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-#define RT_OCC(S, SH, FR) hipLaunchKernelGGL((wf_occlusion<S, kCount, SH, FR>), grid, block, \
-                                               staged_bytes<S>(sc) + queue_lds_bytes(b.G * ngen), sb, sc, fp, b, k, ngen)
-        if (!fused && ws.grid_occ == 1) RT_OCC(kSrcGridL, false, false);
-        else if (!fused && ws.grid_occ == 2) RT_OCC(kSrcGridG, false, false);
-        else if (!fused) RT_OCC(kSrcO, false, false);
-        else if (ws.grid_occ == 1) { if (sc.has_fresnel) RT_OCC(kSrcGridL, true, true); else RT_OCC(kSrcGridL, true, false); }
-        else if (ws.grid_occ == 2) { if (sc.has_fresnel) RT_OCC(kSrcGridG, true, true); else RT_OCC(kSrcGridG, true, false); }
-        else if (sc.has_fresnel) RT_OCC(kSrcO, true, true);
-        else RT_OCC(kSrcO, true, false);
-#undef RT_OCC
-        (void)lds_o;
-        if (mb && (e = mb->mark(sb, kKfOcclusion)) != hipSuccess) return e;
-    }
-    if (fused) return hipSuccess;
-    if (mb && (e = mb->begin(sb)) != hipSuccess) return e;
-    const dim3 sgrid(b.shade_wgs > 0 && b.shade_wgs < b.G ? b.shade_wgs : b.G);
-    if (sc.has_fresnel) hipLaunchKernelGGL(wf_shade<true>, sgrid, block, 0, sb, sc, fp, b, k, ngen);
-    else hipLaunchKernelGGL(wf_shade<false>, sgrid, block, 0, sb, sc, fp, b, k, ngen);
-    return mb ? mb->mark(sb, kKfShade) : hipSuccess;
+    return launch_shading<kSrcO, kCount>(sc, fp, b, k, ws, sb, ws.mb[bi]);
 }
 
 // One chunk (fp.row0, fp.rows) through every generation.  src: the sphere
@@ -1688,7 +1248,9 @@ hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBuf
 // mark_gen has been launched (chunk pipelining across lanes).  The nearest-hit
 // chain runs on ws.a, the shadow + shading kernels of each generation on ws.b
 // streams (each waiting for its generation's nearest-hit kernel); the fold
-// waits for all of them.
+// waits for all of them.  Supported (src, src_occ) pairs: (0, 0), (1, 1),
+// (2, 2), (7, 7), (7, 10), (9, 10), (2, 11), (5, 11), (6, 11), (8, 11), (25, 11),
+// (26, 11); any other pair runs as (2, 11).
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
@@ -1696,27 +1258,19 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         hipError_t e;
 #define RT_GEN(N, O) e = (count ? launch_generation<N, O, true>(sc, fp, b, k, ws) \
                                 : launch_generation<N, O, false>(sc, fp, b, k, ws))
-        const int combo = src * 100 + src_occ;
-        switch (combo) {
+        switch (src * 100 + src_occ) {
         case kSrcGlobal * 101: RT_GEN(kSrcGlobal, kSrcGlobal); break;
         case kSrcLds * 101: RT_GEN(kSrcLds, kSrcLds); break;
         case kSrcBvhG * 101: RT_GEN(kSrcBvhG, kSrcBvhG); break;
-        case kSrcBvhL * 101: RT_GEN(kSrcBvhL, kSrcBvhL); break;
         case kSrcBvhL8 * 101: RT_GEN(kSrcBvhL8, kSrcBvhL8); break;
-        case kSrcBvh4L * 101: RT_GEN(kSrcBvh4L, kSrcBvh4L); break;
-        case kSrcBvh4L4 * 101: RT_GEN(kSrcBvh4L4, kSrcBvh4L4); break;
         case kSrcBvhL8 * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8, kSrcBvh4L); break;
         case kSrcBvhL8C * 100 + kSrcBvh4L: RT_GEN(kSrcBvhL8C, kSrcBvh4L); break;
-        case kSrcBvhG * 100 + kSrcBvh4G: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
-        case kSrcBvhP * 100 + kSrcBvh4P: RT_GEN(kSrcBvhP, kSrcBvh4P); break;
-        case kSrcBvhPH * 100 + kSrcBvh4P: RT_GEN(kSrcBvhPH, kSrcBvh4P); break;
         case kSrcBvhPH * 100 + kSrcBvh4G: RT_GEN(kSrcBvhPH, kSrcBvh4G); break;
-        case kSrcBvhPHC * 100 + kSrcBvh4P: RT_GEN(kSrcBvhPHC, kSrcBvh4P); break;
         case kSrcBvhPHC * 100 + kSrcBvh4G: RT_GEN(kSrcBvhPHC, kSrcBvh4G); break;
-        case kSrcBvhP * 101: RT_GEN(kSrcBvhP, kSrcBvhP); break;
         case kSrcBvhP * 100 + kSrcBvh4G: RT_GEN(kSrcBvhP, kSrcBvh4G); break;
-        case kSrcBvhG * 100 + kSrcBvh4P: RT_GEN(kSrcBvhG, kSrcBvh4P); break;
-        default: RT_GEN(kSrcBvh4G, kSrcBvh4G); break;
+        case kSrcQ4 * 100 + kSrcBvh4G: RT_GEN(kSrcQ4, kSrcBvh4G); break;
+        case kSrcQ4P * 100 + kSrcBvh4G: RT_GEN(kSrcQ4P, kSrcBvh4G); break;
+        default: RT_GEN(kSrcBvhG, kSrcBvh4G); break;
         }
 #undef RT_GEN
         if (e != hipSuccess) return e;
@@ -1726,15 +1280,6 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         }
     }
     hipError_t e;
-    // the merged tail's shadows and shading (generations >= bmerge), on stream a after the last
-    // nearest-hit launch: one occlusion and one shading launch instead of two per generation
-    if (ws.bmerge > 0) {
-        const int combo = src * 100 + src_occ;
-        e = combo == kSrcBvhL8C * 100 + kSrcBvh4L
-                ? (count ? launch_merged_tail<kSrcBvh4L, true>(sc, fp, b, ws) : launch_merged_tail<kSrcBvh4L, false>(sc, fp, b, ws))
-                : (count ? launch_merged_tail<kSrcBvh4G, true>(sc, fp, b, ws) : launch_merged_tail<kSrcBvh4G, false>(sc, fp, b, ws));
-        if (e != hipSuccess) return e;
-    }
     // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
     if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);
@@ -1744,14 +1289,11 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
     }
-    const hipStream_t s = ws.a;
-    // the chains not folded early (all of them without the split)
-    // (the fused tail folded every chain: its own as it ended them, the others on a B stream)
-    if (!b.eager && (ws.tail_fuse == 0 || !ws.tail_fold) &&
-        (e = launch_fold(sc, fp, b, s, ws.ma, split_fold(ws, fp) ? ws.fold_split + 1u : 0u, kNlevRunning - 1u)) != hipSuccess)
-        return e;
+    // the chains not folded yet (all of them without the fused tail, which folded every chain:
+    // its own as it ended them, the others on a B stream)
+    if (ws.tail_fuse == 0 && (e = launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess) return e;
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
-    if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, s)) != hipSuccess) return e;
+    if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, ws.a)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

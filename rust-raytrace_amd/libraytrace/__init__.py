@@ -123,6 +123,8 @@ def _load():
                                                P(C.c_int32), P(C.c_int32), C.c_size_t, P(C.c_int64)]),
         "rt_view_grid_candidates": (C.c_int, [C.c_void_p, C.c_int, P(C.c_double), C.c_uint32, P(C.c_int32),
                                               P(C.c_int32), P(C.c_float), C.c_size_t, P(C.c_int64)]),
+        "rt_qtree_nodes": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, P(C.c_float), P(C.c_int32), P(C.c_int32),
+                                     C.c_size_t, P(C.c_int64)]),
         "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
         "rt_ctx_get_tuning": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
         "rt_tuning_key": (C.c_char_p, [C.c_int]),
@@ -264,6 +266,25 @@ class Scene:
                 out.append(ids[at:at + c].copy())
                 at += c
         return out, tuple(int(x) for x in info)
+
+    def qtree_nodes(self, leaf_max=0, cap=1 << 16):
+        """Diagnostic (host only): the quantised 4-wide tree rt_scene_upload builds
+        (DevQNode4 records as a structured array, empty when not representable),
+        the f32 child boxes [n, 4, 6] (lo xyz, hi xyz; NaN unused), each slot's
+        leaf spheres (first, count; -1 / 0 for inner children) and (nodes, stack
+        worst case, leaf size)."""
+        dt = np.dtype([("frame", "<i4", 3), ("base", "<u4"), ("lo", "<u4", 3), ("hi", "<u4", 3), ("child", "<u2", 4)])
+        assert dt.itemsize == 48
+        nodes = np.zeros(cap, dt)
+        boxes = np.zeros((cap, 4, 6), np.float32)
+        first = np.zeros((cap, 4), np.int32)
+        count = np.zeros((cap, 4), np.int32)
+        info = np.zeros(3, np.int64)
+        _check(lib.rt_qtree_nodes(self._h, int(leaf_max), nodes.ctypes.data_as(C.c_void_p),
+                                  boxes.ctypes.data_as(C.POINTER(C.c_float)), first.ctypes.data_as(C.POINTER(C.c_int32)),
+                                  count.ctypes.data_as(C.POINTER(C.c_int32)), cap, info.ctypes.data_as(C.POINTER(C.c_int64))))
+        n = int(info[0])
+        return nodes[:n].copy(), boxes[:n].copy(), first[:n].copy(), count[:n].copy(), tuple(int(x) for x in info)
 
     def set_skybox(self, faces):
         """SkyboxBackground { px, nx, py, ny, pz, nz } from six uint8 [h, w, 3] arrays (copied)."""

@@ -304,34 +304,20 @@ def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
     check_parity(gpu_ctx, _axis_tie_scene(), algo)
 
 
-@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3"])
-def test_quad_tail_walk_matches_oracle(gpu_ctx, scene):
-    """The quad walk (four lanes per ray on the 4-wide tree, trace_common.hpp
-    nearest_quad) forced onto every generation from 1 on, whatever the queue
-    size (tail_max huge: 16-ray chunks for small queues, 64-ray chunks in four
-    passes for large ones): ties across leaves, axis-aligned rays, the deepest
-    small tree and a C3 workload all match the oracle bit for bit."""
-    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene,
-         "config3": lambda: scenes.config3(160, 128)}[scene]()
-    with _with_tuning(gpu_ctx, tail_from=1, tail_max=1 << 30):
-        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
-
-
 @pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan", "fresnel"])
 def test_fused_tail_matches_oracle(gpu_ctx, scene):
     """The fused tail (tuning tail_fuse = T, trace_kernel.hip wf_tail): every
     chain still running at generation T-1 goes from its shade record through
     all its remaining bounces -- light-view grid shadows, Phong sum,
     reflection, nearest hit -- in one launch, one chain per work-item, and
-    (tail_fold 1) folds it there, the chains that ended earlier being folded
-    on a B stream meanwhile.  From generation 1 (nearly the whole recursion) and from 4, on
-    ties across leaves, the deepest small tree, NaN planes, Fresnel levels and
-    a C3 workload: bit for bit the oracle's image, and the same ray and
-    shadow-ray counts (the tail publishes every generation's queue and record
-    counts).  The timed render checks that the tail really ran: one tail
-    launch, nearest-hit launches for generations 1 .. T-1 only, shadow and
-    shading launches for 0 .. T-2 (or fewer: tail_shade = D hands the records
-    of D more generations to the tail), one fold."""
+    folds it there, the chains that ended earlier being folded on a B stream
+    meanwhile.  From generation 1 (nearly the whole recursion) to 4, on ties
+    across leaves, the deepest small tree, NaN planes, Fresnel levels and a C3
+    workload: bit for bit the oracle's image, and the same ray and shadow-ray
+    counts (the tail publishes every generation's queue and record counts).
+    The timed render checks that the tail really ran: one tail launch,
+    nearest-hit launches for generations 1 .. T-1 only, shadow and shading
+    launches for 0 .. T-2, and the fold of the chains that ended by T-1."""
     def fresnel():
         s = scenes.config3(96, 72)
         s.max_depth = 10
@@ -343,8 +329,8 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
     # (the tail answers shadows through light-view grids only: directional lights become point lights far away)
     s.lights = [l if l["kind"] == "point" else
                 {"kind": "point", "location": tuple(-40.0 * x for x in l["direction"]), "color": l["color"]} for l in s.lights]
-    for T, fold, D in ((1, 0, 0), (4, 0, 1), (4, 1, 0), (2, 1, 0), (4, 0, 3), (3, 0, 0)):
-        with _with_tuning(gpu_ctx, tail_fuse=T, tail_fold=fold, tail_shade=D):
+    for T in (1, 2, 3, 4):
+        with _with_tuning(gpu_ctx, tail_fuse=T):
             check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
             gpu_ctx.kernel_times()
             gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
@@ -352,35 +338,8 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
             kt = gpu_ctx.kernel_times()
         if T <= s.max_depth + 1:
             assert kt["nearest"][1] == T - 1 and kt["tail"][1] == 1, (T, kt)     # generations 1 .. T-1, the tail
-            d = 0 if fold else min(D, T - 1)
-            assert kt["occlusion"][1] + kt["shadow"][1] == T - 1 - d, (T, kt)   # generations 0 .. T-2-d
-            assert kt["fold"][1] == 1, (T, kt)     # the frame-end fold, or (tail_fold) the chains that ended by T-1
-
-
-@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "extreme", "planes_nan"])
-def test_wave_cooperative_query_matches_oracle(gpu_ctx, scene):
-    """The wave-cooperative query (one ray per wave, clusters of <= 16 spheres
-    tested batch by batch, trace_common.hpp nearest_wave) forced onto every
-    generation from 1 on (wave_max huge): ties across clusters, axis-aligned
-    rays, a deep tree, spheres from 1e-4 to 1e4, NaN planes and a C3
-    workload all match the oracle bit for bit; with the quad walk on too, the
-    three queries share the generations by queue size."""
-    def extreme():
-        s = scenes.config2(57, 41)
-        s.max_depth = 8
-        rng = scenes.SplitMix64(9)
-        for k in range(150):
-            c = (rng.uniform(-30, 30), rng.uniform(0.001, 4), rng.uniform(-60, 0))
-            s.sphere(c, 10 ** rng.uniform(-4, 0.3), scenes.phong((0.3, 0.6, 0.9), (0.6, 0.6, 0.6), 50.0, (0, 0, 0)))
-        s.sphere((0.0, -1e4 + 0.0, -5.0), 1e4, scenes.phong((0.2, 0.2, 0.2), (0.5, 0.5, 0.5), 5.0, (0, 0, 0)))
-        return s
-    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene,
-         "config3": lambda: scenes.config3(160, 128), "extreme": extreme, "planes_nan": _nan_plane_scene}[scene]()
-    with _with_tuning(gpu_ctx, wave_max=1 << 30):
-        check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
-    if scene == "config3":
-        with _with_tuning(gpu_ctx, wave_max=300, tail_from=1, tail_max=3000):
-            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
+            assert kt["occlusion"][1] == T - 1 and kt["shade"][1] == T - 1, (T, kt)   # generations 0 .. T-2
+            assert kt["fold"][1] == 1, (T, kt)     # the chains that ended by T-1
 
 
 @pytest.mark.parametrize("scene", ["axis_ties", "config3", "dense", "planes_nan", "config4", "camera_inside"])
@@ -501,22 +460,48 @@ def test_bvh_ten_thousand_spheres(gpu_ctx):
 
 
 def test_half_node_prefix_source_is_bit_identical(gpu_ctx):
-    """C4's workload (10k spheres: the tree exceeds LDS): the nearest-hit walk over
-    binary16 nodes (bounds rounded outward, twice the nodes in the LDS prefix;
-    the default) and over f32 nodes give the same bytes, colours and rays, equal
-    to the oracle's; also with a 1 KB prefix, so most nodes come from HBM/L2."""
+    """C4's workload (10k spheres: the f32 tree exceeds LDS): the nearest-hit walk
+    over binary16 nodes (bounds rounded outward, twice the nodes in the LDS
+    prefix; the default), over f32 nodes and over the quantised 4-wide tree
+    (whole in LDS, or mostly through L2) give the same bytes, colours and rays,
+    equal to the oracle's; also with a 1 KB prefix, so most nodes come from HBM/L2."""
     spec = scenes.config4(128, 96)
     ref = ref64.render(spec, threads=min(16, os.cpu_count() or 1))
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
     assert np.array_equal(base[1], ref["bgr"])
     assert base[2].rays == ref["counts"]["rays"]
-    for kv in [dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1), dict(split=1),
-               dict(cam_prefix_kb=0), dict(cam_prefix_kb=1)]:
+    for kv in [dict(qtree=1), dict(half_nodes=0), dict(prefix_kb=1), dict(half_nodes=0, prefix_kb=1), dict(split=1),
+               dict(qtree=1, split=0), dict(prefix_kb=1, src=26, src_occ=11), dict(cam=0)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv
         assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), kv
         assert got[2].rays == base[2].rays and got[2].shadow_rays == base[2].shadow_rays, kv
+
+
+@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan", "extreme", "config4"])
+def test_quantised_tree_matches_oracle(gpu_ctx, scene):
+    """The quantised 4-wide tree (trace_common.hpp nearest_q4; host_bvh.cpp
+    quantize_bvh4) forced onto every nearest-hit generation: whole in LDS (src
+    25) and with a 1 KB LDS prefix, every other node read through L2 (src 26).
+    Ties across leaves, axis-aligned rays, the deepest small tree, NaN planes,
+    spheres from 1e-4 to 1e4 (coarse frames), C3 and C4 workloads: bit for bit
+    the oracle's image and ray counts."""
+    def extreme():
+        s = scenes.config2(57, 41)
+        s.max_depth = 8
+        rng = scenes.SplitMix64(9)
+        for k in range(150):
+            c = (rng.uniform(-30, 30), rng.uniform(0.001, 4), rng.uniform(-60, 0))
+            s.sphere(c, 10 ** rng.uniform(-4, 0.3), scenes.phong((0.3, 0.6, 0.9), (0.6, 0.6, 0.6), 50.0, (0, 0, 0)))
+        s.sphere((0.0, -1e4 + 0.0, -5.0), 1e4, scenes.phong((0.2, 0.2, 0.2), (0.5, 0.5, 0.5), 5.0, (0, 0, 0)))
+        s.sphere((1e5, 3.0, -1e5), 2e3, scenes.phong((0.9, 0.9, 0.2), (0.2, 0.2, 0.2), 5.0, (0, 0, 0)))
+        return s
+    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene, "config3": lambda: scenes.config3(160, 128),
+         "planes_nan": _nan_plane_scene, "extreme": extreme, "config4": lambda: scenes.config4(96, 80)}[scene]()
+    for kv in (dict(src=25, src_occ=11), dict(src=26, src_occ=11, prefix_kb=1)):
+        with _with_tuning(gpu_ctx, verbose=1, **kv):
+            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
 
 
 def test_bvh_matches_brute_force_bit_for_bit_full_frame(gpu_ctx):
@@ -571,21 +556,13 @@ def _kernel_times_per_generation(gpu_ctx, base):
     kt = gpu_ctx.kernel_times()
     gens = 8 + 2
     assert kt["camera"][1] == 2 and kt["nearest"][1] == 2 * (gens - 1)
-    # shadow queries of the lit generations 0..max_depth (none past the cut-off): the
-    # plain kernel for every (record, light) pair, or the item lists from generation 1 on
-    assert kt["occlusion"][1] + kt["shadow"][1] == 2 * (gens - 1)      # config3 has lights
-    # shading runs in its own kernel unless the context is tuned fuse=1 (then inside the shadow kernels)
-    assert kt["shade"][1] in (0, 2 * (gens - 1))
-    # frame-end fold (default): one launch per chunk, in chain order
+    # shadow queries and shading of the lit generations 0..max_depth (none past the cut-off)
+    assert kt["occlusion"][1] == 2 * (gens - 1) and kt["shade"][1] == 2 * (gens - 1)   # config3 has lights
+    assert kt["shadow"][1] == 0 and kt["tail"][1] == 0
+    # frame-end fold: one launch per chunk, in chain order
     assert kt["fold"][1] == 2 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
     assert all(n == 0 for ms, n in gpu_ctx.kernel_times().values())   # harvested
-    # eager fold: one wf_fold_gen per generation, on the shading streams
-    with _with_tuning(gpu_ctx, eager_fold=1):
-        t = gpu_ctx.render(lr.render_opts(64, 48, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS, **base))
-    assert np.array_equal(plain[1], t[1])
-    kt = gpu_ctx.kernel_times()
-    assert kt["fold"][1] == gens and kt["tally"][1] == 1
 
 
 def _with_tuning(ctx, **kv):
@@ -686,23 +663,17 @@ def test_oversized_budget_falls_back_to_smaller_chunks():
 
 
 def test_tuning_knobs_do_not_change_results(gpu_ctx):
-    """Schedule knobs (one stream, no camera tiles, workgroup-first dealing,
-    fused shading with shadow lists, other region counts, the frame-end fold
-    instead of the per-generation one) leave every bit of a C3-workload frame
+    """Schedule knobs (one stream, per-ray camera rays, workgroup-first dealing,
+    other region counts and stream counts, other sphere sources, the fused tail
+    from several generations and widths) leave every bit of a C3-workload frame
     unchanged."""
     spec = scenes.config3(192, 160)
     base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
-    for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(fuse=1), dict(fuse=1, lists0=1), dict(fuse_from=3), dict(fuse_from=0), dict(regions=96),
-               dict(bstreams=1), dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10),
-               dict(tail_from=0), dict(tail_from=1, tail_max=1 << 30), dict(tail_from=2, tail_max=20000, lists=0),
-               dict(tail_from=1, tail_max=1 << 30, regions=96), dict(eager_fold=1), dict(eager_fold=1, split=0),
-               dict(eager_fold=1, fuse=1), dict(split=0, fuse_from=2), dict(bstreams=3), dict(bstreams=3, fuse=1),
-               dict(fold_split=1), dict(fold_split=4), dict(fold_split=8), dict(fold_split=3, bstreams=1),
-               dict(fold_split=2, fuse=1), dict(fold_split=5, bstreams=3), dict(bmerge=1), dict(bmerge=3),
-               dict(bmerge=5, tail_from=1, tail_max=1 << 30), dict(bmerge=2, regions=2048), dict(wave_max=0),
-               dict(wave_max=1 << 30), dict(wave_max=1 << 30, regions=96), dict(wave_max=500, bmerge=4), dict(cam=3),
+    for kv in [dict(split=0), dict(cam=0), dict(deal=0), dict(regions=96), dict(bstreams=1), dict(bstreams=3),
+               dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10), dict(src=7, src_occ=7),
+               dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
-               dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, tail_fold=1)]:
+               dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

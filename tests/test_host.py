@@ -29,7 +29,7 @@ def test_abi_struct_sizes_match_header():
     assert C.sizeof(lr.rt_object) == 4 + 4 + 48 + 72 + 8 + 8 + 4 + 4
     assert C.sizeof(lr.rt_render_opts) == 16 * 4 + 8     # ABI 2: + seed
     assert C.sizeof(lr.rt_light) == 8 + 72 + 24
-    assert C.sizeof(lr.rt_stats) == 10 * 8                 # ABI 3: + chunks (RT_ABI_VERSION 4)
+    assert C.sizeof(lr.rt_stats) == 10 * 8                 # `chunks` since ABI 3; unchanged at ABI 4
 
 
 def test_env_tuning_is_opt_in_and_validated(monkeypatch):

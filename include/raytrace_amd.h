@@ -269,6 +269,12 @@ int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* 
  * render are read with rt_ctx_stats (which synchronises). */
 int rt_render_device(rt_ctx* ctx, const rt_render_opts* opts, void* d_rgb, void* d_bgr, void* stream);
 int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
+/* Diagnostic (device): the sphere test's division t = x / (2a) (shapes.rs:68,75)
+ * computed as the device computes it (the per-ray reciprocal of 2a finished with
+ * the division's own correction steps, DESIGN.md §4 "Division by 2a") -> fast[i],
+ * and as the device's own f64 division -> slow[i], for n operand pairs.  Tests
+ * compare both with IEEE division bit for bit.  Synchronous. */
+int rt_div_a2_check(rt_ctx* ctx, const double* x, const double* a, uint32_t n, double* fast, double* slow);
 /* Queue sizes of the last wavefront chunk: queue[k] = rays traced at depth k
  * (generation 0: 0, the camera rays are not queued), shaded[k] = hits that
  * issued shadow queries.  Diagnostic. */

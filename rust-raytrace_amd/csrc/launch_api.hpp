@@ -81,6 +81,8 @@ struct WfStreams {
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
+// Diagnostic: div_a2(x, sphere_k(a)) and x / (2a) on the device (rt_div_a2_check).
+hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s);
 
 // The general path (path_kernel.hip): every material / light / camera class,
 // keyed random draws, one work-item per pixel over the HBM recursion stack.

@@ -1312,6 +1312,29 @@ int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bg
     return guarded(c, [&] { return render_device(c, o, d_rgb, d_bgr, stream); });
 }
 
+int rt_div_a2_check(rt_ctx* c, const double* x, const double* a, uint32_t n, double* fast, double* slow) {
+    if (!c || (n && (!x || !a || !fast || !slow))) return RT_E_INVALID;
+    if (n == 0) return RT_OK;
+    return guarded(c, [&] {
+        HIP_TRY(c, hipSetDevice(c->device));
+        const size_t bytes = static_cast<size_t>(n) * sizeof(double);
+        double* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, 4 * bytes));
+        auto body = [&]() -> int {
+            HIP_TRY(c, hipMemcpyAsync(d, x, bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(d + n, a, bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_div_a2_probe(d, d + n, n, d + 2 * static_cast<size_t>(n), d + 3 * static_cast<size_t>(n), c->stream));
+            HIP_TRY(c, hipMemcpyAsync(fast, d + 2 * static_cast<size_t>(n), bytes, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(slow, d + 3 * static_cast<size_t>(n), bytes, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            return RT_OK;
+        };
+        const int rc = body();
+        (void)hipFree(d);
+        return rc;
+    });
+}
+
 int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));

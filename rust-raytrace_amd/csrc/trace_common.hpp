@@ -265,10 +265,20 @@ __device__ __forceinline__ bool occluded_brute(const DevScene& sc, SpherePtr S, 
 // rounded outward on the host; here every slab interval is computed in f32
 // from the f32-rounded ray and then widened by a relative kBoxTol, which
 // covers the f32 rounding of origin, direction and slab arithmetic (each a few
-// ulps, relative to the t values they perturb).  Direction components below
-// 1e-20 are clamped (no 0 * inf NaNs); such a ray moves < 1e-14 along that
-// axis over any relevant t, far below the box padding.  DESIGN.md "BVH
-// exactness" has the argument in full.
+// ulps, relative to the t values they perturb).  The slab test runs on the
+// direction scaled by a power of two 2^-te that brings its largest component
+// into [0.5, 1) whenever that component lies outside [2^-20, 2^20] (te = 0,
+// no scaling, for the unit-length camera, reflection and point-light shadow
+// rays): t' = t 2^te, exactly, and every t limit handed to the box tests is
+// scaled the same way (t_limit(rb, t)).  Without it the f32 direction of a
+// directional light's unnormalised shadow ray (-direction, raytrace.rs:41,
+// scene.rs:131-139) or of a reflection off a plane whose normal is far from
+// unit length over- or underflows, or has every component clamped (round 5:
+// a light of magnitude 1e-35 culled occluders).  Direction components below
+// 1e-20 of the scaled direction are clamped (no 0 * inf NaNs); such a ray
+// moves < 1e-14 relative to its largest component along that axis over any
+// relevant t, far below the box padding.  DESIGN.md "BVH exactness" has the
+// argument in full.
 constexpr float kBoxTol = 1e-5f;
 constexpr int kBvhStack = 64;      // host builder bounds the depth (median splits past depth 40)
 constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst case (bvh4_stack_need) against it
@@ -276,9 +286,11 @@ constexpr int kBvh4Stack = 64;     // 4-wide: the host checks the tree's worst c
 // f32 image of a ray for the slab tests: 1/d per axis and -o/d, so each slab
 // bound is one FMA, fma(lo, 1/d, -o/d).  The FMA's rounding terms are of the
 // same two kinds the tolerance argument covers: relative to t (rounding of
-// 1/d and of the result) and a spatial 2^-24 |o| from rounding o/d.
+// 1/d and of the result) and a spatial 2^-24 |o| from rounding o/d.  te: the
+// slab t values are t 2^te (see above).
 struct RayBox {
     float ix, iy, iz, nox, noy, noz;
+    int32_t te;
 };
 
 __device__ __forceinline__ float inv_dir(double d) {
@@ -288,9 +300,12 @@ __device__ __forceinline__ float inv_dir(double d) {
 }
 
 __device__ __forceinline__ RayBox make_raybox(const Ray& r) {
-    const float ix = inv_dir(r.dx), iy = inv_dir(r.dy), iz = inv_dir(r.dz);
+    const double m = fmax(fmax(fabs(r.dx), fabs(r.dy)), fabs(r.dz));
+    // (NaN and infinite directions keep te = 0: their t values are NaN anyway)
+    const int32_t te = (m > 0x1p20 && m < __builtin_huge_val()) || (m < 0x1p-20 && m > 0.0) ? ilogb(m) + 1 : 0;
+    const float ix = inv_dir(ldexp(r.dx, -te)), iy = inv_dir(ldexp(r.dy, -te)), iz = inv_dir(ldexp(r.dz, -te));
     return RayBox{ix, iy, iz, -(static_cast<float>(r.ox) * ix), -(static_cast<float>(r.oy) * iy),
-                  -(static_cast<float>(r.oz) * iz)};
+                  -(static_cast<float>(r.oz) * iz), te};
 }
 
 // Slab bound t at coordinate v along the axis with (1/d, -o/d) = (i, no).
@@ -326,6 +341,8 @@ __device__ __forceinline__ float t_limit(double t) {
     if (static_cast<double>(f) < t) f = __uint_as_float(__float_as_uint(f) + 1u);   // next f32 up (t >= 0)
     return f + kBoxTol * f;
 }
+// ... in the scaled t of the ray's slab tests (t 2^te, exact; te = 0 for unit-length rays)
+__device__ __forceinline__ float t_limit(const RayBox& rb, double t) { return t_limit(ldexp(t, rb.te)); }
 
 // Planes of the scene (always brute force: few, and they carry the NaN quirk).
 __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) {
@@ -528,7 +545,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
-    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(rb, h.t);
     RT_STACK_DECL(kReg, uint64_t);
     int32_t cur = sc.bvh_root;
     for (;;) {
@@ -555,7 +572,7 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
-                        tlim = t_limit(t);
+                        tlim = t_limit(rb, t);
                     }
                 }
             }
@@ -582,7 +599,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
-    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(rb, h.t);
     constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
     // kReg newest entries in registers (the LDS-prefix source), the rest in scratch;
     // kCompactBits > 0: 32-bit entries with that many code bits, kShortStack of them
@@ -658,7 +675,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;
-                        tlim = t_limit(t);
+                        tlim = t_limit(rb, t);
                     }
                 }
             }
@@ -701,7 +718,7 @@ __device__ __forceinline__ bool occluded_bvh(const DevScene& sc, const BvhView& 
     }
     const RayBox rb = make_raybox(r);
     // t*t < r2 implies t < sqrt(r2) (up to rounding, covered by t_limit's margin)
-    const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
+    const float tlim = has_range ? t_limit(rb, sqrt(r2)) : __builtin_inff();
     RT_STACK_DECL(kReg, int32_t);
     int32_t cur = sc.bvh_root;
     for (;;) {
@@ -812,7 +829,7 @@ __device__ __forceinline__ Hit nearest_q4(const DevScene& sc, const BvhView& v, 
     const double a = r.dx * r.dx + r.dy * r.dy + r.dz * r.dz;
     const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
-    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(h.t);
+    float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(rb, h.t);
     const bool fx = rb.ix < 0.0f, fy = rb.iy < 0.0f, fz = rb.iz < 0.0f;     // near slab bound = hi
     RT_STACK_DECL_N(0, uint64_t, kQ4Stack);
     rt_keep_in_scratch(stk_m);
@@ -873,7 +890,7 @@ __device__ __forceinline__ Hit nearest_q4(const DevScene& sc, const BvhView& v, 
                     const int32_t obj = v.obj[k];
                     if (tt < h.t || (tt == h.t && obj < h.obj)) {
                         h.t = tt; h.obj = obj; h.prim = k;
-                        tlim = t_limit(tt);
+                        tlim = t_limit(rb, tt);
                     }
                 }
             }
@@ -912,7 +929,7 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
         if (sphere_t(v.sph[hint], r, sk, t) && (!has_range || t * t < r2)) return true;
     }
     const RayBox rb = make_raybox(r);
-    const float tlim = has_range ? t_limit(sqrt(r2)) : __builtin_inff();
+    const float tlim = has_range ? t_limit(rb, sqrt(r2)) : __builtin_inff();
     // pushes are unconditional stores at the stack top (junk when nothing is
     // pushed; the next push overwrites it): no branch per child
     int32_t stk_m[kBvh4Stack];

@@ -1317,6 +1317,24 @@ extern "C" int rt_debug_stamps(unsigned long long* out, int n, int reset) {
 namespace rtamd {
 #endif
 
+// Diagnostic (rt_div_a2_check): the sphere test's division t = x / (2a) as
+// sphere_t computes it (sphere_k's hoisted reciprocal finished by div_a2) and
+// as the compiler's own f64 division, side by side.
+__global__ __launch_bounds__(256) void div_a2_probe(const double* x, const double* a, uint32_t n, double* fast,
+                                                    double* slow) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const SphK k = sphere_k(a[i]);
+        fast[i] = div_a2(x[i], k);
+        slow[i] = x[i] / (2.0 * a[i]);
+    }
+}
+
+hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s) {
+    const uint32_t blocks = std::max(1u, std::min(4096u, (n + 255u) / 256u));
+    hipLaunchKernelGGL(div_a2_probe, dim3(blocks), dim3(256), 0, s, x, a, n, fast, slow);
+    return hipGetLastError();
+}
+
 hipError_t upload_srgb_table(const double* avg255) {
     return hipMemcpyToSymbol(HIP_SYMBOL(c_srgb_avg), avg255, 255 * sizeof(double));
 }

@@ -125,6 +125,8 @@ def _load():
                                               P(C.c_int32), P(C.c_float), C.c_size_t, P(C.c_int64)]),
         "rt_qtree_nodes": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, P(C.c_float), P(C.c_int32), P(C.c_int32),
                                      C.c_size_t, P(C.c_int64)]),
+        "rt_div_a2_check": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), C.c_uint32, P(C.c_double),
+                                      P(C.c_double)]),
         "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
         "rt_ctx_get_tuning": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
         "rt_tuning_key": (C.c_char_p, [C.c_int]),
@@ -439,6 +441,19 @@ class Context:
         s = (C.c_uint32 * n)()
         _check(lib.rt_ctx_generation_counts(self._h, q, s, n), self._h)
         return list(q), list(s)
+
+    def div_a2_check(self, x, a):
+        """Diagnostic: (the sphere test's x / (2a) as the device computes it, the
+        device's own f64 division) for float64 arrays x, a (rt_div_a2_check)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        assert x.shape == a.shape and x.ndim == 1
+        fast = np.empty_like(x)
+        slow = np.empty_like(x)
+        P = C.POINTER(C.c_double)
+        _check(lib.rt_div_a2_check(self._h, x.ctypes.data_as(P), a.ctypes.data_as(P), x.size, fast.ctypes.data_as(P),
+                                   slow.ctypes.data_as(P)), self._h)
+        return fast, slow
 
     def kernel_times(self):
         """{family: (summed ms, launches)} over the RT_TIME_KERNELS renders since

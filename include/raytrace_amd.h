@@ -290,7 +290,7 @@ enum rt_kernel_family {
     RT_KF_FOLD = 3,         /* wf_fold */
     RT_KF_TALLY = 4,        /* wf_tally */
     RT_KF_CAMERA = 5,       /* wf_nearest, generation 0 (camera rays) */
-    RT_KF_SHADOW = 6,       /* (unused since round 5: the shadow item lists were removed) */
+    RT_KF_COMPOSE = 6,      /* wf_compose: the row-ordered frame pass (tuning compose) */
     RT_KF_TAIL = 7,         /* wf_tail: the fused generations >= tail_fuse */
     RT_KF_COUNT = 8
 };
@@ -316,7 +316,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * lights all have light-view grids finish in one launch, one chain per
  * work-item through its remaining bounces, folded there; 0 off, -1 auto),
  * tail_width (that launch's chains per wave, 0 auto), qtree (1: trees beyond
- * LDS take the quantised 4-wide tree for the nearest hit).
+ * LDS take the quantised 4-wide tree for the nearest hit), compose (1: the
+ * chains' final colours go to a per-chain buffer and one row-ordered pass,
+ * RT_KF_COMPOSE, writes the frame with coalesced stores; 0: each chain writes
+ * its pixel as it ends).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

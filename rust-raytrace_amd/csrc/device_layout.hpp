@@ -256,7 +256,12 @@ struct PathStack {
 //   term     terminal colour of each chain [3][capa] (f64), then nlev (u8,
 //            levels pushed) [capa];
 //   rq / rs  [k*G + r]: entries of region r of Q_k / of generation k's records;
-//   cpix     the chunk pixel of each chain [qcap] (u32).
+//   cpix     the chunk pixel of each chain [qcap] (u32);
+//   pmap     (compose) per chunk pixel [cap]: its chain, or kPixBackground /
+//            kPixAmbient | object for a camera ray that ended without a chain;
+//   ccol     (compose) per chain [capa]: final colour f32 r,g,b and the sRGB
+//            bytes b | g << 8 | r << 16 (16 B), written by the fold in chain
+//            order and read by wf_compose, which writes the frame row by row.
 // Queue and record arrays are G regions of R entries (qcap = G*R); region r is
 // written only by workgroup r of the producing kernel.
 struct WfBufs {
@@ -265,7 +270,7 @@ struct WfBufs {
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
     uint64_t qcap;                  // G * R
-    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix;   // byte offsets of the sections
+    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix, o_pmap, o_ccol;   // byte offsets of the sections
     uint32_t cap;                   // pixel capacity
     uint32_t capa;                  // qcap rounded up to 64: stride of the per-chain arrays (levels,
                                     // terminals; chain c = generation 0's record entry c)
@@ -277,6 +282,8 @@ struct WfBufs {
     uint32_t spread_below;          // queues below this many items are dealt workgroup-first regardless
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
+    uint32_t compose;               // 1: final colours go through pmap / ccol and wf_compose writes the
+                                    //   frame in row order; 0: the camera pass and the fold write pixels
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
@@ -297,10 +304,14 @@ struct WfBufs {
     RT_HD double* term(int f) const { return reinterpret_cast<double*>(mem + o_term) + static_cast<uint64_t>(f) * capa; }
     RT_HD uint8_t* nlev() const { return reinterpret_cast<uint8_t*>(reinterpret_cast<double*>(mem + o_term) + 3ull * capa); }
     RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
+    RT_HD uint32_t* pmap() const { return reinterpret_cast<uint32_t*>(mem + o_pmap); }   // chunk pixel -> chain / code
+    RT_HD uint32_t* ccol() const { return reinterpret_cast<uint32_t*>(mem + o_ccol); }   // chain c -> final colour [4c, 4c+4)
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
 };
 constexpr uint32_t kNlevRunning = 0xFFu;   // WfBufs::nlev of a chain that has not ended yet
+constexpr uint32_t kPixBackground = 0xFFFFFFFFu;   // WfBufs::pmap: the camera ray missed every object
+constexpr uint32_t kPixAmbient = 0x80000000u;      // ... | object: it ended on that object's ambient colour
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
 constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G

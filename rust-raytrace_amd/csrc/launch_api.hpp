@@ -11,7 +11,7 @@ namespace rtamd {
 
 // Kernel families of the wavefront schedule (rt_ctx_kernel_times indices).
 enum KernelFamily : int8_t {
-    kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCamera = 5, kKfShadow = 6, kKfTail = 7, kKfCount = 8
+    kKfNearest = 0, kKfOcclusion = 1, kKfShade = 2, kKfFold = 3, kKfTally = 4, kKfCamera = 5, kKfCompose = 6, kKfTail = 7, kKfCount = 8
 };
 
 // Per-launch timing (RT_TIME_KERNELS): begin() records a start event before a

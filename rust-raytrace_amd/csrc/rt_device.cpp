@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -83,6 +83,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"qtree", 0, 0, 1},                          // 1: trees beyond the f32 tree's LDS budget take the quantised 4-wide
                                                  // tree (src 25 whole in LDS, 26 LDS prefix + L2) for the nearest hit;
                                                  // measured slower than binary16 (C4 55.0 vs 50.4 ms, C5 330 vs 307 ms)
+    {"compose", 1, 0, 1},                        // 1: the frame is written row by row by wf_compose from the fold's
+                                                 // chain-ordered colours (coalesced stores); 0: per pixel by the
+                                                 // camera pass and the fold
 };
 
 }  // namespace
@@ -362,8 +365,10 @@ void drop_lanes(rt_ctx* c) {
 
 // Working-set bytes per pixel slot of a chunk (ensure_wf's sections, per slot):
 // two queues, one shade-record array and one level array per lit generation,
-// terminals and level counts, the chain's pixel.
-uint64_t wf_bytes_per_slot(uint64_t levels) { return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + 4; }
+// terminals and level counts, the chain's pixel, the pixel map and the chain colours.
+uint64_t wf_bytes_per_slot(uint64_t levels) {
+    return 2ull * 8 * 8 + levels * (7 * 8 + 4 * 4) + levels * (4 * 8 + 4) + (3 * 8 + 1) + 4 + 4 + 16;
+}
 
 // Default working-set budget of a render (all lanes): 85% of what the device
 // has free plus what this context's lanes already hold, at most kWfBudget.
@@ -416,6 +421,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     const uint64_t s_term = capa * (3 * 8 + 1);
     const uint64_t s_reg = static_cast<uint64_t>(kMaxGenerations) * G * 4;
     const uint64_t s_cpix = q * 4;
+    const uint64_t s_pmap = static_cast<uint64_t>(cap) * 4;
+    const uint64_t s_ccol = capa * 16;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
     b.o_lev = off; off = align_up(off + s_lev, 256);
@@ -423,6 +430,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_rq = off; off = align_up(off + s_reg, 256);
     b.o_rs = off; off = align_up(off + s_reg, 256);
     b.o_cpix = off; off = align_up(off + s_cpix, 256);
+    b.o_pmap = off; off = align_up(off + s_pmap, 256);
+    b.o_ccol = off; off = align_up(off + s_ccol, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -1183,6 +1192,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
+            c->lanes[l].b.compose = c->t(kTuneCompose) != 0 ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
         // rt_render copies each chunk's rows as soon as that chunk's fold is done (the fold

@@ -299,10 +299,15 @@ __device__ __forceinline__ float inv_dir(double d) {
     return 1.0f / f;
 }
 
+#ifndef RT_DIR_SCALE
+#define RT_DIR_SCALE 1      // (A/B builds only: 0 = the round-4 unscaled slab tests, not exact for such rays)
+#endif
 __device__ __forceinline__ RayBox make_raybox(const Ray& r) {
     const double m = fmax(fmax(fabs(r.dx), fabs(r.dy)), fabs(r.dz));
-    // (NaN and infinite directions keep te = 0: their t values are NaN anyway)
-    const int32_t te = (m > 0x1p20 && m < __builtin_huge_val()) || (m < 0x1p-20 && m > 0.0) ? ilogb(m) + 1 : 0;
+    // m = f 2^te with f in [0.5, 1) (v_frexp_exp_i32_f64); NaN and infinite directions keep
+    // te = 0 (their t values are NaN anyway)
+    const int32_t te = RT_DIR_SCALE && ((m > 0x1p20 && m < __builtin_huge_val()) || (m < 0x1p-20 && m > 0.0))
+                           ? __builtin_amdgcn_frexp_exp(m) : 0;
     const float ix = inv_dir(ldexp(r.dx, -te)), iy = inv_dir(ldexp(r.dy, -te)), iz = inv_dir(ldexp(r.dz, -te));
     return RayBox{ix, iy, iz, -(static_cast<float>(r.ox) * ix), -(static_cast<float>(r.oy) * iy),
                   -(static_cast<float>(r.oz) * iz), te};

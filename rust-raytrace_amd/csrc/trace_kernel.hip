@@ -314,6 +314,17 @@ __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
                ldn_if<kNtQ>(&b.qf(q, 3)[i]), ldn_if<kNtQ>(&b.qf(q, 4)[i]), ldn_if<kNtQ>(&b.qf(q, 5)[i])};
 }
 
+// Occupancy / unrolling of the fold and shading kernels (A/B builds: EXTRA=-D...)
+#ifndef RT_FOLD_UNROLL
+#define RT_FOLD_UNROLL 4        // levels whose loads are issued together
+#endif
+#ifndef RT_FOLD_WAVES
+#define RT_FOLD_WAVES 1         // wf_fold's launch bounds: min waves per SIMD (1: the compiler's choice, 96 VGPRs)
+#endif
+#ifndef RT_SHADE_WAVES
+#define RT_SHADE_WAVES 1
+#endif
+
 // Sphere sources of the wavefront intersection kernels.
 constexpr int kSrcGlobal = 0;       // brute force, sphere list through the caches
 constexpr int kSrcLds = 1;          // brute force, sphere list staged in LDS per workgroup
@@ -446,6 +457,10 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     return v;
 }
 
+// register entries on top of the compact stack (A/B builds: EXTRA=-DRT_COMPACT_REG=n)
+#ifndef RT_COMPACT_REG
+#define RT_COMPACT_REG 0
+#endif
 // Scene::intersect of one ray through the source's structure (scene.rs:247-249).
 template <int kSrc, bool kCount>
 __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v, const Ray& r, Work* w) {
@@ -454,7 +469,7 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
     // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2)
-        return nearest_bvh_bl<kCount, 2, 0, Src<kSrc>::compact_bits>(sc, v, r, w);
+        return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact_bits ? RT_COMPACT_REG : 0, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh_bl<kCount, 0, 0>(sc, v, r, w);
@@ -519,6 +534,23 @@ __device__ __forceinline__ Col end_colour(const DevScene& sc, int32_t obj) {
     return Col{m.amb[0], m.amb[1], m.amb[2]};
 }
 
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
+
+// The final colour of chain c (pixel p of the chunk): into ccol[c] for wf_compose
+// (chain order: coalesced), or straight into the frame.
+__device__ __forceinline__ void emit_chain(const FrameParams& fp, const WfBufs& b, uint32_t c, uint32_t p, Col res,
+                                           const double* srgb) {
+    if (b.compose) {
+        const uint32_t q = static_cast<uint32_t>(to_srgb(res.b, srgb)) | (static_cast<uint32_t>(to_srgb(res.g, srgb)) << 8) |
+                           (static_cast<uint32_t>(to_srgb(res.r, srgb)) << 16);
+        const U32x4 v = {__float_as_uint(static_cast<float>(res.r)), __float_as_uint(static_cast<float>(res.g)),
+                         __float_as_uint(static_cast<float>(res.b)), q};
+        stn(reinterpret_cast<U32x4*>(b.ccol()) + c, v);
+    } else {
+        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, srgb);
+    }
+}
+
 // Chain c ends in generation k with colour col (wf_fold folds its k levels onto it).
 __device__ __forceinline__ void set_terminal(const WfBufs& b, uint32_t c, Col col, int k) {
     stn(&b.term(0)[c], col.r); stn(&b.term(1)[c], col.g); stn(&b.term(2)[c], col.b);
@@ -563,8 +595,12 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
     int32_t end_obj = INT32_MAX;
     if (live) {
         if (h.obj == INT32_MAX) {                                           // raytrace.rs:265, 228-232
-            if constexpr (kCam) write_background_pixel(fp, b, p);          // no levels: final now
-            else ends = true;
+            if constexpr (kCam) {                                           // no levels: final now
+                if (b.compose) stn(&b.pmap()[p], kPixBackground);
+                else write_background_pixel(fp, b, p);
+            } else {
+                ends = true;
+            }
         } else {
             const DevMaterial& m = sc.mats[h.obj];
             if (static_cast<uint32_t>(k) > fp.max_depth) {                  // raytrace.rs:33 / 126
@@ -592,13 +628,16 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         }
     }
     if (ends) {
-        if constexpr (kCam)                                // no levels: the final pixel now
-            write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, average_samples(end_colour(sc, end_obj), fp.spp));
-        else
+        if constexpr (kCam) {                              // no levels: the final pixel now
+            if (b.compose) stn(&b.pmap()[p], kPixAmbient | static_cast<uint32_t>(end_obj));
+            else write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, average_samples(end_colour(sc, end_obj), fp.spp));
+        } else {
             set_terminal(b, p, end_colour(sc, end_obj), k);
+        }
     }
     const uint32_t slot = lds_append(&counts[0], shade);
     const uint32_t chain = kCam ? static_cast<uint32_t>(obase) + slot : p;   // (slot valid when shade)
+    if (kCam && shade && b.compose) stn(&b.pmap()[p], chain);
     if (shade) {
         const size_t at = rbase + slot;
         stn(&b.rf(0)[at], ptx); stn(&b.rf(1)[at], pty); stn(&b.rf(2)[at], ptz);
@@ -864,7 +903,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
 
 // The Phong sum of every shade record of generation k.
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
+__global__ __launch_bounds__(kWfThreads, RT_SHADE_WAVES) void wf_shade(DevScene sc, FrameParams fp, WfBufs b, int k) {
     __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
     region_scan(b.rs() + k * b.G, b.G, s_scan, s_wave);
@@ -954,20 +993,21 @@ __device__ __forceinline__ Col tail_chain(const DevScene& sc, const FrameParams&
 // levels instead of two per level.
 template <bool kFresnel>
 __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, uint32_t p, int nlev, Col acc) {
-    for (int k = nlev - 1; k >= 0; k -= 4) {
-        double sr[4], sg[4], sb[4];
-        int32_t ob[4];
+    constexpr int U = RT_FOLD_UNROLL;
+    for (int k = nlev - 1; k >= 0; k -= U) {
+        double sr[U], sg[U], sb[U];
+        int32_t ob[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (k - u >= 0) {
                 const size_t at = static_cast<size_t>(k - u) * b.capa + p;
                 ob[u] = ldn_if<kNtFold>(&b.lobj()[at]);
                 sr[u] = ldn_if<kNtFold>(&b.lf(0)[at]); sg[u] = ldn_if<kNtFold>(&b.lf(1)[at]); sb[u] = ldn_if<kNtFold>(&b.lf(2)[at]);
             }
         }
-        double kr[4], kg[4], kb[4], kf[4];
+        double kr[U], kg[U], kb[U], kf[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (k - u >= 0) {
                 const DevMaterial& m = sc.mats[ob[u]];
                 kr[u] = m.ks[0]; kg[u] = m.ks[1]; kb[u] = m.ks[2];
@@ -975,7 +1015,7 @@ __device__ __forceinline__ Col fold_levels(const DevScene& sc, const WfBufs& b, 
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (k - u >= 0) {                  // res + (ks * child) * f, f = 1 for Phong (raytrace.rs:63 / 163)
                 acc.r = sr[u] + (kr[u] * acc.r) * kf[u];
                 acc.g = sg[u] + (kg[u] * acc.g) * kf[u];
@@ -1038,8 +1078,7 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
         int nlev = 0;
         const Col term = tail_chain<kFresnel, kCount>(sc, fp, b, v, T - 1, in, nlev, s_cnt, wn, wsh);
         const Col res = average_samples(fold_levels<kFresnel>(sc, b, in.c, nlev, term), fp.spp);
-        const uint32_t p = b.cpix()[in.c];
-        write_pixel(fp, p % fp.tile_w, fp.row0 + p / fp.tile_w, res, s_srgb);
+        emit_chain(fp, b, in.c, b.compose ? 0u : b.cpix()[in.c], res, s_srgb);
     }
     __syncthreads();
     for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
@@ -1068,7 +1107,7 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
 // by generation T-1 fold on a B stream while the tail runs (every level and
 // terminal they need is written by then); the tail folds its own.
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
+__global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
     __shared__ double s_srgb[255];
     __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
@@ -1087,7 +1126,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
         if (j < n) {
             hd.c = static_cast<uint32_t>(region_entry(s_scan, b.G, b.R, static_cast<uint32_t>(j)));
             hd.nlev = b.nlev()[hd.c];
-            hd.p = b.cpix()[hd.c];
+            hd.p = b.compose ? 0u : b.cpix()[hd.c];
             hd.term = Col{ldn_if<kNtFold>(&b.term(0)[hd.c]), ldn_if<kNtFold>(&b.term(1)[hd.c]),
                           ldn_if<kNtFold>(&b.term(2)[hd.c])};
         }
@@ -1099,7 +1138,7 @@ __global__ __launch_bounds__(kWfThreads) void wf_fold(DevScene sc, FrameParams f
         const Head nxt = head(static_cast<uint64_t>(rc + W) * 64u + lane);
         if (cur.nlev >= lo && cur.nlev <= hi) {             // (kNlevRunning: not ended yet, or no chain)
             const Col res = average_samples(fold_levels<kFresnel>(sc, b, cur.c, static_cast<int>(cur.nlev), cur.term), fp.spp);
-            write_pixel(fp, cur.p % fp.tile_w, fp.row0 + cur.p / fp.tile_w, res, s_srgb);
+            emit_chain(fp, b, cur.c, cur.p, res, s_srgb);
         }
         cur = nxt;
     }
@@ -1112,6 +1151,88 @@ hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& 
     if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
+}
+
+// The frame of the chunk, row by row (WfBufs::compose): each wave writes 64
+// consecutive pixels of one row -- their f32 RGB as 192 consecutive dwords and
+// their sRGB BGR as 48 consecutive dwords (or bytes when the row pitch is not a
+// multiple of 4), staged through LDS so every store instruction covers
+// consecutive addresses -- from the pixel map (chain, background or ambient
+// object) and the chains' colours in ccol.  The colours are the fold's /
+// write_pixel's values: f32 of the averaged f64 colour and to_srgb of it.
+constexpr int kComposeWaves = kWfThreads / 64;
+__global__ __launch_bounds__(kWfThreads) void wf_compose(DevScene sc, FrameParams fp, WfBufs b) {
+    __shared__ float s_rgb[kComposeWaves][192];
+    __shared__ uint32_t s_bgr[kComposeWaves][48];
+    __shared__ double s_srgb[255];
+    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t segs = (fp.tile_w + 63u) / 64u;                    // 64-pixel segments per row
+    const uint64_t total = static_cast<uint64_t>(segs) * fp.rows;
+    const bool dw = ((fp.bgr_pitch | reinterpret_cast<uintptr_t>(fp.out_bgr)) & 3u) == 0;   // dword-aligned BGR rows
+    for (uint64_t sg = static_cast<uint64_t>(blockIdx.x) * kComposeWaves + wave; sg < total;
+         sg += static_cast<uint64_t>(gridDim.x) * kComposeWaves) {     // wave-uniform
+        const uint32_t lrow = static_cast<uint32_t>(sg / segs), x0 = static_cast<uint32_t>(sg % segs) * 64u;
+        const uint32_t nv = min(64u, fp.tile_w - x0);                 // pixels in this segment
+        const uint32_t x = x0 + lane;
+        float r = 0.0f, g = 0.0f, bl = 0.0f;
+        uint32_t q = 0;
+        if (lane < nv) {
+            const uint32_t code = ldn(&b.pmap()[static_cast<size_t>(lrow) * fp.tile_w + x]);
+            if (code == kPixBackground) {
+                r = fp.bg_rgb[0]; g = fp.bg_rgb[1]; bl = fp.bg_rgb[2];
+                q = fp.bg_bgr[0] | (static_cast<uint32_t>(fp.bg_bgr[1]) << 8) | (static_cast<uint32_t>(fp.bg_bgr[2]) << 16);
+            } else if (code & kPixAmbient) {                           // (rare) the ambient colour of a camera hit
+                const Col res = average_samples(end_colour(sc, static_cast<int32_t>(code & ~kPixAmbient)), fp.spp);
+                r = static_cast<float>(res.r); g = static_cast<float>(res.g); bl = static_cast<float>(res.b);
+                q = static_cast<uint32_t>(to_srgb(res.b, s_srgb)) | (static_cast<uint32_t>(to_srgb(res.g, s_srgb)) << 8) |
+                    (static_cast<uint32_t>(to_srgb(res.r, s_srgb)) << 16);
+            } else {
+                const U32x4 cc = ldn(reinterpret_cast<const U32x4*>(b.ccol()) + code);
+                r = __uint_as_float(cc[0]); g = __uint_as_float(cc[1]); bl = __uint_as_float(cc[2]);
+                q = cc[3];
+            }
+        }
+        const uint32_t orow = fp.row0 + lrow;
+        if (fp.out_rgb) {
+            s_rgb[wave][3 * lane] = r; s_rgb[wave][3 * lane + 1] = g; s_rgb[wave][3 * lane + 2] = bl;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            float* dst = fp.out_rgb + (static_cast<size_t>(orow) * fp.tile_w + x0) * 3;
+#pragma unroll
+            for (uint32_t j = 0; j < 3; ++j) {
+                const uint32_t i = lane + 64u * j;
+                if (i < 3 * nv) dst[i] = s_rgb[wave][i];
+            }
+        }
+        if (fp.out_bgr) {
+            uint8_t* row = fp.out_bgr + static_cast<size_t>(orow) * fp.bgr_pitch;
+            if (dw) {
+                uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr[wave]);
+                sb[3 * lane] = static_cast<uint8_t>(q); sb[3 * lane + 1] = static_cast<uint8_t>(q >> 8);
+                sb[3 * lane + 2] = static_cast<uint8_t>(q >> 16);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                // dwords [0, ceil(3 nv / 4)) of the segment; bytes past 3 nv are row padding (zero)
+                const uint32_t nd = (3 * nv + 3) / 4;
+                if (lane < nd) {
+                    uint32_t v = s_bgr[wave][lane];
+                    const uint32_t valid = 3 * nv - 4 * lane;                // bytes of this dword that are pixels
+                    if (valid < 4) v &= (1u << (8 * valid)) - 1u;
+                    reinterpret_cast<uint32_t*>(row + 3 * x0)[lane] = v;
+                }
+                __builtin_amdgcn_wave_barrier();
+            } else if (lane < nv) {
+                row[3 * x] = static_cast<uint8_t>(q); row[3 * x + 1] = static_cast<uint8_t>(q >> 8);
+                row[3 * x + 2] = static_cast<uint8_t>(q >> 16);
+            }
+            if (x0 + nv == fp.tile_w)                                  // BMP row padding is zero (main.rs:42)
+                for (uint32_t k = (dw ? (3 * fp.tile_w + 3) & ~3u : 3 * fp.tile_w) + lane; k < fp.bgr_pitch; k += 64)
+                    row[k] = 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // Scene::intersect calls of this chunk: every pixel's camera ray, every later
@@ -1292,6 +1413,13 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     // the chains not folded yet (all of them without the fused tail, which folded every chain:
     // its own as it ended them, the others on a B stream)
     if (ws.tail_fuse == 0 && (e = launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess) return e;
+    if (b.compose) {                         // the frame, row by row, once every chain has its colour
+        if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
+        const uint64_t segs = static_cast<uint64_t>((fp.tile_w + 63u) / 64u) * fp.rows;
+        const uint32_t wgs = static_cast<uint32_t>(std::min<uint64_t>(4u * b.G, (segs + kComposeWaves - 1) / kComposeWaves));
+        hipLaunchKernelGGL(wf_compose, dim3(std::max(1u, wgs)), dim3(kWfThreads), 0, ws.a, sc, fp, b);
+        if (ws.ma && (e = ws.ma->mark(ws.a, kKfCompose)) != hipSuccess) return e;
+    }
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
     if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, ws.a)) != hipSuccess) return e;
     return hipGetLastError();

@@ -30,7 +30,7 @@ RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AREA = 0, 1, 2
 RT_CAMERA_SIMPLE, RT_CAMERA_DOF = 0, 1
 RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
 RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK, RT_TIME_KERNELS = 1, 2, 4, 8
-KERNEL_FAMILIES = ("nearest", "occlusion", "shade", "fold", "tally", "camera", "shadow", "tail")   # rt_kernel_family
+KERNEL_FAMILIES = ("nearest", "occlusion", "shade", "fold", "tally", "camera", "compose", "tail")   # rt_kernel_family
 RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL, RT_ALGO_WAVEFRONT, RT_ALGO_WAVEFRONT_BRUTE = 0, 1, 2, 3, 4
 RT_ALGO_PATH = 5
 RT_JITTER_CENTER, RT_JITTER_RANDOM = 0, 1

@@ -579,7 +579,8 @@ def _kernel_times_per_generation(gpu_ctx, base):
     assert kt["camera"][1] == 2 and kt["nearest"][1] == 2 * (gens - 1)
     # shadow queries and shading of the lit generations 0..max_depth (none past the cut-off)
     assert kt["occlusion"][1] == 2 * (gens - 1) and kt["shade"][1] == 2 * (gens - 1)   # config3 has lights
-    assert kt["shadow"][1] == 0 and kt["tail"][1] == 0
+    assert kt["tail"][1] == 0
+    assert kt["compose"][1] == 2 * gpu_ctx.get_tuning("compose")      # one row-ordered frame pass per render
     # frame-end fold: one launch per chunk, in chain order
     assert kt["fold"][1] == 2 and kt["tally"][1] == 2
     assert all(ms > 0 for ms, n in kt.values() if n)
@@ -694,12 +695,37 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(src=2, src_occ=11), dict(compact_stack=0), dict(src=7, src_occ=10), dict(src=7, src_occ=7),
                dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
-               dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0)]:
+               dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
+               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv
         assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), kv
         assert got[2].rays == base[2].rays, kv
+
+
+@pytest.mark.parametrize("compose", [1, 0])
+def test_row_ordered_compose_matches_oracle(gpu_ctx, compose):
+    """The row-ordered frame pass (tuning compose, trace_kernel.hip wf_compose):
+    widths around the 64-pixel segment (1, 63, 64, 65, 130, 197), tight BGR rows
+    (3 w bytes: byte stores) and dword-padded rows with extra slack (dword
+    stores, the padding zeroed), misses, ambient ends and chains in one frame:
+    the oracle's BGR bytes and f32 colours either way, with and without the
+    fused tail."""
+    for w, h in [(1, 5), (63, 9), (64, 7), (65, 11), (130, 6), (197, 13)]:
+        spec = scenes.config3(w, h)
+        spec.max_depth = 3
+        ref = ref64.render(spec)
+        for tail in (0, 2):
+            with _with_tuning(gpu_ctx, compose=compose, tail_fuse=tail):
+                gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+                for pitch in (0, ((3 * w + 3) & ~3) + 8):
+                    o = lr.render_opts(w, h, max_depth=spec.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT, bgr_pitch=pitch)
+                    rgb, bgr, st = gpu_ctx.render(o)
+                    assert np.array_equal(bgr[:, :3 * w], ref["bgr"]), (w, h, tail, pitch)
+                    assert (bgr[:, 3 * w:] == 0).all(), (w, h, tail, pitch)
+                    check_close(rgb, ref["rgb64"])
+                    assert st.rays == ref["counts"]["rays"]
 
 
 def test_default_spp_is_the_scenes_antialias(gpu_ctx):

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -86,6 +86,10 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"compose", 1, 0, 1},                        // 1: the frame is written row by row by wf_compose from the fold's
                                                  // chain-ordered colours (coalesced stores); 0: per pixel by the
                                                  // camera pass and the fold
+    {"host_chunks", 1, 1, 64},                   // rt_render into host memory: at least this many chunks, so the D2H
+                                                 // copy of one chunk's rows overlaps the next chunk's generations
+    {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
+                                                 // (0: equal chunks)
 };
 
 }  // namespace
@@ -1157,6 +1161,19 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                                                                : default_wf_budget(c);
             cap_px = std::max<uint64_t>(1, budget / static_cast<uint64_t>(lanes_req) / wf_bytes_per_slot(levels));
         }
+        // rt_render into host memory: chunks of at most tile_h / host_chunks rows (the copy of a
+        // chunk's rows overlaps the later chunks' generations); host_first sizes the first of two
+        uint32_t first_rows = 0;
+        if (c->want_bands && c->t(kTuneHostChunks) > 1) {
+            const uint64_t hc = static_cast<uint64_t>(c->t(kTuneHostChunks));
+            const uint64_t pf = static_cast<uint64_t>(c->t(kTuneHostFirst));
+            if (hc == 2 && pf > 0) {
+                first_rows = static_cast<uint32_t>(std::max<uint64_t>(8, (o->tile_h * pf / 100) / 8 * 8));
+                if (first_rows >= o->tile_h) first_rows = 0;
+                else cap_px = std::min<uint64_t>(cap_px, static_cast<uint64_t>((std::max(first_rows, o->tile_h - first_rows) + 7) / 8 * 8) * o->tile_w);
+            }
+            if (first_rows == 0) cap_px = std::min<uint64_t>(cap_px, (o->tile_h + hc - 1) / hc * o->tile_w);
+        }
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));
         uint32_t chunk_rows = 0, n_chunks = 0, G = 1, R = 0;
@@ -1166,6 +1183,11 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             chunk_rows = std::min(chunk_rows, (o->tile_h + 7) / 8 * 8);
             n_chunks = (o->tile_h + chunk_rows - 1) / chunk_rows;
             chunk_rows = std::max<uint32_t>(8, ((o->tile_h + n_chunks - 1) / n_chunks + 7) / 8 * 8);
+            if (first_rows) {                      // two chunks of first_rows and tile_h - first_rows rows
+                const uint32_t need = (std::max(first_rows, o->tile_h - first_rows) + 7) / 8 * 8;
+                if (n_chunks == 2 && need * static_cast<uint64_t>(o->tile_w) <= cap_px) chunk_rows = need;
+                else first_rows = 0;
+            }
             n_lanes = std::max(1, std::min<int>(lanes_req, static_cast<int>(n_chunks)));
             int rc2 = ensure_lanes(c, n_lanes);
             if (rc2 != RT_OK) return rc2;
@@ -1195,19 +1217,24 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->lanes[l].b.compose = c->t(kTuneCompose) != 0 ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
+        auto chunk_row0 = [&](uint32_t ci) { return first_rows ? (ci ? first_rows : 0u) : ci * chunk_rows; };
+        auto chunk_nrows = [&](uint32_t ci) {
+            return first_rows ? (ci ? o->tile_h - first_rows : first_rows) : std::min(chunk_rows, o->tile_h - ci * chunk_rows);
+        };
         // rt_render copies each chunk's rows as soon as that chunk's fold is done (the fold
         // runs in chain order, so a chunk's rows are final together)
         c->n_bands = 0;
         if (c->want_bands && n_chunks <= static_cast<uint32_t>(kMaxBands)) {
             for (uint32_t i = 0; i < n_chunks; ++i) {
                 if (!c->band_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->band_ev[i], hipEventDisableTiming));
-                c->band_row0[i] = i * chunk_rows;
-                c->band_nrows[i] = std::min(chunk_rows, o->tile_h - c->band_row0[i]);
+                c->band_row0[i] = chunk_row0(i);
+                c->band_nrows[i] = chunk_nrows(i);
             }
             c->n_bands = static_cast<int>(n_chunks);
         }
         if (c->t(kTuneVerbose))
-            std::fprintf(stderr, "rtamd: chunks %u x %u rows, lanes %d, G %u, R %u\n", n_chunks, chunk_rows, n_lanes, G, R);
+            std::fprintf(stderr, "rtamd: chunks %u x %u rows (first %u), lanes %d, G %u, R %u\n", n_chunks, chunk_rows, first_rows,
+                         n_lanes, G, R);
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
         // per-launch timing needs one in-order stream
         const bool timed = (o->flags & RT_TIME_KERNELS) != 0 && n_lanes == 1;
@@ -1229,8 +1256,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             rt_ctx::Lane& L = c->lanes[ci % n_lanes];
             if (ci > 0 && n_lanes > 1) HIP_TRY(c, hipStreamWaitEvent(L.s, c->lanes[(ci - 1) % n_lanes].mark, 0));
             FrameParams f = fp;
-            f.row0 = ci * chunk_rows;
-            f.rows = std::min(chunk_rows, o->tile_h - f.row0);
+            f.row0 = chunk_row0(ci);
+            f.rows = chunk_nrows(ci);
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
             WfStreams ws{};

@@ -728,6 +728,22 @@ def test_row_ordered_compose_matches_oracle(gpu_ctx, compose):
                     assert st.rays == ref["counts"]["rays"]
 
 
+def test_host_chunks_overlap_copies_bit_identically(gpu_ctx):
+    """rt_render into host memory in several chunks (tuning host_chunks,
+    host_first: each chunk's rows copied while the next one renders): the same
+    bytes and colours as one chunk, rows split unevenly, on one and two lanes."""
+    spec = scenes.config3(200, 147)
+    base = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+    for kv in [dict(host_chunks=2), dict(host_chunks=3), dict(host_chunks=2, host_first=30),
+               dict(host_chunks=2, host_first=70, lanes=2), dict(host_chunks=5, lanes=2)]:
+        with _with_tuning(gpu_ctx, **kv):
+            got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
+        assert np.array_equal(got[1], base[1]), kv
+        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), kv
+        assert got[2].rays == base[2].rays, kv
+        assert got[2].chunks == kv["host_chunks"] and base[2].chunks == 1, kv
+
+
 def test_default_spp_is_the_scenes_antialias(gpu_ctx):
     """rt_render_opts.spp = 0 (the default options) renders with the uploaded
     scene's Options.antialias (scene.rs:191-198)."""

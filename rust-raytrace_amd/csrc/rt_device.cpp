@@ -1172,7 +1172,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 if (first_rows >= o->tile_h) first_rows = 0;
                 else cap_px = std::min<uint64_t>(cap_px, static_cast<uint64_t>((std::max(first_rows, o->tile_h - first_rows) + 7) / 8 * 8) * o->tile_w);
             }
-            if (first_rows == 0) cap_px = std::min<uint64_t>(cap_px, (o->tile_h + hc - 1) / hc * o->tile_w);
+            if (first_rows == 0) cap_px = std::min<uint64_t>(cap_px, ((o->tile_h + hc - 1) / hc + 7) / 8 * 8 * o->tile_w);
         }
         const uint32_t tiles_x = (o->tile_w + 7) / 8;
         const int mark_gen = std::max(0, std::min<int>(static_cast<int>(c->t(kTuneStaggerGen)), static_cast<int>(o->max_depth) + 1));

@@ -83,9 +83,11 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"qtree", 0, 0, 1},                          // 1: trees beyond the f32 tree's LDS budget take the quantised 4-wide
                                                  // tree (src 25 whole in LDS, 26 LDS prefix + L2) for the nearest hit;
                                                  // measured slower than binary16 (C4 55.0 vs 50.4 ms, C5 330 vs 307 ms)
-    {"compose", 1, 0, 1},                        // 1: the frame is written row by row by wf_compose from the fold's
+    {"compose", 0, 0, 1},                        // 1: the frame is written row by row by wf_compose from the fold's
                                                  // chain-ordered colours (coalesced stores); 0: per pixel by the
-                                                 // camera pass and the fold
+                                                 // camera pass and the fold (C3 3.104-3.123 vs 3.235-3.243 ms with
+                                                 // 1: the pass itself takes 113 us, the scattered stores it
+                                                 // replaces cost the camera pass and the fold less than that)
     {"host_chunks", 1, 1, 64},                   // rt_render into host memory: at least this many chunks, so the D2H
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent

@@ -457,9 +457,11 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     return v;
 }
 
-// register entries on top of the compact stack (A/B builds: EXTRA=-DRT_COMPACT_REG=n)
+// register entries on top of the compact stack (the whole tree in LDS, src 9): one (C3 3.054 vs
+// 3.116 ms, 8-way share 0.756 vs 0.765 ms on one box; two 3.168 vs 3.144 ms); A/B builds:
+// EXTRA=-DRT_COMPACT_REG=n
 #ifndef RT_COMPACT_REG
-#define RT_COMPACT_REG 0
+#define RT_COMPACT_REG 1
 #endif
 // Scene::intersect of one ray through the source's structure (scene.rs:247-249).
 template <int kSrc, bool kCount>
@@ -467,7 +469,8 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     if constexpr (Src<kSrc>::cgrid) return nearest_cgrid<kCount>(sc, v, r, w);
     else if constexpr (Src<kSrc>::q4) return nearest_q4<kCount, kSrc == kSrcQ4>(sc, v, r, w);
     // two stack entries in registers when the tree is read through L2 below its LDS prefix
-    // (C4 74.0 -> 71.4 ms); none when the whole tree is in LDS (C3 3.66 -> 3.80 ms with 1-4)
+    // (C4 74.0 -> 71.4 ms); RT_COMPACT_REG on the compact stack with the whole tree in LDS (the
+    // 64-bit stack: 3.66 -> 3.80 ms with 1-4 in round 2)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2)
         return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact_bits ? RT_COMPACT_REG : 0, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2, Src<kSrc>::compact_bits>(sc, v, r, w);

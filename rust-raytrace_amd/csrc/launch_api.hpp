@@ -79,8 +79,6 @@ struct WfStreams {
     int tail_width;       //   chains per wave, 0 auto), which folds them; the others fold on b[0]
     bool tail_nowait;     // the tail does not wait for the b streams: wf_tail_fold on b[0] after them, and
                           //   per tail wave the second of the two folds its chains (WfBufs::tflag)
-    int fold_early;       // > 0 (no fused tail): the chains that ended by generation fold_early - 1 fold on
-                          //   that generation's b stream; the frame-end fold takes the others
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneTailNowait, kTuneFoldEarly, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneTailNowait, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -96,8 +96,6 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // without waiting for the B streams; each tail wave and
                                                  // wf_tail_fold (on b[0] after the B streams) meet on a counter and
                                                  // the second folds that wave's chains
-    {"fold_early", 0, 0, 33},                    // K > 0 (no fused tail): the chains that ended by generation K-1
-                                                 // fold on a B stream during the later generations
 };
 
 }  // namespace
@@ -1301,7 +1299,6 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>({G, static_cast<uint32_t>(c->n_cu),
                                                                    static_cast<uint32_t>(kMaxTailWaves / (kWfThreads / 64))}));
                 ws.tail_nowait = c->t(kTuneTailNowait) != 0 && ws.nb > 0 && ws.b[0] != ws.a;
-                ws.fold_early = static_cast<int>(c->t(kTuneFoldEarly));
             }
             ws.ma = timed ? &marks : nullptr;
             ws.cam = cam;

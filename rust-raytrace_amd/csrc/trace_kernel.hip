@@ -1480,22 +1480,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
             e = hipEventRecord(mark, ws.a);
             if (e != hipSuccess) return e;
         }
-        // early fold (WfStreams::fold_early = K): once generation K-1's shading is queued, the chains
-        // that ended by K-1 fold on its B stream (after the other B streams' shading), overlapped
-        // with the latency-bound late generations; the frame-end fold takes the rest
-        if (ws.fold_early > 0 && ws.tail_fuse == 0 && k == ws.fold_early - 1 && static_cast<uint32_t>(k) <= fp.max_depth &&
-            ws.nb > 0 && ws.b[0] != ws.a) {
-            const int fi = k % ws.nb;
-            for (int i = 0; i < ws.nb; ++i) {
-                if (i == fi) continue;
-                if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(ws.b[fi], ws.b_done[i], 0)) != hipSuccess) return e;
-            }
-            if ((e = launch_fold(sc, fp, b, ws.b[fi], ws.mb[fi], 0u, static_cast<uint32_t>(k))) != hipSuccess) return e;
-        }
     }
-    const bool early = ws.fold_early > 0 && ws.tail_fuse == 0 && static_cast<uint32_t>(ws.fold_early - 1) <= fp.max_depth &&
-                       ws.nb > 0 && ws.b[0] != ws.a;
     hipError_t e;
     // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
     if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
@@ -1508,9 +1493,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     // the chains not folded yet (all of them without the fused tail, which folded every chain:
     // its own as it ended them, the others on a B stream)
-    if (ws.tail_fuse == 0 &&
-        (e = launch_fold(sc, fp, b, ws.a, ws.ma, early ? static_cast<uint32_t>(ws.fold_early) : 0u, kNlevRunning - 1u)) != hipSuccess)
-        return e;
+    if (ws.tail_fuse == 0 && (e = launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess) return e;
     if (b.compose) {                         // the frame, row by row, once every chain has its colour
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
         const uint64_t segs = static_cast<uint64_t>((fp.tile_w + 63u) / 64u) * fp.rows;

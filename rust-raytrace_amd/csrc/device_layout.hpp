@@ -261,10 +261,7 @@ struct PathStack {
 //            kPixAmbient | object for a camera ray that ended without a chain;
 //   ccol     (compose) per chain [capa]: final colour f32 r,g,b and the sRGB
 //            bytes b | g << 8 | r << 16 (16 B), written by the fold in chain
-//            order and read by wf_compose, which writes the frame row by row;
-//   tflag    (fused tail without the wait) per tail wave [kMaxTailWaves]: the
-//            fold handshake between that wave and wf_tail_fold (0 between
-//            frames: the second party resets it).
+//            order and read by wf_compose, which writes the frame row by row.
 // Queue and record arrays are G regions of R entries (qcap = G*R); region r is
 // written only by workgroup r of the producing kernel.
 struct WfBufs {
@@ -273,7 +270,7 @@ struct WfBufs {
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
     uint64_t qcap;                  // G * R
-    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix, o_pmap, o_ccol, o_tflag;   // byte offsets of the sections
+    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix, o_pmap, o_ccol;   // byte offsets of the sections
     uint32_t cap;                   // pixel capacity
     uint32_t capa;                  // qcap rounded up to 64: stride of the per-chain arrays (levels,
                                     // terminals; chain c = generation 0's record entry c)
@@ -309,7 +306,6 @@ struct WfBufs {
     RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
     RT_HD uint32_t* pmap() const { return reinterpret_cast<uint32_t*>(mem + o_pmap); }   // chunk pixel -> chain / code
     RT_HD uint32_t* ccol() const { return reinterpret_cast<uint32_t*>(mem + o_ccol); }   // chain c -> final colour [4c, 4c+4)
-    RT_HD uint32_t* tflag() const { return reinterpret_cast<uint32_t*>(mem + o_tflag); }
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
 };
@@ -318,8 +314,6 @@ constexpr uint32_t kPixBackground = 0xFFFFFFFFu;   // WfBufs::pmap: the camera r
 constexpr uint32_t kPixAmbient = 0x80000000u;      // ... | object: it ended on that object's ambient colour
 
 constexpr int kWfThreads = 1024;      // workgroup size of the queue kernels
-constexpr int kMaxTailWaves = 4096;   // WfBufs::tflag entries: wf_tail's workgroups (<= 256) x 16 waves
-constexpr uint32_t kNlevTail = 64u;   // WfBufs::nlev of a tail chain awaiting its fold: 64 + its level count
 constexpr int kMaxRegions = 2048;     // upper bound of WfBufs::G
 constexpr int kMaxScan = 4096;        // region sizes one region_scan covers (several generations' regions)
 constexpr int kMaxGenerations = 34;   // RT_MAX_DEPTH_LIMIT + 2 generations, + 1 spare for the last producer

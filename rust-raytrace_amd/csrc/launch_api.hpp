@@ -77,8 +77,6 @@ struct WfStreams {
     int tail_fuse;        // > 0: the chains running at generation tail_fuse - 1 finish in one wf_tail
     int tail_wgs;         //   launch on stream a (that many workgroups, all resident: one per CU;
     int tail_width;       //   chains per wave, 0 auto), which folds them; the others fold on b[0]
-    bool tail_nowait;     // the tail does not wait for the b streams: wf_tail_fold on b[0] after them, and
-                          //   per tail wave the second of the two folds its chains (WfBufs::tflag)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneTailNowait, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,10 +92,6 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
                                                  // (0: equal chunks)
-    {"tail_nowait", 0, 0, 1},                    // 1: the fused tail starts right after the last nearest-hit launch,
-                                                 // without waiting for the B streams; each tail wave and
-                                                 // wf_tail_fold (on b[0] after the B streams) meet on a counter and
-                                                 // the second folds that wave's chains
 };
 
 }  // namespace
@@ -243,7 +239,6 @@ struct rt_ctx {
         std::vector<hipEvent_t> near_done; // per generation: nearest-hit kernel finished (s -> sb)
         void* mem = nullptr;
         size_t bytes = 0;
-        uint64_t tflag_at = UINT64_MAX;        // WfBufs::o_tflag the handshake words were zeroed at
         WfBufs b{};
     };
     std::vector<Lane> lanes;
@@ -434,7 +429,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     const uint64_t s_cpix = q * 4;
     const uint64_t s_pmap = static_cast<uint64_t>(cap) * 4;
     const uint64_t s_ccol = capa * 16;
-    const uint64_t s_tflag = static_cast<uint64_t>(kMaxTailWaves) * 4;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
     b.o_lev = off; off = align_up(off + s_lev, 256);
@@ -444,7 +438,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_cpix = off; off = align_up(off + s_cpix, 256);
     b.o_pmap = off; off = align_up(off + s_pmap, 256);
     b.o_ccol = off; off = align_up(off + s_ccol, 256);
-    b.o_tflag = off; off = align_up(off + s_tflag, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -481,11 +474,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
         }
         if (e != hipSuccess) return hip_fail(c, e, "hipMalloc(wavefront working set)");
         L.bytes = off;
-        L.tflag_at = UINT64_MAX;
-    }
-    if (b.o_tflag != L.tflag_at) {           // the tail's fold handshake words start at 0 (each frame's
-        HIP_TRY(c, hipMemsetAsync(static_cast<unsigned char*>(L.mem) + b.o_tflag, 0, s_tflag, L.s));   // second
-        L.tflag_at = b.o_tflag;              // party resets its word)
     }
     b.mem = static_cast<unsigned char*>(L.mem);
     b.totals = c->d_counters + kTotals;
@@ -1296,9 +1284,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                                 c->t(kTuneGridOcc) != 0;
                 ws.tail_fuse = ok ? T : 0;
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
-                ws.tail_wgs = static_cast<int>(std::min<uint32_t>({G, static_cast<uint32_t>(c->n_cu),
-                                                                   static_cast<uint32_t>(kMaxTailWaves / (kWfThreads / 64))}));
-                ws.tail_nowait = c->t(kTuneTailNowait) != 0 && ws.nb > 0 && ws.b[0] != ws.a;
+                ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;
             ws.cam = cam;

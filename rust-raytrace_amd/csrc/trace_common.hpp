@@ -347,10 +347,7 @@ __device__ __forceinline__ float t_limit(double t) {
     return f + kBoxTol * f;
 }
 // ... in the scaled t of the ray's slab tests (t 2^te, exact; te = 0 for unit-length rays)
-#ifndef RT_DIAG_TL
-#define RT_DIAG_TL 1
-#endif
-__device__ __forceinline__ float t_limit(const RayBox& rb, double t) { return t_limit(RT_DIAG_TL ? ldexp(t, rb.te) : t); }
+__device__ __forceinline__ float t_limit(const RayBox& rb, double t) { return t_limit(ldexp(t, rb.te)); }
 
 // Planes of the scene (always brute force: few, and they carry the NaN quirk).
 __device__ __forceinline__ Hit nearest_planes(const DevScene& sc, const Ray& r) {

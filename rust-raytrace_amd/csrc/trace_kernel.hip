@@ -1055,49 +1055,8 @@ __device__ __forceinline__ Col fold_pixel(const DevScene& sc, const WfBufs& b, u
 // record loads and level stores stay coalesced.  gridDim.x workgroups, all
 // resident; workgroup w publishes its counts in region w and zeros in the
 // other regions r = w (mod gridDim.x) of every generation >= T.
-// Chains per wave of the fused tail (tuning tail_width; auto: about half of the waves get chains).
-__device__ __forceinline__ uint32_t tail_run(int W, uint32_t n, uint32_t nw) {
-    return W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * n + nw - 1) / nw));
-}
-
-// Fold the chains of tail wave `slot` (WfStreams::tail_nowait): their terminals
-// and level counts (kNlevTail + count) as the tail stored them, the levels of
-// every generation (the B streams' and the tail's).  Called by whichever of the
-// tail wave and wf_tail_fold comes second to the wave's handshake word, after
-// an agent-scope acquire, so both sides' stores are visible.
-template <bool kFresnel>
-__device__ __forceinline__ void fold_tail_wave(const DevScene& sc, const FrameParams& fp, const WfBufs& b, const uint32_t* scan,
-                                               int T, uint32_t slot, uint32_t cw, uint32_t n, uint32_t nw, const double* srgb) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const size_t rk = static_cast<size_t>(T - 1) * b.qcap;
-    for (uint64_t base = static_cast<uint64_t>(slot) * cw; base < n; base += static_cast<uint64_t>(nw) * cw) {
-        const uint64_t j = base + lane;
-        if (lane >= cw || j >= n) continue;
-        const size_t at = rk + region_entry(scan, b.G, b.R, static_cast<uint32_t>(j));
-        const uint32_t c = b.ru(2)[at];
-        const int nlev = static_cast<int>(b.nlev()[c]) - static_cast<int>(kNlevTail);
-        const Col term{b.term(0)[c], b.term(1)[c], b.term(2)[c]};
-        const Col res = average_samples(fold_levels<kFresnel>(sc, b, c, nlev, term), fp.spp);
-        emit_chain(fp, b, c, b.compose ? 0u : b.cpix()[c], res, srgb);
-    }
-}
-
-// The handshake of tail wave `slot` (whole wave, converged): true for the second
-// of the two parties, which then owns the fold and resets the word.
-__device__ __forceinline__ bool tail_handshake(const WfBufs& b, uint32_t slot) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");             // this wave's stores before the count
-    uint32_t old = 0;
-    if ((threadIdx.x & 63u) == 0)
-        old = __hip_atomic_fetch_add(&b.tflag()[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, 0, 64);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");             // the other party's stores after it
-    if (old == 0) return false;
-    if ((threadIdx.x & 63u) == 0) __hip_atomic_store(&b.tflag()[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-}
-
 template <bool kFresnel, bool kCount>
-__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int W, int nowait) {
+__global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParams fp, WfBufs b, int T, int W) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint32_t s_cnt[2][kMaxGenerations];
     __shared__ double s_srgb[255];
@@ -1109,7 +1068,7 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
     const int gens = static_cast<int>(fp.max_depth) + 2;
     const uint32_t nw = gridDim.x * (kWfThreads / 64);
     const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    const uint32_t cw = tail_run(W, n, nw);
+    const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * n + nw - 1) / nw));
     Work wn, wsh;
     const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
     __syncthreads();
@@ -1121,15 +1080,9 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
         const ShadeIn in = shade_load(b, at, false);
         int nlev = 0;
         const Col term = tail_chain<kFresnel, kCount>(sc, fp, b, v, T - 1, in, nlev, s_cnt, wn, wsh);
-        if (nowait) {                       // the levels <= T-2 may not be written yet: fold later
-            set_terminal(b, in.c, term, static_cast<int>(kNlevTail) + nlev);
-            continue;
-        }
         const Col res = average_samples(fold_levels<kFresnel>(sc, b, in.c, nlev, term), fp.spp);
         emit_chain(fp, b, in.c, b.compose ? 0u : b.cpix()[in.c], res, s_srgb);
     }
-    if (nowait && static_cast<uint64_t>(slot) * cw < n && tail_handshake(b, slot))   // wave-uniform
-        fold_tail_wave<kFresnel>(sc, fp, b, ql.scan, T, slot, cw, n, nw, s_srgb);
     __syncthreads();
     for (uint32_t rg = blockIdx.x; rg < b.G; rg += gridDim.x) {
         const bool own = rg == blockIdx.x;
@@ -1140,25 +1093,6 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
     }
     flush_work<kCount>(b, 2, wn);
     flush_work<kCount>(b, 4, wsh);
-}
-
-// The other party of the tail's handshakes (WfStreams::tail_nowait): launched on
-// b[0] once every B stream's shading is done (the levels of generations <= T-2
-// are written), with the tail's grid and run width, so wave `slot` here meets
-// tail wave `slot`: the second of the two folds that wave's chains.
-template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads) void wf_tail_fold(DevScene sc, FrameParams fp, WfBufs b, int T, int W) {
-    __shared__ uint32_t s_scan[kMaxRegions + 1];
-    __shared__ uint32_t s_wave[kWfThreads / 64];
-    __shared__ double s_srgb[255];
-    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
-    region_scan(b.rs() + (T - 1) * b.G, b.G, s_scan, s_wave);
-    const uint32_t n = s_scan[b.G];
-    const uint32_t nw = gridDim.x * (kWfThreads / 64);
-    const uint32_t slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    const uint32_t cw = tail_run(W, n, nw);
-    if (static_cast<uint64_t>(slot) * cw < n && tail_handshake(b, slot))          // wave-uniform
-        fold_tail_wave<kFresnel>(sc, fp, b, s_scan, T, slot, cw, n, nw, s_srgb);
 }
 
 // One chain per work-item: the chains of the chunk are generation 0's shade
@@ -1383,12 +1317,10 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (ws.tail_fuse > 0 && k >= ws.tail_fuse) {      // the fused tail: every generation >= T in one launch
         if (k > ws.tail_fuse) return hipSuccess;
         // the tail folds its chains: the levels of generations <= T-2 (the B streams) must be written
-        // (tail_nowait: b[0] waits for the other B streams instead, and folds after them what the
-        // tail could not)
         for (int i = 0; i < ws.nb; ++i) {
-            if (ws.b[i] == ws.a || (ws.tail_nowait && i == 0)) continue;
+            if (ws.b[i] == ws.a) continue;
             if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(ws.tail_nowait ? ws.b[0] : ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
         }
         // the chains that ended by generation T-1, folded on a B stream while the tail runs
         if (ws.b[0] != ws.a) {
@@ -1400,19 +1332,9 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
             return e;
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
         const size_t lds_t = staged_bytes<kSrcBvhL8C>(sc) + queue_lds_bytes(b.G);
-        const int nw = ws.tail_nowait ? 1 : 0;
-        if (sc.has_fresnel)
-            hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, nw);
-        else
-            hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width, nw);
-        if (ws.ma && (e = ws.ma->mark(ws.a, kKfTail)) != hipSuccess) return e;
-        if (ws.tail_nowait) {             // after the early chains' fold on b[0]
-            if (ws.mb[0] && (e = ws.mb[0]->begin(ws.b[0])) != hipSuccess) return e;
-            if (sc.has_fresnel) hipLaunchKernelGGL(wf_tail_fold<true>, dim3(ws.tail_wgs), block, 0, ws.b[0], sc, fp, b, k, ws.tail_width);
-            else hipLaunchKernelGGL(wf_tail_fold<false>, dim3(ws.tail_wgs), block, 0, ws.b[0], sc, fp, b, k, ws.tail_width);
-            if (ws.mb[0] && (e = ws.mb[0]->mark(ws.b[0], kKfFold)) != hipSuccess) return e;
-        }
-        return hipGetLastError();
+        if (sc.has_fresnel) hipLaunchKernelGGL((wf_tail<true, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width);
+        else hipLaunchKernelGGL((wf_tail<false, kCount>), dim3(ws.tail_wgs), block, lds_t, ws.a, sc, fp, b, k, ws.tail_width);
+        return ws.ma ? ws.ma->mark(ws.a, kKfTail) : hipGetLastError();
     }
     e = ws.ma ? ws.ma->begin(ws.a) : hipSuccess;
     if (e != hipSuccess) return e;

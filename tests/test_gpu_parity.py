@@ -327,9 +327,7 @@ def test_axis_aligned_rays_and_ties_across_leaves(gpu_ctx, algo):
 
 @pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan", "fresnel"])
 def test_fused_tail_matches_oracle(gpu_ctx, scene):
-    """The fused tail (tuning tail_fuse = T, trace_kernel.hip wf_tail), waiting for
-    the B streams or not (tail_nowait: each tail wave and wf_tail_fold meet on a
-    counter, the second folds the wave's chains): every
+    """The fused tail (tuning tail_fuse = T, trace_kernel.hip wf_tail): every
     chain still running at generation T-1 goes from its shade record through
     all its remaining bounces -- light-view grid shadows, Phong sum,
     reflection, nearest hit -- in one launch, one chain per work-item, and
@@ -352,8 +350,8 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
     # (the tail answers shadows through light-view grids only: directional lights become point lights far away)
     s.lights = [l if l["kind"] == "point" else
                 {"kind": "point", "location": tuple(-40.0 * x for x in l["direction"]), "color": l["color"]} for l in s.lights]
-    for T, nowait in [(1, 0), (2, 0), (3, 0), (4, 0), (1, 1), (2, 1), (3, 1), (4, 1)]:
-        with _with_tuning(gpu_ctx, tail_fuse=T, tail_nowait=nowait):
+    for T in (1, 2, 3, 4):
+        with _with_tuning(gpu_ctx, tail_fuse=T):
             check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
             gpu_ctx.kernel_times()
             gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
@@ -362,8 +360,7 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
         if T <= s.max_depth + 1:
             assert kt["nearest"][1] == T - 1 and kt["tail"][1] == 1, (T, kt)     # generations 1 .. T-1, the tail
             assert kt["occlusion"][1] == T - 1 and kt["shade"][1] == T - 1, (T, kt)   # generations 0 .. T-2
-            # the chains that ended by T-1; with tail_nowait also wf_tail_fold, the tail's handshake partner
-            assert kt["fold"][1] == 1 + nowait, (T, kt)
+            assert kt["fold"][1] == 1, (T, kt)     # the chains that ended by T-1
 
 
 @pytest.mark.parametrize("scene", ["axis_ties", "config3", "dense", "planes_nan", "config4", "camera_inside"])
@@ -699,8 +696,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
                dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
-               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(tail_fuse=2, tail_nowait=1),
-               dict(tail_fuse=4, tail_nowait=1, compose=1), dict(tail_fuse=5, tail_nowait=1, tail_width=7)]:
+               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

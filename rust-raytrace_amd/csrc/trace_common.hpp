@@ -316,7 +316,16 @@ __device__ __forceinline__ RayBox make_raybox(const Ray& r) {
 // Slab bound t at coordinate v along the axis with (1/d, -o/d) = (i, no).
 __device__ __forceinline__ float slab_t(float v, float i, float no) { return __builtin_fmaf(v, i, no); }
 
-// Interval widening by the relative kBoxTol (one FMA with an |x| modifier).
+// Interval widening by the relative kBoxTol (one FMA with an |x| modifier), or as
+// one multiply by these factors where the sign cases do not matter (RT_WIDEN_MUL).
+#ifndef RT_WIDEN_MUL
+#define RT_WIDEN_MUL 1
+#endif
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0       // packed slab FMAs in the LDS walk (A/B builds)
+#endif
+constexpr float kWidenLo = 1.0f - kBoxTol;
+constexpr float kWidenHi = 1.0f + kBoxTol;
 __device__ __forceinline__ float widen_lo(float t) { return __builtin_fmaf(-kBoxTol, fabsf(t), t); }
 __device__ __forceinline__ float widen_hi(float t) { return __builtin_fmaf(kBoxTol, fabsf(t), t); }
 
@@ -649,10 +658,32 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             if constexpr (kNodes == 2) {
                 const float2 nx = nxa[cur], fx = fxa[cur], ny = nya[cur], fy = fya[cur], nz = nza[cur], fz = fza[cur];
                 const int2 cc = ca[cur];
-                t0 = widen_lo(fmaxf(fmaxf(slab_t(nx.x, rb.ix, rb.nox), slab_t(ny.x, rb.iy, rb.noy)), slab_t(nz.x, rb.iz, rb.noz)));
-                t1 = widen_lo(fmaxf(fmaxf(slab_t(nx.y, rb.ix, rb.nox), slab_t(ny.y, rb.iy, rb.noy)), slab_t(nz.y, rb.iz, rb.noz)));
-                const float f0 = widen_hi(fminf(fminf(slab_t(fx.x, rb.ix, rb.nox), slab_t(fy.x, rb.iy, rb.noy)), slab_t(fz.x, rb.iz, rb.noz)));
-                const float f1 = widen_hi(fminf(fminf(slab_t(fx.y, rb.ix, rb.nox), slab_t(fy.y, rb.iy, rb.noy)), slab_t(fz.y, rb.iz, rb.noz)));
+#if RT_PK_SLAB
+                // both children's slab bounds of an axis in one packed FMA (v_pk_fma_f32)
+                typedef float F2 __attribute__((ext_vector_type(2)));
+                auto pk = [](float2 v, float i, float no) {
+                    return __builtin_elementwise_fma(F2{v.x, v.y}, F2{i, i}, F2{no, no});
+                };
+                const F2 snx = pk(nx, rb.ix, rb.nox), sny = pk(ny, rb.iy, rb.noy), snz = pk(nz, rb.iz, rb.noz);
+                const F2 sfx = pk(fx, rb.ix, rb.nox), sfy = pk(fy, rb.iy, rb.noy), sfz = pk(fz, rb.iz, rb.noz);
+                const float a0 = fmaxf(fmaxf(snx.x, sny.x), snz.x), a1 = fmaxf(fmaxf(snx.y, sny.y), snz.y);
+                const float b0 = fminf(fminf(sfx.x, sfy.x), sfz.x), b1 = fminf(fminf(sfx.y, sfy.y), sfz.y);
+#else
+                const float a0 = fmaxf(fmaxf(slab_t(nx.x, rb.ix, rb.nox), slab_t(ny.x, rb.iy, rb.noy)), slab_t(nz.x, rb.iz, rb.noz));
+                const float a1 = fmaxf(fmaxf(slab_t(nx.y, rb.ix, rb.nox), slab_t(ny.y, rb.iy, rb.noy)), slab_t(nz.y, rb.iz, rb.noz));
+                const float b0 = fminf(fminf(slab_t(fx.x, rb.ix, rb.nox), slab_t(fy.x, rb.iy, rb.noy)), slab_t(fz.x, rb.iz, rb.noz));
+                const float b1 = fminf(fminf(slab_t(fx.y, rb.ix, rb.nox), slab_t(fy.y, rb.iy, rb.noy)), slab_t(fz.y, rb.iz, rb.noz));
+#endif
+#if RT_WIDEN_MUL
+                // the relative widening as one multiply per bound (§4 item 2): t (1 - tol) for the
+                // entry, f (1 + tol) for the exit.  Where the two forms differ (t or f < 0) the
+                // compare below clamps t to 0 and a negative exit fails either way; +inf stays +inf
+                t0 = a0 * kWidenLo; t1 = a1 * kWidenLo;
+                const float f0 = b0 * kWidenHi, f1 = b1 * kWidenHi;
+#else
+                t0 = widen_lo(a0); t1 = widen_lo(a1);
+                const float f0 = widen_hi(b0), f1 = widen_hi(b1);
+#endif
                 h0 = fmaxf(t0, 0.0f) <= fminf(f0, tlim);           // box_hit's folded test
                 h1 = fmaxf(t1, 0.0f) <= fminf(f1, tlim);
                 c0 = cc.x;

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneFoldEarly, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneFoldEarly, kTuneFoldEarlyWgs, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -95,6 +95,7 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"fold_early", 0, 0, 33},                    // K > 0 (no fused tail): the chains that ended by generation K-1
                                                  // fold on a B stream during the later generations, the frame-end
                                                  // fold only the chains of Q_K (listed by generation K-1)
+    {"fold_early_wgs", 0, 0, 2048},              // the early fold's workgroups (0: the regions G)
 };
 
 }  // namespace
@@ -1291,6 +1292,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
                 ws.fold_early = static_cast<int>(c->t(kTuneFoldEarly));
+                ws.fold_early_wgs = static_cast<int>(c->t(kTuneFoldEarlyWgs));
             }
             ws.ma = timed ? &marks : nullptr;
             ws.cam = cam;

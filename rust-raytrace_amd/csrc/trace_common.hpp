@@ -321,9 +321,6 @@ __device__ __forceinline__ float slab_t(float v, float i, float no) { return __b
 #ifndef RT_WIDEN_MUL
 #define RT_WIDEN_MUL 1
 #endif
-#ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0       // packed slab FMAs in the LDS walk (A/B builds)
-#endif
 constexpr float kWidenLo = 1.0f - kBoxTol;
 constexpr float kWidenHi = 1.0f + kBoxTol;
 __device__ __forceinline__ float widen_lo(float t) { return __builtin_fmaf(-kBoxTol, fabsf(t), t); }
@@ -658,22 +655,10 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             if constexpr (kNodes == 2) {
                 const float2 nx = nxa[cur], fx = fxa[cur], ny = nya[cur], fy = fya[cur], nz = nza[cur], fz = fza[cur];
                 const int2 cc = ca[cur];
-#if RT_PK_SLAB
-                // both children's slab bounds of an axis in one packed FMA (v_pk_fma_f32)
-                typedef float F2 __attribute__((ext_vector_type(2)));
-                auto pk = [](float2 v, float i, float no) {
-                    return __builtin_elementwise_fma(F2{v.x, v.y}, F2{i, i}, F2{no, no});
-                };
-                const F2 snx = pk(nx, rb.ix, rb.nox), sny = pk(ny, rb.iy, rb.noy), snz = pk(nz, rb.iz, rb.noz);
-                const F2 sfx = pk(fx, rb.ix, rb.nox), sfy = pk(fy, rb.iy, rb.noy), sfz = pk(fz, rb.iz, rb.noz);
-                const float a0 = fmaxf(fmaxf(snx.x, sny.x), snz.x), a1 = fmaxf(fmaxf(snx.y, sny.y), snz.y);
-                const float b0 = fminf(fminf(sfx.x, sfy.x), sfz.x), b1 = fminf(fminf(sfx.y, sfy.y), sfz.y);
-#else
                 const float a0 = fmaxf(fmaxf(slab_t(nx.x, rb.ix, rb.nox), slab_t(ny.x, rb.iy, rb.noy)), slab_t(nz.x, rb.iz, rb.noz));
                 const float a1 = fmaxf(fmaxf(slab_t(nx.y, rb.ix, rb.nox), slab_t(ny.y, rb.iy, rb.noy)), slab_t(nz.y, rb.iz, rb.noz));
                 const float b0 = fminf(fminf(slab_t(fx.x, rb.ix, rb.nox), slab_t(fy.x, rb.iy, rb.noy)), slab_t(fz.x, rb.iz, rb.noz));
                 const float b1 = fminf(fminf(slab_t(fx.y, rb.ix, rb.nox), slab_t(fy.y, rb.iy, rb.noy)), slab_t(fz.y, rb.iz, rb.noz));
-#endif
 #if RT_WIDEN_MUL
                 // the relative widening as one multiply per bound (§4 item 2): t (1 - tol) for the
                 // entry, f (1 + tol) for the exit.  Where the two forms differ (t or f < 0) the

@@ -1154,11 +1154,12 @@ __global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc
 }
 
 hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& b, hipStream_t s, LaunchMarks* m,
-                       uint32_t lo, uint32_t hi, int list = 0) {
+                       uint32_t lo, uint32_t hi, int list = 0, uint32_t wgs = 0) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
-    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
+    const dim3 grid(wgs > 0 ? std::min(wgs, b.G) : b.G);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
+    else hipLaunchKernelGGL((wf_fold<false>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 
@@ -1424,7 +1425,9 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
                 if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
                 if ((e = hipStreamWaitEvent(ws.b[fi], ws.b_done[i], 0)) != hipSuccess) return e;
             }
-            if ((e = launch_fold(sc, fp, b, ws.b[fi], ws.mb[fi], 0u, static_cast<uint32_t>(k))) != hipSuccess) return e;
+            if ((e = launch_fold(sc, fp, b, ws.b[fi], ws.mb[fi], 0u, static_cast<uint32_t>(k), 0,
+                                 static_cast<uint32_t>(ws.fold_early_wgs))) != hipSuccess)
+                return e;
         }
     }
     hipError_t e;

@@ -824,8 +824,9 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     c->deep_bvh4 = bvh4_stack_need(bvh4) > 64;
     // compact stack (trace_common.hpp kShortStack, stk_entry16): the stack never holds more
     // entries than the deepest inner node's depth; node indices and leaf codes
-    // (first << 3 | count - 1) must fit a signed 16-bit field
-    c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 32768 && spheres.size() <= 4096;
+    // (first << 3 | count - 1) must fit a signed 16-bit field; the whole-LDS walk stores inner
+    // nodes as byte offsets (c + 1) * 8 (trace_common.hpp node_byte_off)
+    c->short_stack = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 4095 && spheres.size() <= 4096;
     c->short_stack18 = bvh_depth(bvh) <= 32 && bvh.nodes.size() < 131072 && spheres.size() <= 16383;
     // binary16 nodes only for trees that do not fit LDS whole (the prefix source reads them)
     const bool big_tree = bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget;

@@ -415,7 +415,13 @@ __device__ __forceinline__ BvhView global_view(const DevScene& sc) {
 // wave spreads over all 32 8-B bank slots (the pair arrays have an 8-B stride).
 __host__ __device__ constexpr size_t node_planes_bytes(int32_t n) { return (static_cast<size_t>(n) * 56u + 15u) / 16u * 16u; }
 
-template <int kThreads>
+// kByteOff (nearest_bvh_bl's walk): an inner child c is stored as the byte
+// offset (c + 1) * 8 of its pairs, so a visit addresses every array with one add
+// and no shift, and 0 (an inline constant) is free to mean "no node"; leaf codes
+// (negative) are unchanged.
+__host__ __device__ constexpr int32_t node_byte_off(int32_t c) { return c >= 0 ? (c + 1) * 8 : c; }
+
+template <int kThreads, bool kByteOff = false>
 __device__ __forceinline__ const float2* stage_node_planes(const DevBvhNode* src, int32_t n, unsigned char* lds) {
     float2* L = reinterpret_cast<float2*>(lds);
     int2* C = reinterpret_cast<int2*>(L + 6 * n);
@@ -426,7 +432,7 @@ __device__ __forceinline__ const float2* stage_node_planes(const DevBvhNode* src
             L[(2 * a) * n + i] = make_float2(nd.lo0[a], nd.lo1[a]);
             L[(2 * a + 1) * n + i] = make_float2(nd.hi0[a], nd.hi1[a]);
         }
-        C[i] = make_int2(nd.c0, nd.c1);
+        C[i] = kByteOff ? make_int2(node_byte_off(nd.c0), node_byte_off(nd.c1)) : make_int2(nd.c0, nd.c1);
     }
     return L;
 }
@@ -611,7 +617,9 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     const SphK sk = sphere_k(a);
     const RayBox rb = make_raybox(r);
     float tlim = h.obj == INT32_MAX ? __builtin_inff() : t_limit(rb, h.t);
-    constexpr int32_t kNone = INT32_MIN;          // not a node, and no leaf code (~cur would list 8 spheres at 2^28)
+    // not a node and no leaf code: INT32_MIN (~cur would list 8 spheres at 2^28), or 0 for the
+    // byte-offset nodes of the whole-LDS walk (node c is (c + 1) * 8)
+    constexpr int32_t kNone = kNodes == 2 ? 0 : INT32_MIN;
     // kReg newest entries in registers (the LDS-prefix source), the rest in scratch;
     // kCompactBits > 0: 32-bit entries with that many code bits, kShortStack of them
     // (128 B of scratch per lane); 0: 64-bit (node, t) entries
@@ -628,33 +636,35 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     auto e_t = [](StkE e) -> float {
         if constexpr (kCompact) return stk_t_c<kCompactBits>(e); else return stk_t(e);
     };
-    int32_t cur = sc.bvh_root;
+    // whole tree in LDS (kNodes 2): nodes as byte offsets (stage_node_planes<., true>), 0 = none
+    int32_t cur = kNodes == 2 ? node_byte_off(sc.bvh_root) : sc.bvh_root;
     [[maybe_unused]] unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     // whole tree in LDS: per axis the array of NEAR bound pairs (lo when 1/d >= 0,
     // else hi) and of FAR pairs.  fma(v, 1/d, -o/d) is monotone in v for a fixed
     // ray (1/d != 0), so fma(near) = min(fma(lo), fma(hi)) exactly: box_hit's
-    // interval, without its six min/max per child.
-    [[maybe_unused]] const float2 *nxa = nullptr, *fxa = nullptr, *nya = nullptr, *fya = nullptr, *nza = nullptr,
-                                  *fza = nullptr;
-    [[maybe_unused]] const int2* ca = nullptr;
+    // interval, without its six min/max per child.  Byte bases one pair before
+    // node 0, so node byte offset (c + 1) * 8 addresses pair c.
+    [[maybe_unused]] const char *nxa = nullptr, *fxa = nullptr, *nya = nullptr, *fya = nullptr, *nza = nullptr,
+                                *fza = nullptr, *ca = nullptr;
     if constexpr (kNodes == 2) {
-        const float2* L = v.lnodes;
-        const int32_t n = v.nl;
-        nxa = L + (rb.ix >= 0.0f ? 0 : n); fxa = L + (rb.ix >= 0.0f ? n : 0);
-        nya = L + 2 * n + (rb.iy >= 0.0f ? 0 : n); fya = L + 2 * n + (rb.iy >= 0.0f ? n : 0);
-        nza = L + 4 * n + (rb.iz >= 0.0f ? 0 : n); fza = L + 4 * n + (rb.iz >= 0.0f ? n : 0);
-        ca = reinterpret_cast<const int2*>(L + 6 * n);
+        const char* L = reinterpret_cast<const char*>(v.lnodes) - 8;
+        const size_t n8 = static_cast<size_t>(v.nl) * 8;
+        nxa = L + (rb.ix >= 0.0f ? 0 : n8); fxa = L + (rb.ix >= 0.0f ? n8 : 0);
+        nya = L + 2 * n8 + (rb.iy >= 0.0f ? 0 : n8); fya = L + 2 * n8 + (rb.iy >= 0.0f ? n8 : 0);
+        nza = L + 4 * n8 + (rb.iz >= 0.0f ? 0 : n8); fza = L + 4 * n8 + (rb.iz >= 0.0f ? n8 : 0);
+        ca = L + 6 * n8;
     }
     for (;;) {
         RT_WSTAMP(q0);
-        while (cur >= 0) {
+        while (kNodes == 2 ? cur > 0 : cur >= 0) {
             RT_WSTEP(0);
             float t0, t1;
             bool h0, h1;
             int32_t c0, c1;
             if constexpr (kNodes == 2) {
-                const float2 nx = nxa[cur], fx = fxa[cur], ny = nya[cur], fy = fya[cur], nz = nza[cur], fz = fza[cur];
-                const int2 cc = ca[cur];
+                auto pair = [cur](const char* base) { return *reinterpret_cast<const float2*>(base + cur); };
+                const float2 nx = pair(nxa), fx = pair(fxa), ny = pair(nya), fy = pair(fya), nz = pair(nza), fz = pair(fza);
+                const int2 cc = *reinterpret_cast<const int2*>(ca + cur);
                 const float a0 = fmaxf(fmaxf(slab_t(nx.x, rb.ix, rb.nox), slab_t(ny.x, rb.iy, rb.noy)), slab_t(nz.x, rb.iz, rb.noz));
                 const float a1 = fmaxf(fmaxf(slab_t(nx.y, rb.ix, rb.nox), slab_t(ny.y, rb.iy, rb.noy)), slab_t(nz.y, rb.iz, rb.noz));
                 const float b0 = fminf(fminf(slab_t(fx.x, rb.ix, rb.nox), slab_t(fy.x, rb.iy, rb.noy)), slab_t(fz.x, rb.iz, rb.noz));
@@ -669,8 +679,12 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
                 t0 = widen_lo(a0); t1 = widen_lo(a1);
                 const float f0 = widen_hi(b0), f1 = widen_hi(b1);
 #endif
-                h0 = fmaxf(t0, 0.0f) <= fminf(f0, tlim);           // box_hit's folded test
-                h1 = fmaxf(t1, 0.0f) <= fminf(f1, tlim);
+                // box_hit's folded test max(t, 0) <= min(f, tlim) as two compares: tlim is never
+                // NaN, and !(x > f) holds for a NaN f as min(f, tlim) = tlim does (no
+                // canonicalisation of tlim per visit, no min)
+                const float x0 = fmaxf(t0, 0.0f), x1 = fmaxf(t1, 0.0f);
+                h0 = x0 <= tlim && !(x0 > f0);
+                h1 = x1 <= tlim && !(x1 > f1);
                 c0 = cc.x;
                 c1 = cc.y;
             } else {

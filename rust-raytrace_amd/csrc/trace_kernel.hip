@@ -396,7 +396,8 @@ __host__ __device__ inline size_t staged_bytes(const DevScene& sc) {
 
 // Stage what the source keeps in LDS (the whole tree and the spheres, or the
 // top of the tree); returns the view the queries use.
-template <int kSrc>
+// kNearest: the nearest-hit walk's byte-offset node encoding (stage_node_planes).
+template <int kSrc, bool kNearest = false>
 __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* lds) {
     constexpr int T = kWfThreads;
     BvhView v = global_view(sc);
@@ -443,7 +444,7 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
         v.p4 = lp;
         off = static_cast<size_t>(n) * sizeof(DevBvh4Plane);
     } else if constexpr (Src<kSrc>::nodes == 2) {
-        v.lnodes = stage_node_planes<T>(sc.bvh, sc.n_bvh, lds);
+        v.lnodes = stage_node_planes<T, kNearest>(sc.bvh, sc.n_bvh, lds);
         v.nl = sc.n_bvh;
         off = node_planes_bytes(sc.n_bvh);
     }
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_nearest(DevSc
         }
         return;
     }
-    const BvhView v = stage_lds<kSrc>(sc, lds);
+    const BvhView v = stage_lds<kSrc, true>(sc, lds);
     __syncthreads();                                       // publishes the LDS staging and counters
     RT_STAMP_AT(st1);
     acc[0] = st1 - st0;
@@ -1071,7 +1072,7 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
     const uint32_t lane = threadIdx.x & 63u, slot = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     const uint32_t cw = W > 0 ? static_cast<uint32_t>(W) : max(1u, min(64u, (2u * n + nw - 1) / nw));
     Work wn, wsh;
-    const BvhView v = stage_lds<kSrcBvhL8C>(sc, lds);
+    const BvhView v = stage_lds<kSrcBvhL8C, true>(sc, lds);
     __syncthreads();
     const size_t rk = static_cast<size_t>(T - 1) * b.qcap;
     for (uint64_t base = static_cast<uint64_t>(slot) * cw; base < n; base += static_cast<uint64_t>(nw) * cw) {

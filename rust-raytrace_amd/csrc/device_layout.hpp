@@ -261,9 +261,7 @@ struct PathStack {
 //            kPixAmbient | object for a camera ray that ended without a chain;
 //   ccol     (compose) per chain [capa]: final colour f32 r,g,b and the sRGB
 //            bytes b | g << 8 | r << 16 (16 B), written by the fold in chain
-//            order and read by wf_compose, which writes the frame row by row;
-//   flist    (early fold) the chain of every entry of Q_K, K = flist_gen, in the
-//            queue's region layout: the chains the frame-end fold still has.
+//            order and read by wf_compose, which writes the frame row by row.
 // Queue and record arrays are G regions of R entries (qcap = G*R); region r is
 // written only by workgroup r of the producing kernel.
 struct WfBufs {
@@ -272,7 +270,7 @@ struct WfBufs {
                                     // tests, [4..5] shadow box / sphere tests (accumulated over chunks)
     unsigned long long* gen_totals; // per-generation queue / shade-record totals over the chunks of a render
     uint64_t qcap;                  // G * R
-    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix, o_pmap, o_ccol, o_flist;   // byte offsets of the sections
+    uint64_t o_rec, o_lev, o_term, o_rq, o_rs, o_cpix, o_pmap, o_ccol;   // byte offsets of the sections
     uint32_t cap;                   // pixel capacity
     uint32_t capa;                  // qcap rounded up to 64: stride of the per-chain arrays (levels,
                                     // terminals; chain c = generation 0's record entry c)
@@ -284,8 +282,6 @@ struct WfBufs {
     uint32_t spread_below;          // queues below this many items are dealt workgroup-first regardless
     uint32_t wg_major;              // chunk dealing: 1 = consecutive chunks to the waves of one
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
-    uint32_t flist_gen;             // > 0: wf_nearest of generation flist_gen - 1 also lists the chains of
-                                    //   the rays it queues for flist_gen (the early fold's remainder)
     uint32_t compose;               // 1: final colours go through pmap / ccol and wf_compose writes the
                                     //   frame in row order; 0: the camera pass and the fold write pixels
 
@@ -310,7 +306,6 @@ struct WfBufs {
     RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
     RT_HD uint32_t* pmap() const { return reinterpret_cast<uint32_t*>(mem + o_pmap); }   // chunk pixel -> chain / code
     RT_HD uint32_t* ccol() const { return reinterpret_cast<uint32_t*>(mem + o_ccol); }   // chain c -> final colour [4c, 4c+4)
-    RT_HD uint32_t* flist() const { return reinterpret_cast<uint32_t*>(mem + o_flist); }
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
 };

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneFoldEarly, kTuneFoldEarlyWgs, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,10 +92,6 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
                                                  // (0: equal chunks)
-    {"fold_early", 0, 0, 33},                    // K > 0 (no fused tail): the chains that ended by generation K-1
-                                                 // fold on a B stream during the later generations, the frame-end
-                                                 // fold only the chains of Q_K (listed by generation K-1)
-    {"fold_early_wgs", 0, 0, 2048},              // the early fold's workgroups (0: the regions G)
 };
 
 }  // namespace
@@ -433,7 +429,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     const uint64_t s_cpix = q * 4;
     const uint64_t s_pmap = static_cast<uint64_t>(cap) * 4;
     const uint64_t s_ccol = capa * 16;
-    const uint64_t s_flist = q * 4;
     uint64_t off = align_up(s_queue, 256);
     b.o_rec = off; off = align_up(off + s_rec, 256);
     b.o_lev = off; off = align_up(off + s_lev, 256);
@@ -443,7 +438,6 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_cpix = off; off = align_up(off + s_cpix, 256);
     b.o_pmap = off; off = align_up(off + s_pmap, 256);
     b.o_ccol = off; off = align_up(off + s_ccol, 256);
-    b.o_flist = off; off = align_up(off + s_flist, 256);
     if (off > L.bytes) {
         if (L.mem) {
             (void)hipStreamSynchronize(L.s);
@@ -1292,8 +1286,6 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_fuse = ok ? T : 0;
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
-                ws.fold_early = static_cast<int>(c->t(kTuneFoldEarly));
-                ws.fold_early_wgs = static_cast<int>(c->t(kTuneFoldEarlyWgs));
             }
             ws.ma = timed ? &marks : nullptr;
             ws.cam = cam;

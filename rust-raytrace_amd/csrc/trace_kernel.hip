@@ -664,7 +664,6 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
         stn(&b.qf(qn, 3)[at], rr.dx); stn(&b.qf(qn, 4)[at], rr.dy); stn(&b.qf(qn, 5)[at], rr.dz);
         stn(&b.qf(qn, 6)[at], nsig);
         stn(&b.qpix(qn)[at], chain);
-        if (static_cast<uint32_t>(k + 1) == b.flist_gen) stn(&b.flist()[at], chain);   // the early fold's remainder
     }
 }
 
@@ -1111,17 +1110,13 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
 // Only chains of lo <= nlev <= hi: with the fused tail, the chains that ended
 // by generation T-1 fold on a B stream while the tail runs (every level and
 // terminal they need is written by then); the tail folds its own.
-// list: the chains are those of Q_lo's rays (WfBufs::flist, written by generation lo-1:
-// the chains the early fold left), not generation 0's records.
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi,
-                                                                     int list) {
+__global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
     __shared__ double s_srgb[255];
     __shared__ uint32_t s_scan[kMaxRegions + 1];
     __shared__ uint32_t s_wave[kWfThreads / 64];
     for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
-    // generation 0's records = the chains, or Q_lo's entries (also publishes s_srgb)
-    region_scan(list ? b.rq() + static_cast<size_t>(lo) * b.G : b.rs(), b.G, s_scan, s_wave);
+    region_scan(b.rs(), b.G, s_scan, s_wave);             // generation 0's records = the chains (also publishes s_srgb)
     const uint32_t n = s_scan[b.G];
     // software pipelined: the next chunk's chain header (level count, pixel, terminal) is
     // loaded before this chain's levels are folded, one dependent round trip less per chain
@@ -1134,7 +1129,6 @@ __global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc
         Head hd{0u, kNlevRunning, 0u, Col{0.0, 0.0, 0.0}};
         if (j < n) {
             hd.c = static_cast<uint32_t>(region_entry(s_scan, b.G, b.R, static_cast<uint32_t>(j)));
-            if (list) hd.c = b.flist()[hd.c];
             hd.nlev = b.nlev()[hd.c];
             hd.p = b.compose ? 0u : b.cpix()[hd.c];
             hd.term = Col{ldn_if<kNtFold>(&b.term(0)[hd.c]), ldn_if<kNtFold>(&b.term(1)[hd.c]),
@@ -1155,12 +1149,11 @@ __global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc
 }
 
 hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& b, hipStream_t s, LaunchMarks* m,
-                       uint32_t lo, uint32_t hi, int list = 0, uint32_t wgs = 0) {
+                       uint32_t lo, uint32_t hi) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    const dim3 grid(wgs > 0 ? std::min(wgs, b.G) : b.G);
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
-    else hipLaunchKernelGGL((wf_fold<false>), grid, dim3(kWfThreads), 0, s, sc, fp, b, lo, hi, list);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 
@@ -1383,18 +1376,9 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
 // waits for all of them.  Supported (src, src_occ) pairs: (0, 0), (1, 1),
 // (2, 2), (7, 7), (7, 10), (9, 10), (2, 11), (5, 11), (6, 11), (8, 11), (25, 11),
 // (26, 11); any other pair runs as (2, 11).
-hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b_in, int src, int src_occ,
+hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen) {
     const int gens = static_cast<int>(fp.max_depth) + 2;          // depths 0 .. max_depth+1
-    // early fold (WfStreams::fold_early = K): once generation K-1's shading is queued, the chains
-    // that ended by K-1 fold on its B stream (after the other B streams' shading), overlapped with
-    // the latency-bound late generations; the frame-end fold takes the chains of Q_K, which
-    // generation K-1 lists as it queues their rays
-    const int K = ws.fold_early;
-    const bool early = K > 0 && ws.tail_fuse == 0 && static_cast<uint32_t>(K - 1) <= fp.max_depth && ws.nb > 0 &&
-                       ws.b[0] != ws.a;
-    WfBufs b = b_in;
-    b.flist_gen = early ? static_cast<uint32_t>(K) : 0u;
     for (int k = 0; k < gens; ++k) {
         hipError_t e;
 #define RT_GEN(N, O) e = (count ? launch_generation<N, O, true>(sc, fp, b, k, ws) \
@@ -1419,17 +1403,6 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
             e = hipEventRecord(mark, ws.a);
             if (e != hipSuccess) return e;
         }
-        if (early && k == K - 1) {
-            const int fi = k % ws.nb;
-            for (int i = 0; i < ws.nb; ++i) {
-                if (i == fi) continue;
-                if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(ws.b[fi], ws.b_done[i], 0)) != hipSuccess) return e;
-            }
-            if ((e = launch_fold(sc, fp, b, ws.b[fi], ws.mb[fi], 0u, static_cast<uint32_t>(k), 0,
-                                 static_cast<uint32_t>(ws.fold_early_wgs))) != hipSuccess)
-                return e;
-        }
     }
     hipError_t e;
     // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
@@ -1443,10 +1416,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     // the chains not folded yet (all of them without the fused tail, which folded every chain:
     // its own as it ended them, the others on a B stream)
-    if (ws.tail_fuse == 0 &&
-        (e = early ? launch_fold(sc, fp, b, ws.a, ws.ma, static_cast<uint32_t>(K), kNlevRunning - 1u, 1)
-                   : launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess)
-        return e;
+    if (ws.tail_fuse == 0 && (e = launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess) return e;
     if (b.compose) {                         // the frame, row by row, once every chain has its colour
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
         const uint64_t segs = static_cast<uint64_t>((fp.tile_w + 63u) / 64u) * fp.rows;

@@ -363,25 +363,6 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
             assert kt["fold"][1] == 1, (T, kt)     # the chains that ended by T-1
 
 
-@pytest.mark.parametrize("scene", ["axis_ties", "sphere_chain", "config3", "planes_nan"])
-def test_early_fold_matches_oracle(gpu_ctx, scene):
-    """The early fold (tuning fold_early = K, no fused tail): the chains that
-    ended by generation K-1 fold on a B stream while later generations run, the
-    frame-end fold takes the chains of Q_K (listed by generation K-1): the
-    oracle's image for K = 1 .. 6, with two fold launches per render (one when
-    K-1 exceeds the depth)."""
-    s = {"axis_ties": _axis_tie_scene, "sphere_chain": _sphere_chain_scene, "config3": lambda: scenes.config3(160, 128),
-         "planes_nan": _nan_plane_scene}[scene]()
-    for K in (1, 2, 3, 4, 6):
-        with _with_tuning(gpu_ctx, tail_fuse=0, fold_early=K):
-            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
-            gpu_ctx.kernel_times()
-            gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
-                                          flags=lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS))
-            kt = gpu_ctx.kernel_times()
-        assert kt["fold"][1] == (2 if K - 1 <= s.max_depth else 1), (K, kt)
-
-
 @pytest.mark.parametrize("scene", ["axis_ties", "config3", "dense", "planes_nan", "config4", "camera_inside"])
 def test_camera_view_grid_matches_oracle(gpu_ctx, scene):
     """Generation 0 through the camera's view grid (tuning cam 3, trace_common.hpp
@@ -715,9 +696,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
                dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
-               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0),
-               dict(fold_early=1), dict(fold_early=4), dict(fold_early=6, bstreams=1), dict(fold_early=9, compose=1),
-               dict(fold_early=12)]:
+               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

@@ -209,10 +209,12 @@ __device__ __forceinline__ bool wg_has_work(const WfBufs& b, uint32_t n, uint32_
 // (s_scan[G] = queue size; G <= kMaxScan: the regions of up to kMaxScan / G
 // consecutive generations, laid out one after the other).  s_wave: 16 words.
 // Ends with a barrier.
+template <int kT = kWfThreads>
 __device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan, uint32_t* s_wave) {
-    const uint32_t per = (G + kWfThreads - 1) / kWfThreads;       // 1 .. 4
+    const uint32_t per = (G + kT - 1) / kT;                         // 1 .. 4 (1024 threads), .. 16 (256)
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint32_t v[4] = {0, 0, 0, 0}, sum = 0;
+    constexpr int kPer = (kMaxScan + kT - 1) / kT;
+    uint32_t v[kPer] = {}, sum = 0;
     for (uint32_t e = 0; e < per; ++e) {
         const uint32_t i = t * per + e;
         v[e] = i < G ? counts[i] : 0u;
@@ -227,7 +229,7 @@ __device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan
     __syncthreads();
     if (t == 0) {
         uint32_t acc = 0;
-        for (int w = 0; w < kWfThreads / 64; ++w) { const uint32_t x = s_wave[w]; s_wave[w] = acc; acc += x; }
+        for (int w = 0; w < kT / 64; ++w) { const uint32_t x = s_wave[w]; s_wave[w] = acc; acc += x; }
     }
     __syncthreads();
     uint32_t run = s_wave[wave] + inc - sum;
@@ -236,7 +238,7 @@ __device__ void region_scan(const uint32_t* counts, uint32_t G, uint32_t* s_scan
         if (i < G) s_scan[i] = run;
         run += v[e];
     }
-    if (t == kWfThreads - 1) s_scan[G] = run;
+    if (t == kT - 1) s_scan[G] = run;
     __syncthreads();
 }
 
@@ -320,6 +322,9 @@ __device__ __forceinline__ Ray load_ray(const WfBufs& b, int q, size_t i) {
 #endif
 #ifndef RT_FOLD_WAVES
 #define RT_FOLD_WAVES 1         // wf_fold's launch bounds: min waves per SIMD (1: the compiler's choice, 96 VGPRs)
+#endif
+#ifndef RT_FOLD_THREADS
+#define RT_FOLD_THREADS 256     // wf_fold's workgroup size
 #endif
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 1
@@ -1110,17 +1115,22 @@ __global__ __launch_bounds__(kWfThreads, 4) void wf_tail(DevScene sc, FrameParam
 // Only chains of lo <= nlev <= hi: with the fused tail, the chains that ended
 // by generation T-1 fold on a B stream while the tail runs (every level and
 // terminal they need is written by then); the tail folds its own.
+// RT_FOLD_THREADS-thread workgroups (256: at the fold's ~96 VGPRs five of them,
+// 20 waves, fit a CU where one 1024-thread workgroup leaves 4 wave slots idle),
+// dealt block-major over (kWfThreads / RT_FOLD_THREADS) x G workgroups.
 template <bool kFresnel>
-__global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo, uint32_t hi) {
+__global__ __launch_bounds__(RT_FOLD_THREADS, RT_FOLD_WAVES) void wf_fold(DevScene sc, FrameParams fp, WfBufs b, uint32_t lo,
+                                                                          uint32_t hi) {
+    constexpr int kT = RT_FOLD_THREADS;
     __shared__ double s_srgb[255];
     __shared__ uint32_t s_scan[kMaxRegions + 1];
-    __shared__ uint32_t s_wave[kWfThreads / 64];
-    for (int i = threadIdx.x; i < 255; i += kWfThreads) s_srgb[i] = c_srgb_avg[i];
-    region_scan(b.rs(), b.G, s_scan, s_wave);             // generation 0's records = the chains (also publishes s_srgb)
+    __shared__ uint32_t s_wave[kT / 64];
+    for (int i = threadIdx.x; i < 255; i += kT) s_srgb[i] = c_srgb_avg[i];
+    region_scan<kT>(b.rs(), b.G, s_scan, s_wave);         // generation 0's records = the chains (also publishes s_srgb)
     const uint32_t n = s_scan[b.G];
     // software pipelined: the next chunk's chain header (level count, pixel, terminal) is
     // loaded before this chain's levels are folded, one dependent round trip less per chain
-    const uint32_t W = gridDim.x * (kWfThreads / 64), lane = threadIdx.x & 63u;
+    const uint32_t W = gridDim.x * (kT / 64), lane = threadIdx.x & 63u;
     struct Head {
         uint32_t c, nlev, p;
         Col term;
@@ -1136,7 +1146,7 @@ __global__ __launch_bounds__(kWfThreads, RT_FOLD_WAVES) void wf_fold(DevScene sc
         }
         return hd;
     };
-    uint32_t rc = wave_slot(b, n);
+    uint32_t rc = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
     Head cur = head(static_cast<uint64_t>(rc) * 64u + lane);
     for (; static_cast<uint64_t>(rc) * 64u < n; rc += W) {
         const Head nxt = head(static_cast<uint64_t>(rc + W) * 64u + lane);
@@ -1152,8 +1162,9 @@ hipError_t launch_fold(const DevScene& sc, const FrameParams& fp, const WfBufs& 
                        uint32_t lo, uint32_t hi) {
     hipError_t e;
     if (m && (e = m->begin(s)) != hipSuccess) return e;
-    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
-    else hipLaunchKernelGGL((wf_fold<false>), dim3(b.G), dim3(kWfThreads), 0, s, sc, fp, b, lo, hi);
+    const dim3 grid(b.G * (kWfThreads / RT_FOLD_THREADS)), block(RT_FOLD_THREADS);
+    if (sc.has_fresnel) hipLaunchKernelGGL((wf_fold<true>), grid, block, 0, s, sc, fp, b, lo, hi);
+    else hipLaunchKernelGGL((wf_fold<false>), grid, block, 0, s, sc, fp, b, lo, hi);
     return m ? m->mark(s, kKfFold) : hipGetLastError();
 }
 

@@ -64,10 +64,8 @@ static_assert(sizeof(DevBvhNode) == 64, "BVH node is one 64-B line");
 // the f32 box and the culling argument of DESIGN.md §4 carries over.  32 B:
 // twice the nodes of an LDS prefix and half the bytes per L2 fetch below it.
 // Built only when every bound is finite and within the half range (+-65504).
-// Per child c and axis a one dword (lo, hi) at b[2 (3c + a)], so a walk can put
-// the ray's near bound in the low half by one byte permute per axis.
 struct alignas(16) DevBvhNodeH {
-    uint16_t b[12];                 // child 0: (lo, hi) of x, y, z; child 1 the same (binary16 bits)
+    uint16_t b[12];                 // lo0 xyz, hi0 xyz, lo1 xyz, hi1 xyz (binary16 bits)
     int32_t c0, c1;
 };
 static_assert(sizeof(DevBvhNodeH) == 32, "half BVH node is 32 B");

@@ -393,8 +393,8 @@ std::vector<DevBvhNodeH> half_nodes(const BvhResult& b2) {
         const DevBvhNode& n = b2.nodes[k];
         DevBvhNodeH& h = out[k];
         for (int a = 0; a < 3; ++a) {
-            if (!half_round_down(n.lo0[a], h.b[2 * a]) || !half_round_up(n.hi0[a], h.b[2 * a + 1]) ||
-                !half_round_down(n.lo1[a], h.b[6 + 2 * a]) || !half_round_up(n.hi1[a], h.b[6 + 2 * a + 1]))
+            if (!half_round_down(n.lo0[a], h.b[a]) || !half_round_up(n.hi0[a], h.b[3 + a]) ||
+                !half_round_down(n.lo1[a], h.b[6 + a]) || !half_round_up(n.hi1[a], h.b[9 + a]))
                 return {};
         }
         h.c0 = n.c0;

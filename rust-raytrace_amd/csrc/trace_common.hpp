@@ -464,8 +464,8 @@ __device__ __forceinline__ DevBvhNode fetch_node(const BvhView& v, int32_t i) {
         DevBvhNode nd;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            nd.lo0[a] = half_bits_f(h.b[2 * a]); nd.hi0[a] = half_bits_f(h.b[2 * a + 1]);
-            nd.lo1[a] = half_bits_f(h.b[6 + 2 * a]); nd.hi1[a] = half_bits_f(h.b[6 + 2 * a + 1]);
+            nd.lo0[a] = half_bits_f(h.b[a]); nd.hi0[a] = half_bits_f(h.b[3 + a]);
+            nd.lo1[a] = half_bits_f(h.b[6 + a]); nd.hi1[a] = half_bits_f(h.b[9 + a]);
         }
         nd.c0 = h.c0; nd.c1 = h.c1;
         return nd;
@@ -646,10 +646,6 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
     // node 0, so node byte offset (c + 1) * 8 addresses pair c.
     [[maybe_unused]] const char *nxa = nullptr, *fxa = nullptr, *nya = nullptr, *fya = nullptr, *nza = nullptr,
                                 *fza = nullptr, *ca = nullptr;
-    // binary16 nodes (kNodes 3): v_perm selectors putting the near bound in the low half
-    [[maybe_unused]] const uint32_t selx = rb.ix >= 0.0f ? 0x03020100u : 0x01000302u;
-    [[maybe_unused]] const uint32_t sely = rb.iy >= 0.0f ? 0x03020100u : 0x01000302u;
-    [[maybe_unused]] const uint32_t selz = rb.iz >= 0.0f ? 0x03020100u : 0x01000302u;
     if constexpr (kNodes == 2) {
         const char* L = reinterpret_cast<const char*>(v.lnodes) - 8;
         const size_t n8 = static_cast<size_t>(v.nl) * 8;
@@ -691,29 +687,6 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
                 h1 = x1 <= tlim && !(x1 > f1);
                 c0 = cc.x;
                 c1 = cc.y;
-            } else if constexpr (kNodes == 3) {
-                // binary16 node: per child and axis the (lo, hi) dword permuted so that the
-                // low half is the ray's near bound (hi when 1/d < 0), then one mixed FMA per
-                // bound (exact half -> f32) and no min / max per axis
-                const DevBvhNodeH hn = *(cur < v.nl ? v.hpnodes + cur : v.hgnodes + cur);
-                const uint32_t* d = reinterpret_cast<const uint32_t*>(hn.b);
-                auto nf = [](uint32_t w, uint32_t sel, float i, float no, float& tn, float& tf) {
-                    const uint32_t p = __builtin_amdgcn_perm(w, w, sel);
-                    tn = slab_t(half_bits_f(static_cast<uint16_t>(p)), i, no);
-                    tf = slab_t(half_bits_f(static_cast<uint16_t>(p >> 16)), i, no);
-                };
-                float nx0, fx0, ny0, fy0, nz0, fz0, nx1, fx1, ny1, fy1, nz1, fz1;
-                nf(d[0], selx, rb.ix, rb.nox, nx0, fx0); nf(d[1], sely, rb.iy, rb.noy, ny0, fy0);
-                nf(d[2], selz, rb.iz, rb.noz, nz0, fz0); nf(d[3], selx, rb.ix, rb.nox, nx1, fx1);
-                nf(d[4], sely, rb.iy, rb.noy, ny1, fy1); nf(d[5], selz, rb.iz, rb.noz, nz1, fz1);
-                t0 = fmaxf(fmaxf(nx0, ny0), nz0) * kWidenLo;
-                t1 = fmaxf(fmaxf(nx1, ny1), nz1) * kWidenLo;
-                const float f0 = fminf(fminf(fx0, fy0), fz0) * kWidenHi, f1 = fminf(fminf(fx1, fy1), fz1) * kWidenHi;
-                const float x0 = fmaxf(t0, 0.0f), x1 = fmaxf(t1, 0.0f);
-                h0 = x0 <= tlim && !(x0 > f0);                      // as in the LDS walk
-                h1 = x1 <= tlim && !(x1 > f1);
-                c0 = hn.c0;
-                c1 = hn.c1;
             } else {
                 const DevBvhNode nd = fetch_node<kNodes>(v, cur);
                 h0 = box_hit(nd.lo0, nd.hi0, rb, tlim, t0);

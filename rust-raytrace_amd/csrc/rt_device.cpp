@@ -47,7 +47,7 @@ struct TuneDef {
 // fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs, shade_wgs.
 constexpr TuneDef kTune[kTuneCount] = {
     {"chunk_pixels", 0, 0, INT32_MAX},          // wavefront chunk cap (0: what the working-set budget holds at the depth)
-    {"bvh_leaf", 0, 0, 8},                       // 0: 2, or 4 when the tree would not fit the LDS budget
+    {"bvh_leaf", 0, 0, 8},                       // 0: 2 (4 for a quantised tree beyond the LDS budget)
     {"light_grids", 1, 0, 1},                    // light-view grids for point-light shadow queries
     {"light_grid_res", 0, 0, 4096},              // 0: from the median sphere's angular size
     {"src", -1, -1, 26},                         // nearest-hit sphere source (trace_kernel.hip kSrc*)
@@ -707,7 +707,8 @@ int rt_qtree_nodes(const rt_scene* s, int leaf_max, void* nodes, float* boxes, i
                     if (std::isfinite(v)) extent = std::max(extent, std::fabs(v));
         }
         const double pad = 1e-5 * (1.0 + extent);
-        // scene_upload's leaf rule: 2, or 4 when that tree and the spheres would not fit the LDS budget
+        // the quantised tree's leaf rule (scene_upload with tuning qtree): 2, or 4 when that tree
+        // and the spheres would not fit the LDS budget
         int leaf = leaf_max > 0 ? leaf_max : 2;
         BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf);
         if (leaf_max == 0 && bvh.nodes.size() * sizeof(DevBvhNode) + sx.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
@@ -810,7 +811,10 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const double pad = 1e-5 * (1.0 + extent);
     const int leaf_env = static_cast<int>(c->t(kTuneBvhLeaf));
     BvhResult bvh = build_sphere_bvh(sx, sy, sz, srad, pad, leaf_env > 0 ? leaf_env : 2);
-    if (leaf_env <= 0 && bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
+    // leaves of 2 whatever the tree's size (C4 49.4 vs 50.3 ms, C5 293.3 vs 297.1 ms with 4 on one
+    // box); 4 only for the quantised tree (tuning qtree), whose C4 tree then fits the LDS
+    if (leaf_env <= 0 && c->t(kTuneQTree) != 0 &&
+        bvh.nodes.size() * sizeof(DevBvhNode) + spheres.size() * (sizeof(DevSphere) + 4) > kLdsBudget)
         bvh = build_sphere_bvh(sx, sy, sz, srad, pad, 4);
     const Bvh4Result bvh4 = collapse_bvh4(bvh);
     // traversal stacks hold 64 entries (trace_common.hpp kBvhStack / kBvh4Stack)

@@ -484,8 +484,16 @@ def main():
         f = i % F
         ctxs[f].render_device(o, outs[f][0].data_ptr(), outs[f][1].data_ptr(), streams[f].cuda_stream)
 
+    # the cold first frame (a process that renders one frame, as main.rs does, pays it): the
+    # working set's allocation, the first launch of every kernel (code object load) and the
+    # scratch setup of the hardware queues, against the second (warm) frame
+    cold_ms = []
     for i in range(max(args.warmup, F)):
+        t0c = time.perf_counter()
         step(i=i)
+        if i < 2:
+            torch.cuda.synchronize(dev)
+            cold_ms.append((time.perf_counter() - t0c) * 1e3)
     torch.cuda.synchronize(dev)
     st = ctx.stats()                       # rays of one frame-slice (deterministic: same every step)
     local_rays, local_traced = st.rays, st.traced_rays
@@ -646,6 +654,11 @@ def main():
                         "generation_queue_sizes": gen_q[:args.depth + 3] if world == 1 else None,
                         "generation_shaded": gen_s[:args.depth + 3] if world == 1 else None},
         }
+        if len(cold_ms) == 2:
+            line["first_frame_ms"] = {"first": round(cold_ms[0], 3), "second": round(cold_ms[1], 3),
+                                      "note": "wall clock of the first two renders after the upload (synchronised): "
+                                              "the first pays the working set's hipMalloc, each kernel's first "
+                                              "launch and the queues' scratch setup"}
         line["upload_ms"] = {"first": round(upload_ms[0], 3), "repeat": round(min(upload_ms[1:]), 3),
                              "note": "rt_scene_upload once per scene, outside the timed region: host SAH BVH + "
                                      "4-wide tree + light-view grids + camera view, then one H2D copy of the blob"}

@@ -1279,12 +1279,18 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             // fused tail (tuning tail_fuse = T): the src-9 tree and light-view grid shadows
             {
                 // auto: from generation 4 for chunks of <= 4.5 M pixel slots (one rank's share of a 4- or
-                // 8-way C3 frame), from 5 up to 9 M (a 2-way share), off above (the whole C3 frame: 2.933
-                // vs 2.921 ms with T = 7); with the tail's own fold on one box: 8-way share 0.855 -> 0.751
-                // ms, 4-way 1.140 -> 1.040, 2-way 1.725 -> 1.642
+                // 8-way C3 frame), from 5 up to 9 M (a 2-way share); with the tail's own fold on one box:
+                // 8-way share 0.855 -> 0.751 ms, 4-way 1.140 -> 1.040, 2-way 1.725 -> 1.642 (round 5
+                // re-check: 4-way T 5 / 6 1.030 / 1.052 vs 1.039, 2-way T 6 / 7 1.675 / 1.683 vs 1.636-1.642)
                 const uint64_t S = static_cast<uint64_t>(tiles_x) * 64u * (chunk_rows / 8);
                 int T = static_cast<int>(c->t(kTuneTailFuse));
-                if (T < 0) T = S <= 4500000u ? 4 : S <= 9000000u ? 5 : 0;
+                // above 9 M slots (the whole C3 frame): from generation max_depth - 1 when that is
+                // >= 4 (round 5, depth 8: T = 7 2.898-2.902 vs 2.943-2.945 ms without the tail; 6 /
+                // 8 / 9: 2.961 / 2.947-2.960 / 2.970 ms)
+                if (T < 0) {
+                    const int late = static_cast<int>(o->max_depth) - 1;
+                    T = S <= 4500000u ? 4 : S <= 9000000u ? 5 : (late >= 4 ? late : 0);
+                }
                 const bool ok = T >= 1 && static_cast<uint32_t>(T) <= o->max_depth + 1 && src == 9 && c->all_lights_gridded &&
                                 c->t(kTuneGridOcc) != 0;
                 ws.tail_fuse = ok ? T : 0;

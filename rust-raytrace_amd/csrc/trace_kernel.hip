@@ -463,6 +463,10 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     return v;
 }
 
+// register entries on top of the binary16 prefix walk's stack (src 5, 6; A/B builds)
+#ifndef RT_HALF_REG
+#define RT_HALF_REG 2
+#endif
 // register entries on top of the compact stack (the whole tree in LDS, src 9): one (C3 3.054 vs
 // 3.116 ms, 8-way share 0.756 vs 0.765 ms on one box; two 3.168 vs 3.144 ms); A/B builds:
 // EXTRA=-DRT_COMPACT_REG=n
@@ -479,7 +483,7 @@ __device__ __forceinline__ Hit nearest_any(const DevScene& sc, const BvhView& v,
     // 64-bit stack: 3.66 -> 3.80 ms with 1-4 in round 2)
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::nodes == 2)
         return nearest_bvh_bl<kCount, 2, Src<kSrc>::compact_bits ? RT_COMPACT_REG : 0, Src<kSrc>::compact_bits>(sc, v, r, w);
-    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, 2, Src<kSrc>::compact_bits>(sc, v, r, w);
+    else if constexpr (Src<kSrc>::bvh && Src<kSrc>::half) return nearest_bvh_bl<kCount, 3, RT_HALF_REG, Src<kSrc>::compact_bits>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh && Src<kSrc>::prefix) return nearest_bvh_bl<kCount, 1, 2>(sc, v, r, w);
     else if constexpr (Src<kSrc>::bvh) return nearest_bvh_bl<kCount, 0, 0>(sc, v, r, w);
     else return nearest_brute<kCount>(sc, v.sph, r, w);

@@ -463,9 +463,10 @@ __device__ __forceinline__ BvhView stage_lds(const DevScene& sc, unsigned char* 
     return v;
 }
 
-// register entries on top of the binary16 prefix walk's stack (src 5, 6; A/B builds)
+// register entries on top of the binary16 prefix walk's stack (src 5, 6): three (C4 49.80-49.86
+// vs 50.07-50.09 ms with two, 50.41 with one, 50.36 with four; C5 equal within 0.5%)
 #ifndef RT_HALF_REG
-#define RT_HALF_REG 2
+#define RT_HALF_REG 3
 #endif
 // register entries on top of the compact stack (the whole tree in LDS, src 9): one (C3 3.054 vs
 // 3.116 ms, 8-way share 0.756 vs 0.765 ms on one box; two 3.168 vs 3.144 ms); A/B builds:

@@ -77,8 +77,6 @@ struct WfStreams {
     int tail_fuse;        // > 0: the chains running at generation tail_fuse - 1 finish in one wf_tail
     int tail_wgs;         //   launch on stream a (that many workgroups, all resident: one per CU;
     int tail_width;       //   chains per wave, 0 auto), which folds them; the others fold on b[0]
-    int fold_early;       // K (< tail_fuse): the chains that ended by generation K-1 fold on that
-                          //   generation's b stream before the tail (0: all of them beside the tail)
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);

@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneFoldEarly, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,8 +92,6 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
                                                  // (0: equal chunks)
-    {"fold_early", 0, 0, 32},                    // K < the fused tail's T: the chains that ended by generation K-1
-                                                 // fold on a B stream before the tail, the rest beside it
 };
 
 }  // namespace
@@ -1297,7 +1295,6 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                                 c->t(kTuneGridOcc) != 0;
                 ws.tail_fuse = ok ? T : 0;
                 ws.tail_width = static_cast<int>(c->t(kTuneTailWidth));
-                ws.fold_early = static_cast<int>(c->t(kTuneFoldEarly));
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;

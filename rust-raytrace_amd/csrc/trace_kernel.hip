@@ -1344,9 +1344,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
             if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(ws.b[0], ws.near_done[k], 0)) != hipSuccess) return e;
         }
-        // (after an early fold, WfStreams::fold_early = K, only the chains that ended in K .. T-1)
-        const uint32_t lo = ws.fold_early > 0 && ws.fold_early < k ? static_cast<uint32_t>(ws.fold_early) : 0u;
-        if ((e = launch_fold(sc, fp, b, ws.b[0], ws.b[0] != ws.a ? ws.mb[0] : ws.ma, lo, static_cast<uint32_t>(k - 1))) !=
+        if ((e = launch_fold(sc, fp, b, ws.b[0], ws.b[0] != ws.a ? ws.mb[0] : ws.ma, 0u, static_cast<uint32_t>(k - 1))) !=
             hipSuccess)
             return e;
         if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
@@ -1420,20 +1418,6 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         if (mark && k == mark_gen) {
             e = hipEventRecord(mark, ws.a);
             if (e != hipSuccess) return e;
-        }
-        // early fold (WfStreams::fold_early = K, with the fused tail from a later generation): once
-        // generation K-1's shading is queued, the chains that ended by K-1 fold on its B stream after
-        // the other B streams' shading, while the chain runs generations K .. T-1; the fold beside
-        // the tail then takes only the chains that ended in K .. T-1
-        if (ws.fold_early > 0 && ws.tail_fuse > ws.fold_early && k == ws.fold_early - 1 && ws.nb > 0 &&
-            ws.b[0] != ws.a) {
-            const int fi = k % ws.nb;
-            for (int i = 0; i < ws.nb; ++i) {
-                if (i == fi) continue;
-                if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(ws.b[fi], ws.b_done[i], 0)) != hipSuccess) return e;
-            }
-            if ((e = launch_fold(sc, fp, b, ws.b[fi], ws.mb[fi], 0u, static_cast<uint32_t>(k))) != hipSuccess) return e;
         }
     }
     hipError_t e;

@@ -363,28 +363,6 @@ def test_fused_tail_matches_oracle(gpu_ctx, scene):
             assert kt["fold"][1] == 1, (T, kt)     # the chains that ended by T-1
 
 
-@pytest.mark.parametrize("scene", ["sphere_chain", "config3", "planes_nan"])
-def test_early_fold_before_the_tail_matches_oracle(gpu_ctx, scene):
-    """The early fold (tuning fold_early = K below the fused tail's T): the
-    chains that ended by generation K-1 fold on a B stream before the tail, the
-    ones that ended in K .. T-1 beside it, the tail's own in the tail: the
-    oracle's image, and two fold launches besides the tail."""
-    s = {"sphere_chain": _sphere_chain_scene, "config3": lambda: scenes.config3(160, 128),
-         "planes_nan": _nan_plane_scene}[scene]()
-    s.lights = [l if l["kind"] == "point" else
-                {"kind": "point", "location": tuple(-40.0 * x for x in l["direction"]), "color": l["color"]} for l in s.lights]
-    for T, K in [(3, 1), (4, 2), (4, 3), (6, 4)]:
-        if T > s.max_depth + 1:
-            continue
-        with _with_tuning(gpu_ctx, tail_fuse=T, fold_early=K):
-            check_parity(gpu_ctx, s, lr.RT_ALGO_WAVEFRONT)
-            gpu_ctx.kernel_times()
-            gpu_ctx.render(lr.render_opts(s.width, s.height, max_depth=s.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT,
-                                          flags=lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS))
-            kt = gpu_ctx.kernel_times()
-        assert kt["tail"][1] == 1 and kt["fold"][1] == 2, (T, K, kt)
-
-
 @pytest.mark.parametrize("scene", ["axis_ties", "config3", "dense", "planes_nan", "config4", "camera_inside"])
 def test_camera_view_grid_matches_oracle(gpu_ctx, scene):
     """Generation 0 through the camera's view grid (tuning cam 3, trace_common.hpp
@@ -718,8 +696,7 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
                dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
-               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1),
-               dict(tail_fuse=5, fold_early=3), dict(tail_fuse=7, fold_early=4), dict(fold_early=2, tail_fuse=0)]:
+               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

@@ -66,11 +66,7 @@ struct LightGridResult {
     std::vector<DevLightGrid> grids;    // one per light (R = 0: no grid, e.g. not a point light)
     std::vector<uint32_t> off;          // cell offsets into ent (per face rect: w * h + 1)
     std::vector<DevLgEntry> ent;
-    std::vector<DevCone> cone;          // per grid g and sphere k at [g * n + k] (DevCone)
 };
-constexpr double kConeMargin = 1e-5;    // subtracted from the cosine bound (f32 dot products err < 1e-6)
-// The cone of a sphere (centre c, padded radius r) seen from P (DevCone).
-DevCone sphere_cone(const double c[3], double r, const double P[3]);
 LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
                                   const std::vector<DevLight>& lights, double pad, int r_override);
 // The camera's view grid (the same cube-map layout, one grid centred on `pos`)

@@ -135,16 +135,6 @@ struct DevLgEntry {
     float near;
 };
 
-// The cone a sphere subtends from a grid's centre (a point light or the camera,
-// host_lightgrid.cpp): the unit direction u to its centre and a lower bound of
-// cos of its half-angle asin((r + pad) / |c - P|), less kConeMargin.  Every hit
-// point of the sphere seen from P lies in the cone, so a ray from P (or a
-// shadow segment ending at P) whose unit direction w has w.u < cosl cannot hit
-// it.  cosl = -2: never rejected.
-struct DevCone {
-    float ux, uy, uz, cosl;
-};
-
 struct DevScene {
     const DevSphere* spheres;       // file order among spheres (or BVH order, see sphere_obj)
     const int32_t* sphere_obj;      // object id of each sphere (tie-break key, material index)
@@ -175,11 +165,9 @@ struct DevScene {
     const DevLightGrid* lgrid;       // per light (null: no grids)
     const uint32_t* lg_off;
     const DevLgEntry* lg_ent;
-    const DevCone* lg_cone;          // per light l and sphere k at [l * n_spheres + k] (null: none)
     const DevLightGrid* cgrid;       // the camera's view grid (camera rays' nearest hit; null: none)
     const uint32_t* cg_off;
     const DevLgEntry* cg_ent;
-    const DevCone* cg_cone;          // per sphere, seen from the camera (null: none)
     const DevQNode4* q4;             // the quantised 4-wide tree (null: not representable)
     int32_t n_q4;                    // its nodes (breadth-first; root = node 0)
     int32_t pfxq;                    // nodes [0, pfxq) staged in LDS by the quantised-tree source (set per render)

@@ -50,27 +50,11 @@ int cell_of(double u, int R) {
 
 }  // namespace
 
-DevCone sphere_cone(const double c[3], double r, const double P[3]) {
-    const double u[3] = {c[0] - P[0], c[1] - P[1], c[2] - P[2]};
-    const double D = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
-    DevCone k{0.0f, 0.0f, 0.0f, -2.0f};
-    if (!std::isfinite(D) || !std::isfinite(r) || !(D > 0.0)) return k;
-    const double sn = r / D;
-    if (!(sn < 1.0 - 1e-6)) return k;                         // P (nearly) inside: never rejected
-    const double cs = std::sqrt((1.0 - sn) * (1.0 + sn)) - kConeMargin;
-    float cf = static_cast<float>(cs);
-    if (static_cast<double>(cf) > cs) cf = std::nextafter(cf, -3.0f);
-    k.ux = static_cast<float>(u[0] / D); k.uy = static_cast<float>(u[1] / D); k.uz = static_cast<float>(u[2] / D);
-    k.cosl = cf;
-    return k;
-}
-
 LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const std::vector<double>& r_leaf,
                                   const std::vector<DevLight>& lights, double pad, int r_override) {
     LightGridResult out;
     out.grids.assign(lights.size(), DevLightGrid{});
     const size_t n = spheres.size();
-    out.cone.assign(lights.size() * n, DevCone{0.0f, 0.0f, 0.0f, -2.0f});
     for (size_t li = 0; li < lights.size(); ++li) {
         const DevLight& Lt = lights[li];
         DevLightGrid& g = out.grids[li];
@@ -79,10 +63,6 @@ LightGridResult build_light_grids(const std::vector<DevSphere>& spheres, const s
         const double L[3] = {Lt.v[0], Lt.v[1], Lt.v[2]};
         if (!std::isfinite(L[0]) || !std::isfinite(L[1]) || !std::isfinite(L[2])) continue;
         g.lx = L[0]; g.ly = L[1]; g.lz = L[2];
-        for (size_t k = 0; k < n; ++k) {
-            const double c[3] = {spheres[k].cx, spheres[k].cy, spheres[k].cz};
-            out.cone[li * n + k] = sphere_cone(c, std::fabs(r_leaf[k]) + pad, L);
-        }
         // boxes relative to L, widened for the subtraction's rounding
         std::vector<double> lo(3 * n), hi(3 * n), nearv(n);
         std::vector<char> always(n, 0);
@@ -199,11 +179,6 @@ LightGridResult build_view_grid(const std::vector<DevSphere>& spheres, const std
     const size_t n = spheres.size();
     if (n == 0 || !std::isfinite(pos[0]) || !std::isfinite(pos[1]) || !std::isfinite(pos[2])) return out;
     g.lx = pos[0]; g.ly = pos[1]; g.lz = pos[2];
-    out.cone.resize(n);
-    for (size_t k = 0; k < n; ++k) {
-        const double c[3] = {spheres[k].cx, spheres[k].cy, spheres[k].cz};
-        out.cone[k] = sphere_cone(c, std::fabs(r_leaf[k]) + pad, pos);
-    }
     std::vector<double> lo(3 * n), hi(3 * n), nearv(n);
     std::vector<char> always(n, 0);
     for (size_t k = 0; k < n; ++k) {

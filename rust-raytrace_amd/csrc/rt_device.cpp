@@ -35,7 +35,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCones, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,8 +92,6 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
                                                  // (0: equal chunks)
-    {"cones", 1, 0, 1},                          // grid queries skip a listed sphere whose cone from the grid's
-                                                 // centre the ray's direction lies outside of (at scene upload)
 };
 
 }  // namespace
@@ -874,8 +872,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     const size_t o_cg = place(cg.grids.size() * sizeof(DevLightGrid));
     const size_t o_cgoff = place(cg.off.size() * sizeof(uint32_t));
     const size_t o_cgent = place(cg.ent.size() * sizeof(DevLgEntry));
-    const size_t o_lgcone = place(lg.cone.size() * sizeof(DevCone));
-    const size_t o_cgcone = place(cg.cone.size() * sizeof(DevCone));
     size_t tex_bytes = 0;
     uint64_t face_off[6] = {0, 0, 0, 0, 0, 0};
     if (skybox)
@@ -901,8 +897,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     put(o_cg, cg.grids.data(), cg.grids.size() * sizeof(DevLightGrid));
     put(o_cgoff, cg.off.data(), cg.off.size() * sizeof(uint32_t));
     put(o_cgent, cg.ent.data(), cg.ent.size() * sizeof(DevLgEntry));
-    put(o_lgcone, lg.cone.data(), lg.cone.size() * sizeof(DevCone));
-    put(o_cgcone, cg.cone.data(), cg.cone.size() * sizeof(DevCone));
     if (skybox)
         for (int k = 0; k < 6; ++k) put(o_tex + face_off[k], s->skybox[k].rgb.data(), s->skybox[k].rgb.size());
     // every render still reading the old blob (on any stream) must be done before it is overwritten
@@ -964,8 +958,6 @@ static int scene_upload(rt_ctx* c, const rt_scene* s) {
     d.cgrid = (cg.grids.empty() || cg.grids[0].R <= 0) ? nullptr : reinterpret_cast<const DevLightGrid*>(base + o_cg);
     d.cg_off = reinterpret_cast<const uint32_t*>(base + o_cgoff);
     d.cg_ent = reinterpret_cast<const DevLgEntry*>(base + o_cgent);
-    d.lg_cone = lg.cone.empty() || c->t(kTuneCones) == 0 ? nullptr : reinterpret_cast<const DevCone*>(base + o_lgcone);
-    d.cg_cone = cg.cone.empty() || c->t(kTuneCones) == 0 ? nullptr : reinterpret_cast<const DevCone*>(base + o_cgcone);
     c->all_lights_gridded = !lights.empty() && lg.grids.size() == lights.size();
     for (const DevLightGrid& g : lg.grids) c->all_lights_gridded = c->all_lights_gridded && g.R > 0;
     c->scene_spp = s->antialias;

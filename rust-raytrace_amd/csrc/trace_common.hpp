@@ -1007,8 +1007,8 @@ __device__ __forceinline__ bool occluded_bvh4(const DevScene& sc, const BvhView&
 // A degenerate direction (p at the light, non-finite) tests every sphere.
 template <bool kCount = false>
 __device__ __forceinline__ bool occluded_lgrid(const DevScene& sc, const BvhView& v, const DevLightGrid& g,
-                                               const DevCone* cone, const Ray& r, double r2, double ptx, double pty,
-                                               double ptz, int32_t hint, Work* w = nullptr) {
+                                               const Ray& r, double r2, double ptx, double pty, double ptz,
+                                               int32_t hint, Work* w = nullptr) {
     bool plane_block = false;
     for (int i = 0; i < sc.n_planes; ++i) {
         double t;
@@ -1049,17 +1049,10 @@ __device__ __forceinline__ bool occluded_lgrid(const DevScene& sc, const BvhView
     if (li < 0 || lj < 0 || li >= g.fw[f] || lj >= g.fh[f]) return false;    // no sphere in this direction
     const uint32_t cell = g.off_base[f] + static_cast<uint32_t>(lj * g.fw[f] + li);
     const uint32_t e0 = sc.lg_off[cell], e1 = sc.lg_off[cell + 1];
-    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float dist = len * 1.00001f + 1e-5f;                                        // >= |p - L|
-    const float iw = 1.0f / len;                                                     // w = (p - L) / |p - L|
-    const float wx = dx * iw, wy = dy * iw, wz = dz * iw;
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz) * 1.00001f + 1e-5f;     // >= |p - L|
     for (uint32_t e = e0; e < e1; ++e) {
         const DevLgEntry en = sc.lg_ent[e];
         if (en.near > dist) break;
-        if (cone) {                          // the segment's direction from L outside the sphere's cone
-            const DevCone k = cone[en.sph];
-            if (wx * k.ux + wy * k.uy + wz * k.uz < k.cosl) continue;
-        }
         if (blocks(en.sph)) return true;
     }
     return false;
@@ -1113,16 +1106,9 @@ __device__ __forceinline__ Hit nearest_cgrid(const DevScene& sc, const BvhView& 
     if (li < 0 || lj < 0 || li >= g.fw[f] || lj >= g.fh[f]) return h;        // no sphere box in this direction
     const uint32_t cell = g.off_base[f] + static_cast<uint32_t>(lj * g.fw[f] + li);
     const uint32_t e0 = sc.cg_off[cell], e1 = sc.cg_off[cell + 1];
-    const float iw = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);             // w = d / |d|
-    const float wx = dx * iw, wy = dy * iw, wz = dz * iw;
-    const DevCone* cone = sc.cg_cone;
     for (uint32_t e = e0; e < e1; ++e) {
         const DevLgEntry en = sc.cg_ent[e];
         if (en.near > lim) break;
-        if (cone) {                          // the ray's direction outside the sphere's cone from the camera
-            const DevCone k = cone[en.sph];
-            if (wx * k.ux + wy * k.uy + wz * k.uz < k.cosl) continue;
-        }
         test(en.sph);
     }
     return h;

@@ -905,10 +905,10 @@ __global__ __launch_bounds__(kWfThreads, Src<kSrc>::waves) void wf_occlusion(Dev
         // the sphere the point lies on is tested first (it shadows every light behind its surface)
         bool occluded;
         if constexpr (Src<kSrc>::grid)          // the host checked: every light has a grid
-            occluded = occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sc.lg_cone ? sc.lg_cone + static_cast<size_t>(l) * sc.n_spheres : nullptr, sray, r2, ptx, pty, ptz, hint, &w);
+            occluded = occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w);
         else
             occluded = has_range && sc.lgrid && sc.lgrid[l].R > 0
-                           ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sc.lg_cone ? sc.lg_cone + static_cast<size_t>(l) * sc.n_spheres : nullptr, sray, r2, ptx, pty, ptz, hint, &w)
+                           ? occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, hint, &w)
                            : occluded_any<kSrc, kCount>(sc, v, sray, has_range, r2, hint, &w);
         if (occluded) atomicOr(&b.ru(3)[at], 1u << l);
     }
@@ -956,7 +956,7 @@ __device__ __forceinline__ uint32_t grid_shadow_mask(const DevScene& sc, const B
         double lx, ly, lz, r2;
         (void)light_dir(sc.lights[l], ptx, pty, ptz, lx, ly, lz, r2);
         const Ray sray{ptx + lx * kEps, pty + ly * kEps, ptz + lz * kEps, lx, ly, lz};
-        if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sc.lg_cone ? sc.lg_cone + static_cast<size_t>(l) * sc.n_spheres : nullptr, sray, r2, ptx, pty, ptz, prim, &wsh)) mask |= 1u << l;
+        if (occluded_lgrid<kCount>(sc, v, sc.lgrid[l], sray, r2, ptx, pty, ptz, prim, &wsh)) mask |= 1u << l;
     }
     return mask;
 }

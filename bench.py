@@ -667,6 +667,11 @@ def main():
                                    "bytes": H * W * 15,
                                    "note": "after the timed region: every rank copies its row bands (f32 RGB + "
                                            "BGR) into one shared page-locked host frame; max over ranks"}
+            e2e = ms_per_step + gather_ms
+            line["render_plus_gather"] = {
+                "ms_per_frame": round(e2e, 3), "value": round(total_traced / (e2e * 1e-3) / 1e6, 3), "unit": "Mrays/s",
+                "note": "the frame rendered, then its bands gathered into the host frame, one after the other (a "
+                        "stream of frames could overlap frame i's gather with frame i+1's render)"}
         if host:
             line["pcie_inclusive"] = {
                 "bgr_only": {"ms_per_frame": round(host["bgr"], 3),

@@ -680,7 +680,9 @@ def main():
                                 "value": round(total_traced / (host["rgb_bgr"] * 1e-3) / 1e6, 3), "unit": "Mrays/s"},
                 "samples_ms": {"bgr_only": host["bgr_samples"], "rgb_and_bgr": host["rgb_bgr_samples"]},
                 "note": f"rt_render into reused pageable host buffers: kernels + D2H of {W * H * 3 / 1e6:.0f} MB "
-                        f"BGR (+ {W * H * 12 / 1e6:.0f} MB f32 RGB) through the pinned staging slices"}
+                        f"BGR (+ {W * H * 12 / 1e6:.0f} MB f32 RGB) through the pinned staging slices: the frame "
+                        f"after the camera pass, during the later generations, then the packed segments of the "
+                        f"chain pixels (tuning sparse_out, DESIGN.md §3.11)"}
         if world == 1 and not args.no_cpu:
             try:
                 draws = dict(jitter=1, seed=cfg[3], rng=1) if path_cfg else {}

@@ -322,7 +322,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * its pixel as it ends), host_chunks (rt_render into host memory: at least
  * this many chunks, the D2H copy of each chunk's rows overlapping the later
  * chunks), host_first (with host_chunks 2: the first chunk's percentage of
- * the rows, 0 equal).
+ * the rows, 0 equal), sparse_out (rt_render into host memory, a one-chunk
+ * wavefront render: the frame is copied after the camera pass while the
+ * generations run, then only the 16-pixel row segments holding pixels whose
+ * chain was still running, packed on the device).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

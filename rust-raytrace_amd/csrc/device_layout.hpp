@@ -259,6 +259,8 @@ struct PathStack {
 //   cpix     the chunk pixel of each chain [qcap] (u32);
 //   pmap     (compose) per chunk pixel [cap]: its chain, or kPixBackground /
 //            kPixAmbient | object for a camera ray that ended without a chain;
+//            With mark (sparse host copies) its first cap bytes are cmark
+//            instead: 1 for a pixel that starts a chain, else 0;
 //   ccol     (compose) per chain [capa]: final colour f32 r,g,b and the sRGB
 //            bytes b | g << 8 | r << 16 (16 B), written by the fold in chain
 //            order and read by wf_compose, which writes the frame row by row.
@@ -284,6 +286,7 @@ struct WfBufs {
                                     // workgroup (idle workgroups exit at once), 0 = workgroup-first
     uint32_t compose;               // 1: final colours go through pmap / ccol and wf_compose writes the
                                     //   frame in row order; 0: the camera pass and the fold write pixels
+    uint32_t mark;                  // 1 (sparse host copies, compose 0): the camera pass writes cmark
 
     // queues: f = 0..5 origin / direction, 6 significance
     RT_HD double* qf(int q, int f) const { return reinterpret_cast<double*>(mem) + (static_cast<uint64_t>(q) * 8 + f) * qcap; }
@@ -306,6 +309,9 @@ struct WfBufs {
     RT_HD uint32_t* cpix() const { return reinterpret_cast<uint32_t*>(mem + o_cpix); }   // chain -> chunk pixel
     RT_HD uint32_t* pmap() const { return reinterpret_cast<uint32_t*>(mem + o_pmap); }   // chunk pixel -> chain / code
     RT_HD uint32_t* ccol() const { return reinterpret_cast<uint32_t*>(mem + o_ccol); }   // chain c -> final colour [4c, 4c+4)
+    // (mark) chunk pixel -> 1 if a chain starts there, 0 if the camera pass wrote its final colour
+    // (the pmap section's bytes: compose and mark are never on together)
+    RT_HD uint8_t* cmark() const { return mem + o_pmap; }
     RT_HD uint32_t* rq() const { return reinterpret_cast<uint32_t*>(mem + o_rq); }
     RT_HD uint32_t* rs() const { return reinterpret_cast<uint32_t*>(mem + o_rs); }
 };

@@ -77,10 +77,26 @@ struct WfStreams {
     int tail_fuse;        // > 0: the chains running at generation tail_fuse - 1 finish in one wf_tail
     int tail_wgs;         //   launch on stream a (that many workgroups, all resident: one per CU;
     int tail_width;       //   chains per wave, 0 auto), which folds them; the others fold on b[0]
+    // sparse host copies (b.mark set): after generation 0 (sp_cam), stream sp_s runs the segment
+    // kernels into sp_bits / sp_cnt / sp_off (then sp_ready); after the fold stream a packs the
+    // flagged segments into sp_bgr / sp_rgb (null: that output is off).  sp_s null: off.
+    hipStream_t sp_s = nullptr;
+    hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
+    uint32_t *sp_bits = nullptr, *sp_cnt = nullptr, *sp_off = nullptr;
+    uint8_t* sp_bgr = nullptr;
+    float* sp_rgb = nullptr;
 };
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
+// Sparse host copies (tuning sparse_out): pixels per row segment; after the camera pass
+// (b.mark set) segbits / rowcnt / rowoff of the chunk's rows (wf_chain_segs + wf_row_scan);
+// after the fold the flagged segments packed in row order (wf_chain_pack).
+constexpr uint32_t kSegPx = 16;
+hipError_t launch_chain_segs(const FrameParams& fp, const WfBufs& b, uint32_t* segbits, uint32_t* rowcnt, uint32_t* rowoff,
+                             hipStream_t s);
+hipError_t launch_chain_pack(const FrameParams& fp, const uint32_t* segbits, const uint32_t* rowoff, uint8_t* pk_bgr,
+                             float* pk_rgb, hipStream_t s);
 // Diagnostic: div_a2(x, sphere_k(a)) and x / (2a) on the device (rt_div_a2_check).
 hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s);
 

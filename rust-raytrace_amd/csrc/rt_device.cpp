@@ -11,6 +11,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <stdexcept>
@@ -35,7 +36,7 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneSparseOut, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -92,6 +93,9 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // copy of one chunk's rows overlaps the next chunk's generations
     {"host_first", 0, 0, 90},                    // with host_chunks 2: the first chunk's share of the rows in percent
                                                  // (0: equal chunks)
+    {"sparse_out", 1, 0, 1},                     // rt_render into host memory, one chunk: copy the frame after the camera
+                                                 // pass, then only the 16-pixel segments holding chain pixels (§3.11;
+                                                 // C3 BGR 4.00 -> 3.46-3.63 ms, RGB + BGR 8.09-8.17 -> 7.67-7.72 ms)
 };
 
 }  // namespace
@@ -100,7 +104,8 @@ namespace {
 
 // Host threads that move pinned staging slices into the caller's pageable
 // buffer (rt_render): created once per context, so a frame's copy does not pay
-// thread start-up per slice.  copy() splits one memcpy into kParts parts
+// thread start-up per slice.  run() shares any job of parts (the sparse copies'
+// row scatter) the same way.  copy() splits one memcpy into kParts parts
 // shared by the workers and the calling thread (one thread copies pinned ->
 // pageable memory at ~20-28 GB/s, below the DMA's 56 GB/s).  Workers spin
 // briefly for the next slice before sleeping, so consecutive slices of a frame
@@ -124,10 +129,29 @@ public:
         for (std::thread& t : th_) t.join();
     }
     void copy(void* to, const void* from, size_t len) {
-        if (th_.empty()) start();
         const size_t parts = std::max<size_t>(1, std::min<size_t>(kParts, len >> 20));   // >= 1 MiB each
-        if (parts == 1 || th_.empty()) { std::memcpy(to, from, len); return; }
-        const Job j{static_cast<uint8_t*>(to), static_cast<const uint8_t*>(from), len, parts, (len + parts - 1) / parts};
+        if (parts == 1) { std::memcpy(to, from, len); return; }
+        post(Job{static_cast<uint8_t*>(to), static_cast<const uint8_t*>(from), len, parts, (len + parts - 1) / parts, nullptr});
+    }
+    // fn(0 .. parts-1), shared by the workers and the calling thread
+    void run(size_t parts, const std::function<void(size_t)>& fn) {
+        if (parts == 0) return;
+        if (parts == 1) { fn(0); return; }
+        post(Job{nullptr, nullptr, 0, parts, 0, &fn});
+    }
+    static constexpr size_t kParts = 8;
+
+private:
+    struct Job {
+        uint8_t* to = nullptr;
+        const uint8_t* from = nullptr;
+        size_t len = 0, parts = 0, step = 0;
+        const std::function<void(size_t)>* fn = nullptr;   // else a memcpy in parts
+    };
+    void post(const Job& j) {
+        if (th_.empty()) start();
+        if (th_.empty()) { next_.store(0, std::memory_order_relaxed); work(j); return; }
+        const size_t parts = j.parts;
         {
             std::unique_lock<std::mutex> lk(m_);
             idle_.wait(lk, [&] { return active_ == 0; });    // every worker has left the previous job
@@ -141,13 +165,6 @@ public:
         while (done_.load(std::memory_order_acquire) != parts) std::this_thread::yield();
     }
 
-private:
-    struct Job {
-        uint8_t* to = nullptr;
-        const uint8_t* from = nullptr;
-        size_t len = 0, parts = 0, step = 0;
-    };
-    static constexpr size_t kParts = 8;
     void start() {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned n = std::min<unsigned>(kParts - 1, hw > 1 ? hw - 1 : 1u);
@@ -157,8 +174,12 @@ private:
         for (;;) {
             const size_t q = next_.fetch_add(1, std::memory_order_relaxed);
             if (q >= j.parts) return;
-            const size_t a = q * j.step, b = std::min(j.len, a + j.step);
-            if (a < b) std::memcpy(j.to + a, j.from + a, b - a);
+            if (j.fn) {
+                (*j.fn)(q);
+            } else {
+                const size_t a = q * j.step, b = std::min(j.len, a + j.step);
+                if (a < b) std::memcpy(j.to + a, j.from + a, b - a);
+            }
             done_.fetch_add(1, std::memory_order_release);
         }
     }
@@ -263,6 +284,22 @@ struct rt_ctx {
     hipEvent_t band_ev[kMaxBands] = {};
     uint32_t band_row0[kMaxBands] = {}, band_nrows[kMaxBands] = {};
     HostCopyPool pool;
+    // sparse host copies (tuning sparse_out): device segment bits / row counts /
+    // row offsets / packed BGR / packed RGB, the pinned host copies of the first three and of the
+    // packed segments, and an event per piece of the packed copy
+    bool want_sparse = false;              // set by rt_render around its render
+    bool sparse_on = false;                // the last render marked its chain pixels and packed them
+    void* d_sp = nullptr;
+    size_t sp_cap = 0;
+    uint32_t* d_sp_bits = nullptr, *d_sp_cnt = nullptr, *d_sp_off = nullptr;
+    uint8_t* d_sp_bgr = nullptr;
+    float* d_sp_rgb = nullptr;
+    void* h_sp_meta = nullptr;
+    size_t h_sp_meta_cap = 0;
+    void* h_sp_pk = nullptr;
+    size_t h_sp_pk_cap = 0;
+    hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
+    hipEvent_t sp_ev[kMaxBands] = {};
     int64_t tune[kTuneCount];
     std::string err;
     rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
@@ -549,6 +586,12 @@ void rt_ctx_destroy(rt_ctx* c) {
         if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
     }
     for (hipEvent_t e : c->band_ev) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->sp_ev) if (e) (void)hipEventDestroy(e);
+    if (c->sp_cam) (void)hipEventDestroy(c->sp_cam);
+    if (c->sp_ready) (void)hipEventDestroy(c->sp_ready);
+    if (c->d_sp) (void)hipFree(c->d_sp);
+    if (c->h_sp_meta) (void)hipHostFree(c->h_sp_meta);
+    if (c->h_sp_pk) (void)hipHostFree(c->h_sp_pk);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -992,6 +1035,50 @@ static int check_opts(rt_ctx* c, const rt_render_opts* o, uint32_t& spp, uint32_
     return RT_OK;
 }
 
+// The stream of rt_render's device -> host copies.  A CU-masked stream (mask = every CU) gets a
+// hardware queue of its own (ensure_bstreams), so the copies never queue behind the render's launches.
+static int ensure_copy_stream(rt_ctx* c) {
+    if (c->copy_stream) return RT_OK;
+    std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
+    for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    if (hipExtStreamCreateWithCUMask(&c->copy_stream, static_cast<uint32_t>(mask.size()), mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    }
+    return RT_OK;
+}
+
+// Device buffers of the sparse host copies for a tw x rows tile (segment bits, row counts, row
+// offsets, packed BGR and RGB at their largest: every segment flagged), grown on demand.
+static int ensure_sparse(rt_ctx* c, hipStream_t st, uint32_t tw, uint32_t rows, bool bgr, bool rgb) {
+    int rc = ensure_copy_stream(c);
+    if (rc != RT_OK) return rc;
+    if (!c->sp_cam) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_cam, hipEventDisableTiming));
+    if (!c->sp_ready) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ready, hipEventDisableTiming));
+    const uint64_t nseg = (tw + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32, segs = nseg * rows;
+    const uint64_t s_bits = align_up(rows * words * 4, 256), s_cnt = align_up(rows * 4ull, 256),
+                   s_off = align_up((rows + 1ull) * 4, 256), s_bgr = align_up(segs * 3 * kSegPx, 256),
+                   s_rgb = segs * 3 * kSegPx * sizeof(float);
+    const uint64_t need = s_bits + s_cnt + s_off + s_bgr + s_rgb;
+    (void)bgr; (void)rgb;
+    if (need > c->sp_cap) {
+        HIP_TRY(c, hipStreamSynchronize(st));
+        HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
+        if (c->d_sp) (void)hipFree(c->d_sp);
+        c->d_sp = nullptr;
+        c->sp_cap = 0;
+        HIP_TRY(c, hipMalloc(&c->d_sp, need));
+        c->sp_cap = need;
+    }
+    auto* base = static_cast<uint8_t*>(c->d_sp);
+    c->d_sp_bits = reinterpret_cast<uint32_t*>(base);
+    c->d_sp_cnt = reinterpret_cast<uint32_t*>(base + s_bits);
+    c->d_sp_off = reinterpret_cast<uint32_t*>(base + s_bits + s_cnt);
+    c->d_sp_bgr = base + s_bits + s_cnt + s_off;
+    c->d_sp_rgb = reinterpret_cast<float*>(base + s_bits + s_cnt + s_off + s_bgr);
+    return RT_OK;
+}
+
 static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
     if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
     uint32_t spp, band, stride, pitch;
@@ -1058,6 +1145,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
     c->last_spp_traced = 1;
     c->last_chunks = 0;
     c->n_bands = 0;
+    c->sparse_on = false;
     if (o->tile_w == 0 || o->tile_h == 0) {
         c->last_timed = false;
         HIP_TRY(c, hipEventRecord(c->render_done, st));
@@ -1217,11 +1305,17 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             for (auto& L : c->lanes) drop_lane_memory(L);      // retry with half the pixels per chunk
             cap_px = std::max<uint64_t>(1, static_cast<uint64_t>(chunk_rows) * o->tile_w / 2);
         }
+        // sparse host copies: a whole tile in one chunk on one lane, pixels written where they end
+        c->sparse_on = c->want_sparse && n_chunks == 1 && n_lanes == 1 && c->t(kTuneCompose) == 0 && stride == 1 &&
+                       (fp.out_rgb || fp.out_bgr);
+        if (c->sparse_on && (rc = ensure_sparse(c, st, o->tile_w, o->tile_h, fp.out_bgr != nullptr, fp.out_rgb != nullptr)) != RT_OK)
+            return rc;
         for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
             c->lanes[l].b.spread_below = static_cast<uint32_t>(c->t(kTuneSpreadBelow));
             c->lanes[l].b.compose = c->t(kTuneCompose) != 0 ? 1u : 0u;
+            c->lanes[l].b.mark = c->sparse_on ? 1u : 0u;
         }
         c->last_chunks = n_chunks;
         auto chunk_row0 = [&](uint32_t ci) { return first_rows ? (ci ? first_rows : 0u) : ci * chunk_rows; };
@@ -1300,6 +1394,14 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             ws.ma = timed ? &marks : nullptr;
             ws.cam = cam;
             ws.fold_ev = c->n_bands == 0 ? nullptr : &c->band_ev[ci];
+            if (c->sparse_on) {
+                ws.sp_s = c->copy_stream;
+                ws.sp_cam = c->sp_cam;
+                ws.sp_ready = c->sp_ready;
+                ws.sp_bits = c->d_sp_bits; ws.sp_cnt = c->d_sp_cnt; ws.sp_off = c->d_sp_off;
+                ws.sp_bgr = fp.out_bgr ? c->d_sp_bgr : nullptr;
+                ws.sp_rgb = fp.out_rgb ? c->d_sp_rgb : nullptr;
+            }
             // every light gridded: the shadow kernel without a tree walk (spheres staged in LDS when
             // they fit in 64 KB); tuning "grid_occ" 0 keeps the general kernel
             ws.grid_occ = (c->all_lights_gridded && c->t(kTuneGridOcc) != 0)
@@ -1449,19 +1551,13 @@ int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
 // destination gets the DMA directly; pageable memory goes through kRing pinned
 // slices of kSlice bytes, the copy engine filling slices ahead while the host
 // pool empties them in order.  `pitch`: bytes per output row.
-static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uint32_t rows) {
+// wait = false (sparse copies): no wait on the bands, the copy stream's order alone (its
+// segment kernels follow the camera pass).
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uint32_t rows, bool wait = true) {
     const size_t bytes = pitch * rows;
     if (!bytes) return RT_OK;
-    if (!c->copy_stream) {
-        // a CU-masked stream (mask = every CU) gets a hardware queue of its own (ensure_bstreams),
-        // so the copies never queue behind the fold launches of the render's stream
-        std::vector<uint32_t> mask((c->n_cu + 31) / 32, 0u);
-        for (int cu = 0; cu < c->n_cu; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-        if (hipExtStreamCreateWithCUMask(&c->copy_stream, static_cast<uint32_t>(mask.size()), mask.data()) != hipSuccess) {
-            (void)hipGetLastError();
-            HIP_TRY(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-        }
-    }
+    int rc = ensure_copy_stream(c);
+    if (rc != RT_OK) return rc;
     struct Piece { size_t off, len; int band; };
     std::vector<Piece> pieces;
     const int nb = c->n_bands > 0 ? c->n_bands : 1;
@@ -1471,6 +1567,7 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uin
         for (size_t o = a; o < e; o += kSlice) pieces.push_back(Piece{o, std::min(kSlice, e - o), bi});
     }
     auto wait_band = [&](int bi) -> hipError_t {
+        if (!wait) return hipSuccess;
         return hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[bi] : c->render_done, 0);
     };
     const auto* s8 = static_cast<const uint8_t*>(src);
@@ -1510,6 +1607,83 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uin
     return RT_OK;
 }
 
+// Pinned host buffer of at least `bytes` (grown on demand).
+static int ensure_pinned(rt_ctx* c, void*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return RT_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(c, hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    cap = bytes;
+    return RT_OK;
+}
+
+// rt_render's copies after a sparse render: the row offsets and segment bits,
+// then the whole frame as the camera pass left it (every pixel without a chain is final; the
+// generations run meanwhile), then, once the render is done, the packed chain segments in row
+// ranges, each scattered into the frame by the host pool as soon as it has landed.
+static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, size_t pitch) {
+    const uint32_t rows = o->tile_h, tw = o->tile_w;
+    const uint32_t nseg = (tw + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
+    const size_t s_off = (rows + 1ull) * 4, s_bits = static_cast<size_t>(rows) * words * 4;
+    int rc = ensure_pinned(c, c->h_sp_meta, c->h_sp_meta_cap, s_off + s_bits);
+    if (rc != RT_OK) return rc;
+    auto* h_off = static_cast<uint32_t*>(c->h_sp_meta);
+    auto* h_bits = h_off + (rows + 1);
+    HIP_TRY(c, hipMemcpyAsync(h_off, c->d_sp_off, s_off, hipMemcpyDeviceToHost, c->copy_stream));
+    HIP_TRY(c, hipMemcpyAsync(h_bits, c->d_sp_bits, s_bits, hipMemcpyDeviceToHost, c->copy_stream));
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, rows, false)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(tw) * 3 * sizeof(float), rows, false)) != RT_OK)
+        return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->copy_stream));      // (the offsets and bits were queued first)
+    const uint64_t total = h_off[rows];
+    const size_t seg_b = 3 * kSegPx, seg_r = 3 * kSegPx * sizeof(float);
+    const size_t pk_b = out_bgr ? total * seg_b : 0, pk_r = out_rgb ? total * seg_r : 0;
+    if ((rc = ensure_pinned(c, c->h_sp_pk, c->h_sp_pk_cap, std::max<size_t>(1, pk_b + pk_r))) != RT_OK) return rc;
+    auto* hb = static_cast<uint8_t*>(c->h_sp_pk);
+    auto* hr = reinterpret_cast<float*>(hb + pk_b);
+    HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[0] : c->render_done, 0));
+    const int nr = static_cast<int>(std::min<uint32_t>(kMaxBands, rows));
+    auto r_at = [&](int j) { return static_cast<uint32_t>(static_cast<uint64_t>(rows) * j / nr); };
+    for (int j = 0; j < nr; ++j) {
+        if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
+        const uint64_t a = h_off[r_at(j)], e = h_off[r_at(j + 1)];
+        if (e > a && out_bgr)
+            HIP_TRY(c, hipMemcpyAsync(hb + a * seg_b, c->d_sp_bgr + a * seg_b, (e - a) * seg_b, hipMemcpyDeviceToHost, c->copy_stream));
+        if (e > a && out_rgb)
+            HIP_TRY(c, hipMemcpyAsync(hr + a * 3 * kSegPx, c->d_sp_rgb + a * 3 * kSegPx, (e - a) * seg_r, hipMemcpyDeviceToHost,
+                                      c->copy_stream));
+        HIP_TRY(c, hipEventRecord(c->sp_ev[j], c->copy_stream));
+    }
+    const size_t pad = pitch - 3ull * tw;
+    auto scatter_rows = [&](uint32_t r0, uint32_t r1) {
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint32_t* bits = h_bits + static_cast<size_t>(r) * words;
+            uint64_t i = h_off[r];
+            for (uint32_t w = 0; w < words; ++w)
+                for (uint32_t m = bits[w]; m; m &= m - 1, ++i) {
+                    const uint32_t x0 = (w * 32 + static_cast<uint32_t>(__builtin_ctz(m))) * kSegPx;
+                    const uint32_t n = std::min(kSegPx, tw - x0);
+                    if (out_bgr) {
+                        uint8_t* d = out_bgr + static_cast<size_t>(r) * pitch + 3ull * x0;
+                        std::memcpy(d, hb + i * seg_b, 3ull * n);
+                        if (x0 + n == tw && pad) std::memset(d + 3ull * n, 0, pad);   // BMP row padding
+                    }
+                    if (out_rgb) std::memcpy(out_rgb + (static_cast<size_t>(r) * tw + x0) * 3, hr + i * 3 * kSegPx, 12ull * n);
+                }
+        }
+    };
+    for (int j = 0; j < nr; ++j) {
+        HIP_TRY(c, hipEventSynchronize(c->sp_ev[j]));
+        const uint32_t ra = r_at(j), rb = r_at(j + 1);
+        const size_t parts = std::min<size_t>(HostCopyPool::kParts, rb - ra);
+        c->pool.run(parts, [&](size_t q) {
+            scatter_rows(ra + static_cast<uint32_t>((rb - ra) * q / parts), ra + static_cast<uint32_t>((rb - ra) * (q + 1) / parts));
+        });
+    }
+    return RT_OK;
+}
+
 static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
     uint32_t spp, band, stride, pitch;
     int rc = check_opts(c, o, spp, band, stride, pitch);
@@ -1536,12 +1710,18 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     // an earlier rt_render's copies (copy stream) must be done with d_rgb / d_bgr: they are, since
     // copy_to_host returns only once its last piece has been drained or synchronised
     c->want_bands = true;
+    c->want_sparse = c->t(kTuneSparseOut) != 0;
     rc = render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
     c->want_bands = false;
+    c->want_sparse = false;
     if (rc != RT_OK) return rc;
-    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, o->tile_h)) != RT_OK) return rc;
-    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(o->tile_w) * 3 * sizeof(float), o->tile_h)) != RT_OK)
-        return rc;
+    if (c->sparse_on) {
+        if ((rc = copy_sparse(c, o, out_rgb, out_bgr, pitch)) != RT_OK) return rc;
+    } else {
+        if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, o->tile_h)) != RT_OK) return rc;
+        if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(o->tile_w) * 3 * sizeof(float), o->tile_h)) != RT_OK)
+            return rc;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (stats) return rt_ctx_stats(c, stats);
     return RT_OK;

@@ -649,6 +649,9 @@ __device__ __forceinline__ void finish_nearest(const DevScene& sc, const FramePa
             set_terminal(b, p, end_colour(sc, end_obj), k);
         }
     }
+    if constexpr (kCam) {
+        if (b.mark && live) stn(&b.cmark()[p], static_cast<uint8_t>(shade ? 1 : 0));
+    }
     const uint32_t slot = lds_append(&counts[0], shade);
     const uint32_t chain = kCam ? static_cast<uint32_t>(obase) + slot : p;   // (slot valid when shade)
     if (kCam && shade && b.compose) stn(&b.pmap()[p], chain);
@@ -1259,6 +1262,89 @@ __global__ __launch_bounds__(kWfThreads) void wf_compose(DevScene sc, FrameParam
 // queue entry, and one shadow query per light per shade record; plus the
 // per-generation queue sizes.  One workgroup; atomics because chunks on
 // different streams may finish together.
+// Sparse host copies (rt_render, tuning sparse_out): after the
+// camera pass every pixel that starts no chain is final, so the host copies the
+// frame then, while the generations run; after the fold only the 16-pixel row
+// segments that hold a chain pixel are packed, in row order, and copied.
+// wf_chain_segs: one wave per chunk row: segbits (bit s of the row's words:
+// segment s holds a chain pixel) and the row's segment count.
+__global__ __launch_bounds__(256) void wf_chain_segs(FrameParams fp, WfBufs b, uint32_t* segbits, uint32_t* rowcnt) {
+    const uint32_t row = (blockIdx.x * 256u + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+    if (row >= fp.rows) return;
+    const uint32_t nseg = (fp.tile_w + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
+    const uint8_t* m = b.cmark() + static_cast<size_t>(row) * fp.tile_w;
+    uint32_t cnt = 0;
+    for (uint32_t s0 = 0; s0 < nseg; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        bool any = false;
+        if (s < nseg) {
+            const uint32_t x1 = min(s * kSegPx + kSegPx, fp.tile_w);
+            for (uint32_t x = s * kSegPx; x < x1; ++x) any |= m[x] != 0;
+        }
+        const unsigned long long bal = __ballot(any);
+        cnt += static_cast<uint32_t>(__popcll(bal));
+        if (lane == 0) segbits[static_cast<size_t>(row) * words + s0 / 32] = static_cast<uint32_t>(bal);
+        if (lane == 32 && s0 / 32 + 1 < words) segbits[static_cast<size_t>(row) * words + s0 / 32 + 1] = static_cast<uint32_t>(bal >> 32);
+    }
+    if (lane == 0) rowcnt[row] = cnt;
+}
+
+// rowoff[r] = segments of rows < r (exclusive scan, rowoff[rows] = total); one workgroup.
+__global__ __launch_bounds__(1024) void wf_row_scan(const uint32_t* rowcnt, uint32_t rows, uint32_t* rowoff) {
+    __shared__ uint32_t s_wave[16];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t per = (rows + 1023u) / 1024u, a = t * per, e = min(a + per, rows);
+    uint32_t sum = 0;
+    for (uint32_t i = a; i < e; ++i) sum += rowcnt[i];
+    uint32_t inc = sum;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(inc, off, 64);
+        if (lane >= static_cast<uint32_t>(off)) inc += o;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t w = 0; w < wave; ++w) run += s_wave[w];
+    for (uint32_t i = a; i < e; ++i) { rowoff[i] = run; run += rowcnt[i]; }
+    if (t == 1023) rowoff[rows] = run;
+}
+
+// After the fold: the flagged segments' BGR (48 B) and f32 RGB (192 B) in row
+// order, segment i of the frame at pk_bgr + 48 i / pk_rgb + 48 i; one wave per row.
+__global__ __launch_bounds__(256) void wf_chain_pack(FrameParams fp, const uint32_t* segbits, const uint32_t* rowoff,
+                                                     uint8_t* pk_bgr, float* pk_rgb) {
+    const uint32_t row = (blockIdx.x * 256u + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+    if (row >= fp.rows) return;
+    const uint32_t nseg = (fp.tile_w + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
+    const size_t frow = fp.row0 + row;
+    uint32_t base = rowoff[row];
+    for (uint32_t s0 = 0; s0 < nseg; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        const uint32_t wd = s < nseg ? segbits[static_cast<size_t>(row) * words + s / 32] : 0u;
+        const bool flag = (wd >> (s % 32)) & 1u;
+        const unsigned long long bal = __ballot(flag);
+        const uint32_t rank = base + static_cast<uint32_t>(__popcll(bal & ((1ull << lane) - 1ull)));
+        base += static_cast<uint32_t>(__popcll(bal));
+        if (!flag) continue;
+        const uint32_t x0 = s * kSegPx, n = min(kSegPx, fp.tile_w - x0);
+        if (fp.out_bgr) {
+            const uint8_t* src = fp.out_bgr + frow * fp.bgr_pitch + 3u * x0;
+            uint8_t* dst = pk_bgr + static_cast<size_t>(rank) * (3 * kSegPx);
+            if (n == kSegPx && fp.bgr_pitch % 4u == 0) {
+                for (int k = 0; k < 12; ++k)
+                    reinterpret_cast<uint32_t*>(dst)[k] = reinterpret_cast<const uint32_t*>(src)[k];
+            } else {
+                for (uint32_t k = 0; k < 3 * n; ++k) dst[k] = src[k];
+            }
+        }
+        if (fp.out_rgb) {
+            const float* src = fp.out_rgb + (frow * fp.tile_w + x0) * 3;
+            float* dst = pk_rgb + static_cast<size_t>(rank) * (3 * kSegPx);
+            for (uint32_t k = 0; k < 3 * n; ++k) dst[k] = src[k];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kWfThreads) void wf_tally(FrameParams fp, WfBufs b, int n_lights, int generations) {
     __shared__ unsigned long long s_sum[2 * kMaxGenerations];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1415,6 +1501,12 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         }
 #undef RT_GEN
         if (e != hipSuccess) return e;
+        if (k == 0 && ws.sp_s) {               // every pixel without a chain is final now
+            if ((e = hipEventRecord(ws.sp_cam, ws.a)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ws.sp_s, ws.sp_cam, 0)) != hipSuccess) return e;
+            if ((e = launch_chain_segs(fp, b, ws.sp_bits, ws.sp_cnt, ws.sp_off, ws.sp_s)) != hipSuccess) return e;
+            if ((e = hipEventRecord(ws.sp_ready, ws.sp_s)) != hipSuccess) return e;
+        }
         if (mark && k == mark_gen) {
             e = hipEventRecord(mark, ws.a);
             if (e != hipSuccess) return e;
@@ -1440,8 +1532,26 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         hipLaunchKernelGGL(wf_compose, dim3(std::max(1u, wgs)), dim3(kWfThreads), 0, ws.a, sc, fp, b);
         if (ws.ma && (e = ws.ma->mark(ws.a, kKfCompose)) != hipSuccess) return e;
     }
+    if (ws.sp_s) {                           // the chain pixels' segments, packed in row order
+        if ((e = hipStreamWaitEvent(ws.a, ws.sp_ready, 0)) != hipSuccess) return e;
+        if ((e = launch_chain_pack(fp, ws.sp_bits, ws.sp_off, ws.sp_bgr, ws.sp_rgb, ws.a)) != hipSuccess) return e;
+    }
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
     if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, ws.a)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_segs(const FrameParams& fp, const WfBufs& b, uint32_t* segbits, uint32_t* rowcnt, uint32_t* rowoff,
+                             hipStream_t s) {
+    const dim3 grid((fp.rows + 3u) / 4u);
+    hipLaunchKernelGGL(wf_chain_segs, grid, dim3(256), 0, s, fp, b, segbits, rowcnt);
+    hipLaunchKernelGGL(wf_row_scan, dim3(1), dim3(1024), 0, s, rowcnt, fp.rows, rowoff);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_pack(const FrameParams& fp, const uint32_t* segbits, const uint32_t* rowoff, uint8_t* pk_bgr,
+                             float* pk_rgb, hipStream_t s) {
+    hipLaunchKernelGGL(wf_chain_pack, dim3((fp.rows + 3u) / 4u), dim3(256), 0, s, fp, segbits, rowoff, pk_bgr, pk_rgb);
     return hipGetLastError();
 }
 

@@ -744,6 +744,34 @@ def test_host_chunks_overlap_copies_bit_identically(gpu_ctx):
         assert got[2].chunks == kv["host_chunks"] and base[2].chunks == 1, kv
 
 
+@pytest.mark.parametrize("scene", ["config3", "config2", "fresnel"])
+def test_sparse_host_copies_bit_identical(gpu_ctx, scene):
+    """rt_render into host memory with tuning sparse_out (rt_device.cpp
+    copy_sparse: the frame copied after the camera pass, then the packed
+    segments of the chain pixels scattered into it): every byte and colour as
+    the plain copy, into buffers holding garbage, for widths around the
+    16-pixel segment, padded rows, BGR only, RGB only, with and without the
+    fused tail.  (sparse_out is the default: every other rt_render parity test
+    runs it against the oracle too.)"""
+    for w, h in [(197, 64), (64, 40), (33, 17), (1, 9)]:
+        spec = {"config3": scenes.config3, "config2": scenes.config2, "fresnel": scenes.config2_fresnel}[scene](w, h)
+        gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+        for pitch in (0, ((3 * w + 3) & ~3) + 8):
+            o = lr.render_opts(w, h, max_depth=spec.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT, bgr_pitch=pitch)
+            with _with_tuning(gpu_ctx, sparse_out=0):
+                base = gpu_ctx.render(o)
+            for kv in [dict(sparse_out=1), dict(sparse_out=1, tail_fuse=0)]:
+                for outs in [(True, True), (False, True), (True, False)]:
+                    rgb = np.full_like(base[0], np.nan) if outs[0] else None
+                    bgr = np.full_like(base[1], 0xAB) if outs[1] else None
+                    with _with_tuning(gpu_ctx, **kv):
+                        got = gpu_ctx.render(o, out=(rgb, bgr))
+                    if outs[1]:
+                        assert np.array_equal(got[1], base[1]), (w, h, pitch, kv, outs)
+                    if outs[0]:
+                        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), (w, h, pitch, kv, outs)
+
+
 def test_default_spp_is_the_scenes_antialias(gpu_ctx):
     """rt_render_opts.spp = 0 (the default options) renders with the uploaded
     scene's Options.antialias (scene.rs:191-198)."""

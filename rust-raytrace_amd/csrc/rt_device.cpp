@@ -299,7 +299,8 @@ struct rt_ctx {
     void* h_sp_pk = nullptr;
     size_t h_sp_pk_cap = 0;
     hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
-    hipEvent_t sp_ev[kMaxBands] = {};
+    static constexpr int kSpRanges = 16;   // row ranges of the packed copy, each scattered as it lands
+    hipEvent_t sp_ev[kSpRanges] = {};
     int64_t tune[kTuneCount];
     std::string err;
     rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
@@ -1626,6 +1627,9 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     const uint32_t rows = o->tile_h, tw = o->tile_w;
     const uint32_t nseg = (tw + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
     const size_t s_off = (rows + 1ull) * 4, s_bits = static_cast<size_t>(rows) * words * 4;
+    using Clock = std::chrono::steady_clock;
+    const auto t0 = Clock::now();
+    auto us = [&] { return std::chrono::duration<double, std::micro>(Clock::now() - t0).count(); };
     int rc = ensure_pinned(c, c->h_sp_meta, c->h_sp_meta_cap, s_off + s_bits);
     if (rc != RT_OK) return rc;
     auto* h_off = static_cast<uint32_t*>(c->h_sp_meta);
@@ -1636,6 +1640,7 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(tw) * 3 * sizeof(float), rows, false)) != RT_OK)
         return rc;
     HIP_TRY(c, hipStreamSynchronize(c->copy_stream));      // (the offsets and bits were queued first)
+    const double t_frame = us();
     const uint64_t total = h_off[rows];
     const size_t seg_b = 3 * kSegPx, seg_r = 3 * kSegPx * sizeof(float);
     const size_t pk_b = out_bgr ? total * seg_b : 0, pk_r = out_rgb ? total * seg_r : 0;
@@ -1643,7 +1648,7 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     auto* hb = static_cast<uint8_t*>(c->h_sp_pk);
     auto* hr = reinterpret_cast<float*>(hb + pk_b);
     HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[0] : c->render_done, 0));
-    const int nr = static_cast<int>(std::min<uint32_t>(kMaxBands, rows));
+    const int nr = static_cast<int>(std::min<uint32_t>(rt_ctx::kSpRanges, rows));
     auto r_at = [&](int j) { return static_cast<uint32_t>(static_cast<uint64_t>(rows) * j / nr); };
     for (int j = 0; j < nr; ++j) {
         if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
@@ -1673,14 +1678,21 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
                 }
         }
     };
+    // each range scattered by the pool as soon as it has landed (the later ones still in flight)
+    double t_first = 0.0;
     for (int j = 0; j < nr; ++j) {
         HIP_TRY(c, hipEventSynchronize(c->sp_ev[j]));
+        if (j == 0) t_first = us();
         const uint32_t ra = r_at(j), rb = r_at(j + 1);
         const size_t parts = std::min<size_t>(HostCopyPool::kParts, rb - ra);
         c->pool.run(parts, [&](size_t q) {
             scatter_rows(ra + static_cast<uint32_t>((rb - ra) * q / parts), ra + static_cast<uint32_t>((rb - ra) * (q + 1) / parts));
         });
     }
+    if (c->t(kTuneVerbose))
+        std::fprintf(stderr, "rtamd: sparse copy: %llu of %llu segments; frame copied at %.0f us, first packed range at %.0f, "
+                     "done at %.0f\n", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nseg) * rows,
+                     t_frame, t_first, us());
     return RT_OK;
 }
 

@@ -1331,7 +1331,8 @@ __global__ __launch_bounds__(256) void wf_chain_pack(FrameParams fp, const uint3
             const uint8_t* src = fp.out_bgr + frow * fp.bgr_pitch + 3u * x0;
             uint8_t* dst = pk_bgr + static_cast<size_t>(rank) * (3 * kSegPx);
             if (n == kSegPx && fp.bgr_pitch % 4u == 0) {
-                for (int k = 0; k < 12; ++k)
+                static_assert(kSegPx % 4 == 0, "segments of whole dwords");
+                for (uint32_t k = 0; k < 3 * kSegPx / 4; ++k)
                     reinterpret_cast<uint32_t*>(dst)[k] = reinterpret_cast<const uint32_t*>(src)[k];
             } else {
                 for (uint32_t k = 0; k < 3 * n; ++k) dst[k] = src[k];

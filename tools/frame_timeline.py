@@ -1,6 +1,8 @@
-"""Per-launch timeline of the last uninstrumented wavefront frame of a
-rocprofv3 --kernel-trace run (directory argument): start (us from the frame's
-first launch), duration (us), stream, kernel; up to the frame-end fold."""
+"""Per-launch timeline of the last timed-loop wavefront frame of a rocprofv3
+--kernel-trace run of bench.py (directory argument): the last uninstrumented
+frame before the RT_COUNT_WORK render (the PCIe-inclusive rt_render calls come
+after it); start (us from the frame's first launch), duration (us), stream,
+kernel; up to the frame-end fold."""
 import csv
 import sys
 
@@ -14,7 +16,9 @@ def targs(name):
 
 
 # generation 0 of an uninstrumented frame: wf_nearest<src, kCam = true, kCount = false, ...>
-starts = [i for i, t in enumerate(tr) if "wf_nearest<" in t["Kernel_Name"] and targs(t["Kernel_Name"])[1:3] == ["true", "false"]]
+gen0 = [i for i, t in enumerate(tr) if "wf_nearest<" in t["Kernel_Name"] and targs(t["Kernel_Name"])[1:2] == ["true"]]
+inst = next((i for i in gen0 if targs(tr[i]["Kernel_Name"])[2] == "true"), len(tr))
+starts = [i for i in gen0 if i < inst]
 i0 = starts[-1]
 t0 = int(tr[i0]["Start_Timestamp"])
 for j, t in enumerate(tr[i0:]):

@@ -1,8 +1,9 @@
 """HBM bytes per render from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
 Each pass ran `bench.py --steps S --warmup W` (W + S uninstrumented renders,
-then one RT_COUNT_WORK render).  Frames are split at the generation-0
-wf_nearest launch; the last uninstrumented frame of each pass is used.
+then one RT_COUNT_WORK render, then the PCIe-inclusive rt_render calls).
+Frames are split at the generation-0 wf_nearest launch; the last frame before
+the RT_COUNT_WORK render (a timed-loop frame) is used.
 MI355X_MICROARCH.md ("HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, so it is doubled.
 
@@ -42,7 +43,10 @@ def frames(path, counter):
         if cur is None or "wf_" not in name:
             continue
         cur["kernels"][family(name)] += float(r["Counter_Value"]) * 1024.0
-    return [f for f in out if not f["instrumented"]]
+    # the timed loop's frames: those before the RT_COUNT_WORK render (the PCIe-inclusive
+    # rt_render calls that follow it run the sparse host copies' extra kernels)
+    first_inst = next((i for i, f in enumerate(out) if f["instrumented"]), len(out))
+    return [f for f in out[:first_inst] if not f["instrumented"]]
 
 
 def main():
@@ -79,7 +83,7 @@ def main():
                 "per_kernel_family": kernels,
                 "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, --kernel-trace only; "
                           "KiB -> bytes; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section); "
-                          "last uninstrumented frame of each pass" +
+                          "last timed-loop frame of each pass (before the RT_COUNT_WORK render)" +
                           (f" ({chunks} wavefront chunks summed)" if chunks > 1 else "")}
     json.dump(doc, open(out_path, "w"), indent=1)
     print(json.dumps(doc[key], indent=1))

@@ -30,9 +30,10 @@ BASELINE config 4's "image tiled across GPUs"; per-rank projection on one GPU:
 weak (opt-in) renders the same scene and view at sqrt(N) x the resolution,
 every rank a 4096^2-pixel share; its line names that larger frame in
 `metric`, never the headline's.
-After the timed region every rank copies its bands into ONE shared page-locked
-host frame (the host gather of SURVEY §8(e)), timed and reported as
-`host_gather`.  --config c4 / c5 select the larger configs of BASELINE.json;
+After the timed region every rank renders its bands again, K frames, with
+rt_render straight into ONE shared page-locked host frame (the host gather of
+SURVEY §8(e), RT_OUT_FRAME_ROWS: the copies overlap the render), reported as
+`host_frame` beside the device-only value.  --config c4 / c5 select the larger configs of BASELINE.json;
 --config c1 the reference's own scene (test_scene.txt: IndirectPhong Cornell
 box, 1024 random AA samples, 256x256, depth 1) on the path kernel.
 
@@ -287,13 +288,15 @@ class SharedFrame:
                 pass
 
 
-def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
-    """Every rank copies its bands of the frame (f32 RGB and BGR) into one shared
-    page-locked host frame; returns (best ms of 3, pinned) measured between barriers."""
-    import torch
-    nb = H // BAND
+def frame_gather(dist, world, rank, ctx, lr, W, H, pitch, common, steps, red_dev):
+    """The multi-GPU frame end to end: every rank rt_render's its row bands
+    straight into ONE shared page-locked host frame (RT_OUT_FRAME_ROWS: the library copies
+    each part of its tile as the render finishes it, so the gather overlaps the render).
+    Per output set: rt_ctx_reserve, two untimed frames, then K frames back to back on every
+    rank between barriers; ms per frame = the slowest rank's time / K."""
+    import numpy as np
     rgb_bytes, bgr_bytes = H * W * 12, H * pitch
-    name = [f"rtbench_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}"]
+    name = [f"rtframe_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}"]
     if world > 1:
         dist.broadcast_object_list(name, src=0)
     fr = SharedFrame(name[0], rgb_bytes + bgr_bytes, create=True) if rank == 0 else None
@@ -301,36 +304,37 @@ def host_gather(dist, world, rank, outs_local, W, H, pitch, dev):
         dist.barrier()
     if fr is None:
         fr = SharedFrame(name[0], rgb_bytes + bgr_bytes, create=False)
+    out = {"pinned": bool(fr.pinned)}
     try:
-        host = torch.from_numpy(fr.arr)
-        rgb_h = host[:rgb_bytes].view(nb, BAND * W * 12)[rank::world]
-        bgr_h = host[rgb_bytes:].view(nb, BAND * pitch)[rank::world]
-        out_rgb, out_bgr = outs_local
-        src_rgb = out_rgb.view(torch.uint8).reshape(-1, BAND * W * 12)
-        src_bgr = out_bgr.reshape(-1, BAND * pitch)
-        best = None
-        for _ in range(3):
+        rgb = fr.arr[:rgb_bytes].view(np.float32).reshape(H, W, 3)
+        bgr = fr.arr[rgb_bytes:].reshape(H, pitch)
+        for key, flags, outs in (("bgr_only", lr.RT_OUT_BGR_U8, (None, bgr)),
+                                 ("rgb_and_bgr", lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8, (rgb, bgr))):
+            o = lr.render_opts(W, H, flags=flags | lr.RT_OUT_FRAME_ROWS, bgr_pitch=pitch, **common)
+            ctx.reserve(o, host=True)
+            for _ in range(2):
+                ctx.render(o, out=outs, stats=False)
             if world > 1:
                 dist.barrier()
-            torch.cuda.synchronize(dev)
             t0 = time.perf_counter()
-            rgb_h.copy_(src_rgb)
-            bgr_h.copy_(src_bgr)
-            torch.cuda.synchronize(dev)
+            for _ in range(steps):
+                ctx.render(o, out=outs, stats=False)
+            ms = (time.perf_counter() - t0) * 1e3 / steps
             if world > 1:
-                dist.barrier()
-            ms = (time.perf_counter() - t0) * 1e3
-            best = ms if best is None else min(best, ms)
-        pinned = fr.pinned
-        del host, rgb_h, bgr_h
+                import torch
+                t = torch.tensor([ms], dtype=torch.float64, device=red_dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                ms = t.item()
+            out[key] = ms
+        del rgb, bgr
     finally:
         if world > 1:
             dist.barrier()
         fr.close(unlink=(rank == 0))
-    return best, pinned
+    return out
 
 
-CONFIGS = {"c1": (256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
+CONFIGS = {"c1":(256, 0, 1, 1, 1.0), "c3": (4096, 1000, 8, 3, 1.0), "c4": (8192, 10000, 8, 4, 10.0 ** (1 / 3)),
            "c5": (16384, 100000, 16, 5, 100.0 ** (1 / 3))}       # side, spheres, depth, seed, box scale (scenes.config*)
 HEADLINE_METRIC = "Mrays/sec at 4096x4096, 1000 spheres, depth 8; fraction of HBM roofline"   # BASELINE.json
 
@@ -447,7 +451,9 @@ def main():
     assert H % BAND == 0, "bench frames are whole bands"
     scene = lr.Scene.deserialize(spec.to_text())
     F = max(1, args.inflight)
+    t0x = time.perf_counter()
     ctxs = [lr.Context(local, tuning="env") for _ in range(F)]
+    create_ms = (time.perf_counter() - t0x) * 1e3 / F
     upload_ms = []
     for c in ctxs:
         # rt_scene_upload: host BVH + light-view grid builds + the blob's H2D copy, paid once per scene
@@ -484,9 +490,15 @@ def main():
         f = i % F
         ctxs[f].render_device(o, outs[f][0].data_ptr(), outs[f][1].data_ptr(), streams[f].cuda_stream)
 
-    # the cold first frame (a process that renders one frame, as main.rs does, pays it): the
-    # working set's allocation, the first launch of every kernel (code object load) and the
-    # scratch setup of the hardware queues, against the second (warm) frame
+    # rt_ctx_reserve (outside the timed region, like the upload): the schedule's streams and hardware
+    # queues, the working set and the queues' scratch, so that the first frame runs warm
+    reserve_ms = []
+    for c in ctxs:
+        t0r = time.perf_counter()
+        c.reserve(opts)
+        reserve_ms.append((time.perf_counter() - t0r) * 1e3)
+    # the first two frames after it, against each other: what a process that renders one frame (as
+    # main.rs does) pays for its render once ctx_create, the upload and the reserve are done
     cold_ms = []
     for i in range(max(args.warmup, F)):
         t0c = time.perf_counter()
@@ -542,10 +554,11 @@ def main():
     except lr.RtError:
         gen_q, gen_s = [], []
 
-    # host gather: every rank's bands into one shared page-locked frame
-    gather_ms, gather_pinned = None, None
-    if not args.no_gather and band_world == world:
-        gather_ms, gather_pinned = host_gather(dist, world, rank, outs[0], W, H, pitch, dev)
+    # the frame end to end: every rank's rt_render of its bands straight into one
+    # shared page-locked host frame, the gather overlapping the render (RT_OUT_FRAME_ROWS)
+    hframe = None
+    if not args.no_gather and not path_cfg:
+        hframe = frame_gather(dist, world, rank, ctx, lr, W, H, pitch, common, args.steps, red_dev)
 
     # PCIe-inclusive rate: rt_render into reused pageable host buffers, kernels + D2H.
     # Reported beside `value`, never as it.
@@ -568,14 +581,13 @@ def main():
 
     n_gpus = distinct_devices()
     t = torch.tensor([elapsed, float(local_rays), avg_kernel_ms, float(wst.sphere_tests), float(wst.box_tests),
-                      float(local_traced), gather_ms or 0.0], dtype=torch.float64, device=red_dev)
+                      float(local_traced)], dtype=torch.float64, device=red_dev)
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, avg_kernel_ms = mx[0].item(), mx[2].item()
-        gather_ms = mx[6].item() if gather_ms is not None else None
         total_rays, total_traced = int(sm[1].item()), int(sm[5].item())
         sphere_tests, box_tests = int(sm[3].item()), int(sm[4].item())
     else:
@@ -656,22 +668,28 @@ def main():
         }
         if len(cold_ms) == 2:
             line["first_frame_ms"] = {"first": round(cold_ms[0], 3), "second": round(cold_ms[1], 3),
-                                      "note": "wall clock of the first two renders after the upload (synchronised): "
-                                              "the first pays the working set's hipMalloc, each kernel's first "
-                                              "launch and the queues' scratch setup"}
+                                      "note": "wall clock of the first two renders after rt_scene_upload and "
+                                              "rt_ctx_reserve (synchronised; reserve_ms: the working set's hipMalloc, "
+                                              "the streams' hardware queues and scratch; ctx_create_ms: the context "
+                                              "and the kernels' code objects)"}
+            line["first_frame_ms"]["reserve_ms"] = round(reserve_ms[0], 3)
+            line["first_frame_ms"]["ctx_create_ms"] = round(create_ms, 3)
         line["upload_ms"] = {"first": round(upload_ms[0], 3), "repeat": round(min(upload_ms[1:]), 3),
                              "note": "rt_scene_upload once per scene, outside the timed region: host SAH BVH + "
                                      "4-wide tree + light-view grids + camera view, then one H2D copy of the blob"}
-        if gather_ms is not None:
-            line["host_gather"] = {"ms": round(gather_ms, 3), "pinned": bool(gather_pinned),
-                                   "bytes": H * W * 15,
-                                   "note": "after the timed region: every rank copies its row bands (f32 RGB + "
-                                           "BGR) into one shared page-locked host frame; max over ranks"}
-            e2e = ms_per_step + gather_ms
-            line["render_plus_gather"] = {
-                "ms_per_frame": round(e2e, 3), "value": round(total_traced / (e2e * 1e-3) / 1e6, 3), "unit": "Mrays/s",
-                "note": "the frame rendered, then its bands gathered into the host frame, one after the other (a "
-                        "stream of frames could overlap frame i's gather with frame i+1's render)"}
+        if hframe is not None:
+            def hf(ms):
+                return {"ms_per_frame": round(ms, 3), "value": round(total_traced / (ms * 1e-3) / 1e6, 3),
+                        "unit": "Mrays/s", "vs_device_only": round(ms / ms_per_step, 3)}
+            line["host_frame"] = {
+                "bgr_only": hf(hframe["bgr_only"]), "rgb_and_bgr": hf(hframe["rgb_and_bgr"]),
+                "pinned": hframe["pinned"], "bytes_per_frame": {"bgr_only": H * W * 3, "rgb_and_bgr": H * W * 15},
+                "device_only_ms_per_frame": round(ms_per_step, 4),
+                "note": ("every rank rt_render's its row bands straight into ONE shared page-locked host frame "
+                         "(RT_OUT_FRAME_ROWS: the gather of SURVEY 8(e) overlapping the render: the frame copied after "
+                         "the camera pass, then the packed segments of the chain pixels), K frames back to back; "
+                         "the slowest rank's ms per frame" +
+                         (f"; here rank 0's bands of a {band_world}-rank frame only" if band_world > world else ""))}
         if host:
             line["pcie_inclusive"] = {
                 "bgr_only": {"ms_per_frame": round(host["bgr"], 3),

@@ -52,11 +52,18 @@
 extern "C" {
 #endif
 
-/* 4: rt_abi_version() added; rt_kernel_family gained RT_KF_TAIL (RT_KF_COUNT 8);
- * rt_stats unchanged (80 B, `chunks` since ABI 3).  Later additions of functions
- * only (rt_qtree_nodes) keep the version.  A caller checks rt_abi_version() ==
- * RT_ABI_VERSION of the header it was built against before passing any struct. */
-#define RT_ABI_VERSION 4
+/* 5: rt_out_flags gained RT_OUT_FRAME_ROWS (rt_render writes a banded tile
+ * straight into its rows of a whole-frame host buffer); rt_ctx_reserve added;
+ * rt_kernel_family index 6 is RT_KF_COMPOSE (earlier ABI-4 builds named it
+ * RT_KF_SHADOW); the tuning keys fuse, lists,
+ * lists0, fuse_from, prefix4_kb, cam_prefix_kb, tail_from, tail_max,
+ * eager_fold, fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs and
+ * shade_wgs (variants measured slower and removed) are gone:
+ * rt_ctx_set_tuning answers RT_E_INVALID for them.  rt_stats unchanged (80 B).
+ * 4: rt_abi_version() added; RT_KF_TAIL (RT_KF_COUNT 8).  A caller checks
+ * rt_abi_version() == RT_ABI_VERSION of the header it was built against before
+ * passing any struct; any change of a struct, enum value or tuning key bumps it. */
+#define RT_ABI_VERSION 5
 
 enum rt_status {
     RT_OK = 0,
@@ -169,7 +176,7 @@ int rt_view_grid_candidates(const rt_scene* scene, int resolution, const double*
  * floats; sphere_first / sphere_count: per node and slot the leaf's spheres in
  * leaf order (-1 / 0 for an inner child or unused slot).  info[0..2] = nodes (0:
  * not representable, the device keeps the other trees), the traversal stack's
- * worst case, the leaf size.  Replaces nothing in the reference (scene.rs:247-249
+ * worst case, the leaf size; cap_nodes 0 is a size query (info only).  Replaces nothing in the reference (scene.rs:247-249
  * scans every object); tests decode the nodes and check every box contains its
  * f32 box. */
 int rt_qtree_nodes(const rt_scene* scene, int leaf_max, void* nodes, float* boxes, int32_t* sphere_first,
@@ -208,7 +215,14 @@ enum rt_out_flags {
     RT_OUT_RGB_F32 = 1,
     RT_OUT_BGR_U8 = 2,
     RT_COUNT_WORK = 4,         /* also count box / sphere tests (instrumented kernels; wavefront only) */
-    RT_TIME_KERNELS = 8        /* record a timing event after every launch (wavefront, one stream) */
+    RT_TIME_KERNELS = 8,       /* record a timing event after every launch (wavefront, one stream) */
+    RT_OUT_FRAME_ROWS = 16     /* rt_render only: out_rgb / out_bgr hold the WHOLE frame (height rows; f32
+                                  rows of 3*width floats, BGR rows of bgr_pitch bytes, 0 -> 3*width) and the
+                                  tile's pixel (x, local row j) lands in column x0 + x of its frame row
+                                  y0 + ((j/band)*band_stride + band_phase)*band + j%band; nothing else of
+                                  the buffers is written.  The multi-GPU host gather (main.rs:45-58 split
+                                  over devices): each context renders its row bands straight into one
+                                  shared page-locked frame, the copies overlapping its render. */
 };
 enum rt_algo {
     RT_ALGO_AUTO = 0,
@@ -268,6 +282,16 @@ int rt_render(rt_ctx* ctx, const rt_render_opts* opts, float* out_rgb, uint8_t* 
  * renders into caller-owned DEVICE buffers.  Statistics of the most recent
  * render are read with rt_ctx_stats (which synchronises). */
 int rt_render_device(rt_ctx* ctx, const rt_render_opts* opts, void* d_rgb, void* d_bgr, void* stream);
+/* Prepare the context for renders with these options, synchronously and
+ * without rendering: the schedule's streams and hardware queues, its working
+ * set (sized exactly as the render sizes it), rt_render's device frame and
+ * sparse-copy buffers (host = 1) and the kernels' code objects.  A later
+ * rt_render / rt_render_device with the same options (or smaller ones) then
+ * allocates nothing: a process that renders one frame (main.rs:13-60) calls
+ * it after rt_scene_upload, e.g. while it parses or opens its output.  Needs
+ * an uploaded scene (the schedule depends on it); RT_E_NOMEM if the working
+ * set does not fit even as the smallest chunks. */
+int rt_ctx_reserve(rt_ctx* ctx, const rt_render_opts* opts, int host);
 int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
 /* Diagnostic (device): the sphere test's division t = x / (2a) (shapes.rs:68,75)
  * computed as the device computes it (the per-ray reciprocal of 2a finished with

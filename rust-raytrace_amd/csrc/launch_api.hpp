@@ -97,6 +97,11 @@ hipError_t launch_chain_segs(const FrameParams& fp, const WfBufs& b, uint32_t* s
                              hipStream_t s);
 hipError_t launch_chain_pack(const FrameParams& fp, const uint32_t* segbits, const uint32_t* rowoff, uint8_t* pk_bgr,
                              float* pk_rgb, hipStream_t s);
+// rt_ctx_reserve: a no-op launch of `workgroups` 1024-thread workgroups with private memory
+// on stream s (loads trace_kernel.hip's code object, sets up the stream's queue and scratch);
+// launch_path_warmup loads path_kernel.hip's.
+hipError_t launch_warmup(uint32_t workgroups, hipStream_t s);
+hipError_t launch_path_warmup(hipStream_t s);
 // Diagnostic: div_a2(x, sphere_k(a)) and x / (2a) on the device (rt_div_a2_check).
 hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s);
 

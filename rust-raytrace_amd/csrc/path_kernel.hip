@@ -460,4 +460,14 @@ hipError_t launch_path(const DevScene& sc, const FrameParams& fp, const PathStac
     return hipGetLastError();
 }
 
+// rt_ctx_reserve: the first launch of any kernel of this file loads its code object.
+__global__ void path_warm(uint32_t* sink) {
+    if (sink && threadIdx.x == 0) sink[blockIdx.x] = 0u;
+}
+
+hipError_t launch_path_warmup(hipStream_t s) {
+    hipLaunchKernelGGL(path_warm, dim3(1), dim3(64), 0, s, nullptr);
+    return hipGetLastError();
+}
+
 }  // namespace rtamd

@@ -105,44 +105,33 @@ int main(int argc, char** argv) {
             if ((rc[g] = rt_ctx_create(g, &ctx)) != RT_OK) { errs[g] = rt_last_error(nullptr); return; }
             if ((rc[g] = rt_scene_upload(ctx, scene)) != RT_OK) { errs[g] = rt_last_error(ctx); rt_ctx_destroy(ctx); return; }
             // rows of this device: bands g, g+G, g+2G, ...
-            const uint32_t nb = (H + band - 1) / band;
-            uint32_t my_rows = 0;
-            for (uint32_t b = g; b < nb; b += G) my_rows += std::min(band, H - b * band);
             // full bands only go through the banded mapping; a ragged last band is rendered separately
             const uint32_t full_bands = H / band;
             uint32_t my_full = 0;
             for (uint32_t b = g; b < full_bands; b += G) ++my_full;
-            std::vector<uint8_t> local(static_cast<size_t>(pitch) * my_rows);
+            // every device writes its bands straight into their rows of the shared frame (RT_OUT_FRAME_ROWS:
+            // the library's copies of one band overlap the render of the others); the bands are disjoint rows
             rt_render_opts o;
             rt_render_opts_default(&o, W, H);
             o.max_depth = a.max_depth; o.spp = spp; o.algo = a.algo; o.jitter = a.jitter; o.seed = a.seed;
-            o.flags = RT_OUT_BGR_U8; o.bgr_pitch = pitch;
+            o.flags = RT_OUT_BGR_U8 | RT_OUT_FRAME_ROWS; o.bgr_pitch = pitch;
             o.band = band; o.band_stride = G; o.band_phase = g; o.tile_h = my_full * band;
-            if (o.tile_h && (rc[g] = rt_render(ctx, &o, nullptr, local.data(), &st[g])) != RT_OK) {
+            if (o.tile_h && ((rc[g] = rt_ctx_reserve(ctx, &o, 1)) != RT_OK ||
+                             (rc[g] = rt_render(ctx, &o, nullptr, frame.data(), &st[g])) != RT_OK)) {
                 errs[g] = rt_last_error(ctx); rt_ctx_destroy(ctx); return;
             }
-            uint32_t tail_rows = 0;
-            if (H % band && full_bands % G == static_cast<uint32_t>(g)) {
+            if (H % band && full_bands % G == static_cast<uint32_t>(g)) {   // the ragged last band
                 rt_render_opts t;
                 rt_render_opts_default(&t, W, H);
                 t.max_depth = a.max_depth; t.spp = spp; t.algo = a.algo; t.jitter = a.jitter; t.seed = a.seed;
-                t.flags = RT_OUT_BGR_U8; t.bgr_pitch = pitch;
+                t.flags = RT_OUT_BGR_U8 | RT_OUT_FRAME_ROWS; t.bgr_pitch = pitch;
                 t.y0 = full_bands * band; t.tile_h = H % band;
                 rt_stats ts{};
-                if ((rc[g] = rt_render(ctx, &t, nullptr, local.data() + static_cast<size_t>(o.tile_h) * pitch, &ts)) != RT_OK) {
+                if ((rc[g] = rt_render(ctx, &t, nullptr, frame.data(), &ts)) != RT_OK) {
                     errs[g] = rt_last_error(ctx); rt_ctx_destroy(ctx); return;
                 }
                 st[g].rays += ts.rays; st[g].shadow_rays += ts.shadow_rays; st[g].kernel_ms += ts.kernel_ms;
-                tail_rows = t.tile_h;
             }
-            // host gather: local row j -> frame row
-            for (uint32_t j = 0; j < o.tile_h; ++j) {
-                uint32_t y = ((j / band) * G + g) * band + j % band;
-                std::memcpy(&frame[static_cast<size_t>(y) * pitch], &local[static_cast<size_t>(j) * pitch], pitch);
-            }
-            for (uint32_t j = 0; j < tail_rows; ++j)
-                std::memcpy(&frame[static_cast<size_t>(full_bands * band + j) * pitch],
-                            &local[static_cast<size_t>(o.tile_h + j) * pitch], pitch);
             rt_ctx_destroy(ctx);
         });
     }

@@ -277,6 +277,7 @@ struct rt_ctx {
     // rt_render: pinned staging slices for the device -> host copy of the outputs, a copy
     // stream that waits for each finished row band, and the host threads that empty the slices
     void* pin[kRing] = {};
+    size_t pin_cap = kSlice;               // bytes per staging slice (larger for rows wider than kSlice)
     hipEvent_t pin_ev[kRing] = {};
     hipStream_t copy_stream = nullptr;
     bool want_bands = false;               // set by rt_render around its render: fold in bands, events after each
@@ -541,6 +542,8 @@ int rt_device_count(int* n) {
     return RT_OK;
 }
 
+static int warm_streams(rt_ctx* c, const std::vector<hipStream_t>& ss);
+
 int rt_ctx_create(int device, rt_ctx** out) {
     if (!out) return RT_E_INVALID;
     *out = nullptr;
@@ -563,6 +566,8 @@ int rt_ctx_create(int device, rt_ctx** out) {
         hipMemcpy(c->d_srgb, srgb_average_table(), 255 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
         upload_srgb_table(srgb_average_table()) != hipSuccess)
         return cleanup(fail(nullptr, RT_E_HIP, "context initialisation failed"));
+    // the kernels' code objects load at their first launch: here, not in the first render
+    if (warm_streams(c, {c->stream}) != RT_OK) return cleanup(fail(nullptr, RT_E_HIP, "context warm-up failed"));
     *out = c;
     return RT_OK;
 }
@@ -761,7 +766,9 @@ int rt_qtree_nodes(const rt_scene* s, int leaf_max, void* nodes, float* boxes, i
         const int need = bvh4_stack_need(b4);
         const std::vector<DevQNode4> q = need <= kQ4Stack ? quantize_bvh4(b4) : std::vector<DevQNode4>{};
         if (info) { info[0] = static_cast<int64_t>(q.size()); info[1] = need; info[2] = leaf; }
-        if (q.size() > cap_nodes) return q.empty() ? RT_OK : fail(nullptr, RT_E_INVALID, "node buffer too small");
+        if (cap_nodes == 0) return RT_OK;                  // a size query: info[] alone
+        if (q.size() > cap_nodes) return fail(nullptr, RT_E_INVALID, "node buffer too small");
+        if (q.empty()) return RT_OK;
         const int32_t N = b4.n_nodes;
         std::memcpy(nodes, q.data(), q.size() * sizeof(DevQNode4));
         for (size_t i = 0; i < q.size(); ++i)
@@ -1050,41 +1057,68 @@ static int ensure_copy_stream(rt_ctx* c) {
 }
 
 // Device buffers of the sparse host copies for a tw x rows tile (segment bits, row counts, row
-// offsets, packed BGR and RGB at their largest: every segment flagged), grown on demand.
-static int ensure_sparse(rt_ctx* c, hipStream_t st, uint32_t tw, uint32_t rows, bool bgr, bool rgb) {
+// offsets, and the packed BGR / RGB sections of the outputs requested at their largest: every
+// segment flagged), grown on demand.  They are not part of the working-set budget, so they are
+// taken only from what the device has free beyond kRuntimeHeadroom; if they do not fit (or
+// hipMalloc fails) *ok is false and the render copies its frame the plain way.
+static int ensure_sparse(rt_ctx* c, hipStream_t st, uint32_t tw, uint32_t rows, bool bgr, bool rgb, bool* ok) {
+    *ok = false;
     int rc = ensure_copy_stream(c);
     if (rc != RT_OK) return rc;
     if (!c->sp_cam) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_cam, hipEventDisableTiming));
     if (!c->sp_ready) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ready, hipEventDisableTiming));
     const uint64_t nseg = (tw + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32, segs = nseg * rows;
     const uint64_t s_bits = align_up(rows * words * 4, 256), s_cnt = align_up(rows * 4ull, 256),
-                   s_off = align_up((rows + 1ull) * 4, 256), s_bgr = align_up(segs * 3 * kSegPx, 256),
-                   s_rgb = segs * 3 * kSegPx * sizeof(float);
+                   s_off = align_up((rows + 1ull) * 4, 256), s_bgr = bgr ? align_up(segs * 3 * kSegPx, 256) : 0,
+                   s_rgb = rgb ? segs * 3 * kSegPx * sizeof(float) : 0;
     const uint64_t need = s_bits + s_cnt + s_off + s_bgr + s_rgb;
-    (void)bgr; (void)rgb;
     if (need > c->sp_cap) {
         HIP_TRY(c, hipStreamSynchronize(st));
         HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
         if (c->d_sp) (void)hipFree(c->d_sp);
         c->d_sp = nullptr;
         c->sp_cap = 0;
-        HIP_TRY(c, hipMalloc(&c->d_sp, need));
+        size_t fr = 0, total = 0;
+        if (hipMemGetInfo(&fr, &total) != hipSuccess) { (void)hipGetLastError(); return RT_OK; }
+        if (need > fr || fr - need < kRuntimeHeadroom) return RT_OK;
+        if (hipMalloc(&c->d_sp, need) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_sp = nullptr;
+            return RT_OK;
+        }
         c->sp_cap = need;
     }
     auto* base = static_cast<uint8_t*>(c->d_sp);
     c->d_sp_bits = reinterpret_cast<uint32_t*>(base);
     c->d_sp_cnt = reinterpret_cast<uint32_t*>(base + s_bits);
     c->d_sp_off = reinterpret_cast<uint32_t*>(base + s_bits + s_cnt);
-    c->d_sp_bgr = base + s_bits + s_cnt + s_off;
-    c->d_sp_rgb = reinterpret_cast<float*>(base + s_bits + s_cnt + s_off + s_bgr);
+    c->d_sp_bgr = bgr ? base + s_bits + s_cnt + s_off : nullptr;
+    c->d_sp_rgb = rgb ? reinterpret_cast<float*>(base + s_bits + s_cnt + s_off + s_bgr) : nullptr;
+    *ok = true;
     return RT_OK;
 }
 
-static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
+// rt_ctx_reserve: a no-op launch with private memory on every stream of the schedule (the
+// code objects load, each hardware queue and its scratch are set up), then wait for them.
+static int warm_streams(rt_ctx* c, const std::vector<hipStream_t>& ss) {
+    for (hipStream_t s : ss) {
+        if (!s) continue;
+        HIP_TRY(c, launch_warmup(static_cast<uint32_t>(2 * c->n_cu), s));
+        HIP_TRY(c, launch_path_warmup(s));
+    }
+    for (hipStream_t s : ss)
+        if (s) HIP_TRY(c, hipStreamSynchronize(s));
+    return RT_OK;
+}
+
+// dry (rt_ctx_reserve): every allocation and stream the render would make, then warm_streams
+// instead of the launches; counters and the last render's statistics are left alone.
+static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream, bool dry = false) {
     if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
     uint32_t spp, band, stride, pitch;
     int rc = check_opts(c, o, spp, band, stride, pitch);
     if (rc != RT_OK) return rc;
+    if (o->flags & RT_OUT_FRAME_ROWS) return fail(c, RT_E_INVALID, "RT_OUT_FRAME_ROWS is for rt_render's host buffers");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
     // The context's working sets (counters, wavefront buffers, path stacks) are
@@ -1140,13 +1174,16 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
     if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)
         return fail(c, RT_E_UNSUPPORTED, "the wavefront path handles at most 32 lights");
-    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
-    c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
-    c->last_stream = st;
-    c->last_spp_traced = 1;
-    c->last_chunks = 0;
+    if (!dry) {
+        HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
+        c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
+        c->last_stream = st;
+        c->last_spp_traced = 1;
+        c->last_chunks = 0;
+    }
     c->n_bands = 0;
     c->sparse_on = false;
+    if (dry && (o->tile_w == 0 || o->tile_h == 0)) return warm_streams(c, {st});
     if (o->tile_w == 0 || o->tile_h == 0) {
         c->last_timed = false;
         HIP_TRY(c, hipEventRecord(c->render_done, st));
@@ -1306,11 +1343,32 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             for (auto& L : c->lanes) drop_lane_memory(L);      // retry with half the pixels per chunk
             cap_px = std::max<uint64_t>(1, static_cast<uint64_t>(chunk_rows) * o->tile_w / 2);
         }
-        // sparse host copies: a whole tile in one chunk on one lane, pixels written where they end
-        c->sparse_on = c->want_sparse && n_chunks == 1 && n_lanes == 1 && c->t(kTuneCompose) == 0 && stride == 1 &&
+        // sparse host copies: a whole tile (contiguous rows or row bands) in one chunk on one lane,
+        // pixels written where they end
+        c->sparse_on = c->want_sparse && n_chunks == 1 && n_lanes == 1 && c->t(kTuneCompose) == 0 &&
                        (fp.out_rgb || fp.out_bgr);
-        if (c->sparse_on && (rc = ensure_sparse(c, st, o->tile_w, o->tile_h, fp.out_bgr != nullptr, fp.out_rgb != nullptr)) != RT_OK)
-            return rc;
+        if (c->sparse_on) {
+            bool ok = false;
+            if ((rc = ensure_sparse(c, st, o->tile_w, o->tile_h, fp.out_bgr != nullptr, fp.out_rgb != nullptr, &ok)) != RT_OK)
+                return rc;
+            if (!ok && c->t(kTuneVerbose)) std::fprintf(stderr, "rtamd: sparse copy buffers do not fit: plain copies\n");
+            c->sparse_on = ok;
+        }
+        if (dry) {
+            std::vector<hipStream_t> ss{st};
+            if (c->want_bands) {                   // rt_render's copy stream and its band events
+                if ((rc = ensure_copy_stream(c)) != RT_OK) return rc;
+                ss.push_back(c->copy_stream);
+                for (uint32_t i = 0; i < n_chunks && i < static_cast<uint32_t>(kMaxBands); ++i)
+                    if (!c->band_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->band_ev[i], hipEventDisableTiming));
+            }
+            for (int l = 0; l < n_lanes; ++l) {
+                ss.push_back(c->lanes[l].s);
+                if (split)
+                    for (int i = 0; i < n_b; ++i) ss.push_back(c->lanes[l].sb[i]);
+            }
+            return warm_streams(c, ss);
+        }
         for (int l = 0; l < n_lanes; ++l) {
             c->lanes[l].b.tiles_x = tiles_x;
             c->lanes[l].b.wg_major = wg_major;
@@ -1442,11 +1500,13 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             c->path_bytes = need;
         }
         ps.mem = static_cast<unsigned char*>(c->d_path);
+        if (dry) return warm_streams(c, {st});
         const bool staged = path_lds_bytes(c->dsc, true) <= 48 * 1024;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_path(c->dsc, fp, ps, staged, st));
         HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {
+        if (dry) return warm_streams(c, {st});
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
         HIP_TRY(c, hipEventRecord(c->ev1, st));
@@ -1545,47 +1605,92 @@ int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
     return RT_OK;
 }
 
+// Where rt_render puts a device row (RT_OUT_FRAME_ROWS or not): local row j of the tile, dev_pitch
+// bytes apart on the device, row_bytes of it copied, lands at host byte offset host_row(j) *
+// host_pitch + host_x.  A plain tile: host_row(j) = j, the host rows laid out as the device's; a
+// frame: the tile's frame row (rt_render_opts: y0 + ((j/band)*band_stride + band_phase)*band + j%band).
+struct OutMap {
+    size_t dev_pitch = 0, row_bytes = 0, host_pitch = 0, host_x = 0;
+    bool frame = false;
+    uint32_t y0 = 0, band = 1, stride = 1, phase = 0;
+    size_t host_row(uint32_t j) const {
+        return frame ? y0 + (static_cast<size_t>(j / band) * stride + phase) * band + j % band : j;
+    }
+    size_t host_off(uint32_t j) const { return host_row(j) * host_pitch + host_x; }
+    // consecutive rows are one contiguous byte range on both sides
+    bool contiguous() const { return dev_pitch == host_pitch && row_bytes == dev_pitch && host_x == 0; }
+    // local rows j and j + 1 sit in consecutive host rows
+    bool next_row(uint32_t j) const { return host_row(j + 1) == host_row(j) + 1; }
+};
+
 // Device -> caller-owned host memory, row band by row band: the copy stream
 // waits for each band's fold (c->band_ev, recorded by the render when
 // c->want_bands was set; otherwise for the whole render), so the PCIe transfer
 // of the first bands overlaps the fold of the later ones.  A page-locked
-// destination gets the DMA directly; pageable memory goes through kRing pinned
-// slices of kSlice bytes, the copy engine filling slices ahead while the host
-// pool empties them in order.  `pitch`: bytes per output row.
-// wait = false (sparse copies): no wait on the bands, the copy stream's order alone (its
-// segment kernels follow the camera pass).
-static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uint32_t rows, bool wait = true) {
-    const size_t bytes = pitch * rows;
-    if (!bytes) return RT_OK;
+// destination gets the DMA directly (one copy per run of rows that are
+// consecutive on the host, 2D when the rows are not back to back); pageable
+// memory goes through kRing pinned slices of whole rows, the copy engine
+// filling slices ahead while the host pool empties them in order into their
+// host rows.  wait = false (sparse copies): no wait on the bands, the copy
+// stream's order alone (its segment kernels follow the camera pass).
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, uint32_t rows, bool wait = true) {
+    if (!rows || !m.row_bytes) return RT_OK;
     int rc = ensure_copy_stream(c);
     if (rc != RT_OK) return rc;
-    struct Piece { size_t off, len; int band; };
+    const auto* s8 = static_cast<const uint8_t*>(src);
+    auto* d8 = static_cast<uint8_t*>(dst);
+    hipPointerAttribute_t attr{};
+    const bool pinned = hipPointerGetAttributes(&attr, dst) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();                       // a pageable pointer is not an error
+    const bool contig = m.contiguous();
+    // pieces: rows [j0, j0 + n) of one chunk band, consecutive on the host (pinned), at most one
+    // staging slice of rows (pageable)
+    const size_t slice = std::max(kSlice, m.dev_pitch);
+    const uint32_t slice_rows = static_cast<uint32_t>(std::max<size_t>(1, slice / m.dev_pitch));
+    struct Piece { uint32_t j0, n; int band; };
     std::vector<Piece> pieces;
     const int nb = c->n_bands > 0 ? c->n_bands : 1;
     for (int bi = 0; bi < nb; ++bi) {
-        const size_t a = c->n_bands > 0 ? c->band_row0[bi] * pitch : 0;
-        const size_t e = c->n_bands > 0 ? (static_cast<size_t>(c->band_row0[bi]) + c->band_nrows[bi]) * pitch : bytes;
-        for (size_t o = a; o < e; o += kSlice) pieces.push_back(Piece{o, std::min(kSlice, e - o), bi});
+        const uint32_t a = c->n_bands > 0 ? c->band_row0[bi] : 0;
+        const uint32_t e = c->n_bands > 0 ? std::min(rows, c->band_row0[bi] + c->band_nrows[bi]) : rows;
+        for (uint32_t j = a; j < e;) {
+            uint32_t n = 1;
+            if (pinned) {
+                while (j + n < e && m.next_row(j + n - 1) && (contig || n < 65535)) ++n;
+            } else {
+                n = std::min(slice_rows, e - j);
+            }
+            pieces.push_back(Piece{j, n, bi});
+            j += n;
+        }
     }
     auto wait_band = [&](int bi) -> hipError_t {
         if (!wait) return hipSuccess;
         return hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[bi] : c->render_done, 0);
     };
-    const auto* s8 = static_cast<const uint8_t*>(src);
-    auto* d8 = static_cast<uint8_t*>(dst);
-    hipPointerAttribute_t attr{};
-    if (hipPointerGetAttributes(&attr, dst) == hipSuccess && attr.type == hipMemoryTypeHost) {
+    if (pinned) {
         int last = -1;
         for (const Piece& pc : pieces) {
             if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
-            HIP_TRY(c, hipMemcpyAsync(d8 + pc.off, s8 + pc.off, pc.len, hipMemcpyDeviceToHost, c->copy_stream));
+            if (contig)
+                HIP_TRY(c, hipMemcpyAsync(d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
+                                          hipMemcpyDeviceToHost, c->copy_stream));
+            else
+                HIP_TRY(c, hipMemcpy2DAsync(d8 + m.host_off(pc.j0), m.host_pitch, s8 + pc.j0 * m.dev_pitch, m.dev_pitch,
+                                            m.row_bytes, pc.n, hipMemcpyDeviceToHost, c->copy_stream));
         }
         HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
         return RT_OK;
     }
-    (void)hipGetLastError();                       // a pageable pointer is not an error
+    if (slice > c->pin_cap) {                      // rows wider than a slice: larger slices
+        for (int i = 0; i < kRing; ++i) {
+            if (c->pin[i]) (void)hipHostFree(c->pin[i]);
+            c->pin[i] = nullptr;
+        }
+        c->pin_cap = slice;
+    }
     for (int i = 0; i < kRing; ++i) {
-        if (!c->pin[i]) HIP_TRY(c, hipHostMalloc(&c->pin[i], kSlice, hipHostMallocDefault));
+        if (!c->pin[i]) HIP_TRY(c, hipHostMalloc(&c->pin[i], c->pin_cap, hipHostMallocDefault));
         if (!c->pin_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
     }
     const size_t n = pieces.size();
@@ -1596,13 +1701,24 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, size_t pitch, uin
             const Piece& pc = pieces[issued];
             if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
             const int slot = static_cast<int>(issued % kRing);
-            HIP_TRY(c, hipMemcpyAsync(c->pin[slot], s8 + pc.off, pc.len, hipMemcpyDeviceToHost, c->copy_stream));
+            HIP_TRY(c, hipMemcpyAsync(c->pin[slot], s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch, hipMemcpyDeviceToHost,
+                                      c->copy_stream));
             HIP_TRY(c, hipEventRecord(c->pin_ev[slot], c->copy_stream));
             ++issued;
         }
         const int slot = static_cast<int>(drained % kRing);
         HIP_TRY(c, hipEventSynchronize(c->pin_ev[slot]));
-        c->pool.copy(d8 + pieces[drained].off, c->pin[slot], pieces[drained].len);
+        const Piece& pc = pieces[drained];
+        const auto* from = static_cast<const uint8_t*>(c->pin[slot]);
+        if (!m.frame && contig) {
+            c->pool.copy(d8 + m.host_off(pc.j0), from, pc.n * m.dev_pitch);
+        } else {                                   // row by row into the host rows, shared by the pool
+            const size_t parts = std::min<size_t>(HostCopyPool::kParts, pc.n);
+            c->pool.run(parts, [&](size_t q) {
+                const uint32_t a = pc.j0 + static_cast<uint32_t>(pc.n * q / parts), e = pc.j0 + static_cast<uint32_t>(pc.n * (q + 1) / parts);
+                for (uint32_t j = a; j < e; ++j) std::memcpy(d8 + m.host_off(j), from + (j - pc.j0) * m.dev_pitch, m.row_bytes);
+            });
+        }
         ++drained;
     }
     return RT_OK;
@@ -1622,8 +1738,9 @@ static int ensure_pinned(rt_ctx* c, void*& p, size_t& cap, size_t bytes) {
 // rt_render's copies after a sparse render: the row offsets and segment bits,
 // then the whole frame as the camera pass left it (every pixel without a chain is final; the
 // generations run meanwhile), then, once the render is done, the packed chain segments in row
-// ranges, each scattered into the frame by the host pool as soon as it has landed.
-static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, size_t pitch) {
+// ranges, each scattered into the host rows by the host pool as soon as it has landed.
+static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, const OutMap& mr,
+                       const OutMap& mb) {
     const uint32_t rows = o->tile_h, tw = o->tile_w;
     const uint32_t nseg = (tw + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
     const size_t s_off = (rows + 1ull) * 4, s_bits = static_cast<size_t>(rows) * words * 4;
@@ -1636,9 +1753,8 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     auto* h_bits = h_off + (rows + 1);
     HIP_TRY(c, hipMemcpyAsync(h_off, c->d_sp_off, s_off, hipMemcpyDeviceToHost, c->copy_stream));
     HIP_TRY(c, hipMemcpyAsync(h_bits, c->d_sp_bits, s_bits, hipMemcpyDeviceToHost, c->copy_stream));
-    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, rows, false)) != RT_OK) return rc;
-    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(tw) * 3 * sizeof(float), rows, false)) != RT_OK)
-        return rc;
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, rows, false)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, rows, false)) != RT_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->copy_stream));      // (the offsets and bits were queued first)
     const double t_frame = us();
     const uint64_t total = h_off[rows];
@@ -1660,7 +1776,8 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
                                       c->copy_stream));
         HIP_TRY(c, hipEventRecord(c->sp_ev[j], c->copy_stream));
     }
-    const size_t pad = pitch - 3ull * tw;
+    const size_t pad = mb.row_bytes - 3ull * tw;           // BMP row padding of the tile's rows (device pitch)
+    auto* rgb8 = reinterpret_cast<uint8_t*>(out_rgb);
     auto scatter_rows = [&](uint32_t r0, uint32_t r1) {
         for (uint32_t r = r0; r < r1; ++r) {
             const uint32_t* bits = h_bits + static_cast<size_t>(r) * words;
@@ -1670,11 +1787,11 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
                     const uint32_t x0 = (w * 32 + static_cast<uint32_t>(__builtin_ctz(m))) * kSegPx;
                     const uint32_t n = std::min(kSegPx, tw - x0);
                     if (out_bgr) {
-                        uint8_t* d = out_bgr + static_cast<size_t>(r) * pitch + 3ull * x0;
+                        uint8_t* d = out_bgr + mb.host_off(r) + 3ull * x0;
                         std::memcpy(d, hb + i * seg_b, 3ull * n);
                         if (x0 + n == tw && pad) std::memset(d + 3ull * n, 0, pad);   // BMP row padding
                     }
-                    if (out_rgb) std::memcpy(out_rgb + (static_cast<size_t>(r) * tw + x0) * 3, hr + i * 3 * kSegPx, 12ull * n);
+                    if (out_rgb) std::memcpy(rgb8 + mr.host_off(r) + 12ull * x0, hr + i * 3 * kSegPx, 12ull * n);
                 }
         }
     };
@@ -1696,31 +1813,70 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     return RT_OK;
 }
 
-static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
-    uint32_t spp, band, stride, pitch;
-    int rc = check_opts(c, o, spp, band, stride, pitch);
-    if (rc != RT_OK) return rc;
-    HIP_TRY(c, hipSetDevice(c->device));
-    rt_render_opts oo = *o;
-    oo.flags = (o->flags & ~(RT_OUT_RGB_F32 | RT_OUT_BGR_U8)) | (out_rgb ? RT_OUT_RGB_F32 : 0) | (out_bgr ? RT_OUT_BGR_U8 : 0);
-    const size_t rgb_bytes = static_cast<size_t>(o->tile_w) * o->tile_h * 3 * sizeof(float);
-    const size_t bgr_bytes = static_cast<size_t>(pitch) * o->tile_h;
-    if (c->render_pending && ((out_rgb && rgb_bytes > c->rgb_cap) || (out_bgr && bgr_bytes > c->bgr_cap)))
-        HIP_TRY(c, hipEventSynchronize(c->render_done));     // an earlier render may still write the old buffers
-    if (out_rgb && rgb_bytes > c->rgb_cap) {
+// rt_render's layout on both sides (check_opts has validated o): the device frame of the tile
+// (f32 rows of 12 tile_w bytes, BGR rows of *dev_bgr_pitch bytes) and where each row goes on the host.
+static int host_layout(rt_ctx* c, const rt_render_opts* o, uint32_t pitch, OutMap& mr, OutMap& mb, uint32_t* dev_bgr_pitch) {
+    const bool frame = (o->flags & RT_OUT_FRAME_ROWS) != 0;
+    mr = OutMap{};
+    mr.dev_pitch = mr.row_bytes = static_cast<size_t>(o->tile_w) * 12;
+    mr.host_pitch = mr.dev_pitch;
+    if (frame) {
+        const uint32_t hp = o->bgr_pitch ? o->bgr_pitch : 3 * o->width;
+        if (hp < 3ull * o->width) return fail(c, RT_E_INVALID, "RT_OUT_FRAME_ROWS: bgr_pitch < 3*width");
+        mr.frame = true;
+        mr.y0 = o->y0; mr.band = o->band ? o->band : 1; mr.stride = o->band_stride ? o->band_stride : 1; mr.phase = o->band_phase;
+        mr.host_pitch = static_cast<size_t>(o->width) * 12;
+        mr.host_x = static_cast<size_t>(o->x0) * 12;
+        mb = mr;
+        // the tile's BGR rows carry the frame's row padding when the tile ends at the frame's right edge
+        const uint32_t pad = o->x0 + o->tile_w == o->width ? hp - 3 * o->width : 0;
+        mb.dev_pitch = mb.row_bytes = 3ull * o->tile_w + pad;
+        mb.host_pitch = hp;
+        mb.host_x = 3ull * o->x0;
+        *dev_bgr_pitch = 3 * o->tile_w + pad;
+    } else {
+        mb = OutMap{};
+        mb.dev_pitch = mb.row_bytes = mb.host_pitch = pitch;
+        *dev_bgr_pitch = pitch;
+    }
+    return RT_OK;
+}
+
+// rt_render's device frame for the tile: grown on demand (an earlier render may still write it).
+static int ensure_host_frame(rt_ctx* c, size_t rgb_bytes, size_t bgr_bytes) {
+    if (c->render_pending && (rgb_bytes > c->rgb_cap || bgr_bytes > c->bgr_cap))
+        HIP_TRY(c, hipEventSynchronize(c->render_done));
+    if (rgb_bytes > c->rgb_cap) {
         if (c->d_rgb) (void)hipFree(c->d_rgb);
         c->d_rgb = nullptr; c->rgb_cap = 0;
         HIP_TRY(c, hipMalloc(&c->d_rgb, rgb_bytes));
         c->rgb_cap = rgb_bytes;
     }
-    if (out_bgr && bgr_bytes > c->bgr_cap) {
+    if (bgr_bytes > c->bgr_cap) {
         if (c->d_bgr) (void)hipFree(c->d_bgr);
         c->d_bgr = nullptr; c->bgr_cap = 0;
         HIP_TRY(c, hipMalloc(&c->d_bgr, bgr_bytes));
         c->bgr_cap = bgr_bytes;
     }
-    // an earlier rt_render's copies (copy stream) must be done with d_rgb / d_bgr: they are, since
-    // copy_to_host returns only once its last piece has been drained or synchronised
+    return RT_OK;
+}
+
+static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
+    uint32_t spp, band, stride, pitch;
+    int rc = check_opts(c, o, spp, band, stride, pitch);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    OutMap mr, mb;
+    uint32_t dev_pitch = pitch;
+    if ((rc = host_layout(c, o, pitch, mr, mb, &dev_pitch)) != RT_OK) return rc;
+    rt_render_opts oo = *o;
+    oo.flags = (o->flags & ~(RT_OUT_RGB_F32 | RT_OUT_BGR_U8 | RT_OUT_FRAME_ROWS)) | (out_rgb ? RT_OUT_RGB_F32 : 0) |
+               (out_bgr ? RT_OUT_BGR_U8 : 0);
+    oo.bgr_pitch = dev_pitch;
+    // an earlier rt_render's copies (copy stream) are done with d_rgb / d_bgr: copy_to_host returns
+    // only once its last piece has been drained or synchronised
+    if ((rc = ensure_host_frame(c, out_rgb ? mr.dev_pitch * o->tile_h : 0, out_bgr ? mb.dev_pitch * o->tile_h : 0)) != RT_OK)
+        return rc;
     c->want_bands = true;
     c->want_sparse = c->t(kTuneSparseOut) != 0;
     rc = render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr);
@@ -1728,11 +1884,10 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     c->want_sparse = false;
     if (rc != RT_OK) return rc;
     if (c->sparse_on) {
-        if ((rc = copy_sparse(c, o, out_rgb, out_bgr, pitch)) != RT_OK) return rc;
+        if ((rc = copy_sparse(c, o, out_rgb, out_bgr, mr, mb)) != RT_OK) return rc;
     } else {
-        if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, pitch, o->tile_h)) != RT_OK) return rc;
-        if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, static_cast<size_t>(o->tile_w) * 3 * sizeof(float), o->tile_h)) != RT_OK)
-            return rc;
+        if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, o->tile_h)) != RT_OK) return rc;
+        if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, o->tile_h)) != RT_OK) return rc;
     }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (stats) return rt_ctx_stats(c, stats);
@@ -1742,6 +1897,56 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
 int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {
     if (!c || !o) return RT_E_INVALID;
     return guarded(c, [&] { return render_host(c, o, out_rgb, out_bgr, stats); });
+}
+
+// rt_ctx_reserve: render_device's allocations and streams without its launches (dry), plus, for
+// rt_render (host), the device frame, the staging slices and the sparse copies' pinned buffers.
+static int reserve(rt_ctx* c, const rt_render_opts* o, int host) {
+    if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
+    uint32_t spp, band, stride, pitch;
+    int rc = check_opts(c, o, spp, band, stride, pitch);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    rt_render_opts oo = *o;
+    if (!host) {
+        if (o->flags & RT_OUT_FRAME_ROWS) return fail(c, RT_E_INVALID, "RT_OUT_FRAME_ROWS is for rt_render's host buffers");
+        return render_device(c, &oo, nullptr, nullptr, nullptr, true);
+    }
+    OutMap mr, mb;
+    uint32_t dev_pitch = pitch;
+    if ((rc = host_layout(c, o, pitch, mr, mb, &dev_pitch)) != RT_OK) return rc;
+    oo.flags &= ~RT_OUT_FRAME_ROWS;
+    oo.bgr_pitch = dev_pitch;
+    const bool rgb = (o->flags & RT_OUT_RGB_F32) != 0, bgr = (o->flags & RT_OUT_BGR_U8) != 0;
+    if ((rc = ensure_host_frame(c, rgb ? mr.dev_pitch * o->tile_h : 0, bgr ? mb.dev_pitch * o->tile_h : 0)) != RT_OK) return rc;
+    c->want_bands = true;
+    c->want_sparse = c->t(kTuneSparseOut) != 0;
+    rc = render_device(c, &oo, c->d_rgb, c->d_bgr, nullptr, true);
+    c->want_bands = false;
+    c->want_sparse = false;
+    if (rc != RT_OK) return rc;
+    for (int i = 0; i < kRing; ++i) {               // the staging slices of pageable destinations
+        if (!c->pin[i]) HIP_TRY(c, hipHostMalloc(&c->pin[i], c->pin_cap, hipHostMallocDefault));
+        if (!c->pin_ev[i]) HIP_TRY(c, hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming));
+    }
+    if (c->sparse_on) {
+        const uint64_t nseg = (o->tile_w + kSegPx - 1) / kSegPx, words = (nseg + 31) / 32;
+        if ((rc = ensure_pinned(c, c->h_sp_meta, c->h_sp_meta_cap, (o->tile_h + 1ull) * 4 + o->tile_h * words * 4)) != RT_OK)
+            return rc;
+        // the packed segments' pinned buffer at its worst case (every segment flagged), up to 1 GB;
+        // a render that needs more grows it
+        const uint64_t worst = nseg * o->tile_h * 3 * kSegPx * ((bgr ? 1 : 0) + (rgb ? 4 : 0));
+        if ((rc = ensure_pinned(c, c->h_sp_pk, c->h_sp_pk_cap, std::max<uint64_t>(1, std::min<uint64_t>(worst, 1ull << 30)))) != RT_OK)
+            return rc;
+        for (int j = 0; j < rt_ctx::kSpRanges; ++j)
+            if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
+    }
+    return RT_OK;
+}
+
+int rt_ctx_reserve(rt_ctx* c, const rt_render_opts* o, int host) {
+    if (!c || !o) return RT_E_INVALID;
+    return guarded(c, [&] { return reserve(c, o, host); });
 }
 
 int rt_ctx_set_tuning(rt_ctx* c, const char* key, int64_t value) {

@@ -1576,6 +1576,23 @@ extern "C" int rt_debug_stamps(unsigned long long* out, int n, int reset) {
 namespace rtamd {
 #endif
 
+// rt_ctx_reserve: one launch on a stream loads this file's code object (its first launch does)
+// and has the runtime set up the stream's hardware queue, including the queue's scratch, which
+// it sizes at the first launch that needs private memory: kWarmScratch bytes per lane, at
+// least what any wavefront kernel spills or stacks (128-208 B).
+constexpr uint32_t kWarmScratch = 256;
+__global__ __launch_bounds__(kWfThreads) void wf_warm(uint32_t* sink, uint32_t salt) {
+    volatile uint32_t priv[kWarmScratch / 4];       // volatile + a lane-dependent index: kept in scratch
+    const uint32_t i = (threadIdx.x * 7u + salt) % (kWarmScratch / 4);
+    priv[i] = salt;
+    if (priv[(i + salt) % (kWarmScratch / 4)] == 0xfeedf00du && sink) sink[blockIdx.x] = salt;
+}
+
+hipError_t launch_warmup(uint32_t workgroups, hipStream_t s) {
+    hipLaunchKernelGGL(wf_warm, dim3(std::max(1u, workgroups)), dim3(kWfThreads), 0, s, nullptr, 1u);
+    return hipGetLastError();
+}
+
 // Diagnostic (rt_div_a2_check): the sphere test's division t = x / (2a) as
 // sphere_t computes it (sphere_k's hoisted reciprocal finished by div_a2) and
 // as the compiler's own f64 division, side by side.

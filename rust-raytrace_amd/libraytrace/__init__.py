@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(_HERE)
 LIB_PATH = os.environ.get("RT_LIBRTAMD") or os.path.join(PKG_DIR, "librtamd.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "raytrace_amd.h")
 
-RT_ABI_VERSION = 4               # include/raytrace_amd.h
+RT_ABI_VERSION = 5               # include/raytrace_amd.h
 RT_OK = 0
 RT_E_INVALID, RT_E_NODEVICE, RT_E_HIP, RT_E_NOMEM = -1, -2, -3, -4
 RT_E_UNSUPPORTED, RT_E_PARSE, RT_E_NOSCENE, RT_E_IO = -5, -6, -7, -8
@@ -29,7 +29,7 @@ RT_MAT_PHONG, RT_MAT_INDIRECT_PHONG, RT_MAT_FRESNEL, RT_MAT_TRANSPARENT = 0, 1, 
 RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AREA = 0, 1, 2
 RT_CAMERA_SIMPLE, RT_CAMERA_DOF = 0, 1
 RT_BG_SOLID, RT_BG_SKYBOX = 0, 1
-RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK, RT_TIME_KERNELS = 1, 2, 4, 8
+RT_OUT_RGB_F32, RT_OUT_BGR_U8, RT_COUNT_WORK, RT_TIME_KERNELS, RT_OUT_FRAME_ROWS = 1, 2, 4, 8, 16
 KERNEL_FAMILIES = ("nearest", "occlusion", "shade", "fold", "tally", "camera", "compose", "tail")   # rt_kernel_family
 RT_ALGO_AUTO, RT_ALGO_BRUTE_LDS, RT_ALGO_BRUTE_GLOBAL, RT_ALGO_WAVEFRONT, RT_ALGO_WAVEFRONT_BRUTE = 0, 1, 2, 3, 4
 RT_ALGO_PATH = 5
@@ -116,6 +116,7 @@ def _load():
         "rt_render_opts_default": (None, [P(rt_render_opts), C.c_uint32, C.c_uint32]),
         "rt_render": (C.c_int, [C.c_void_p, P(rt_render_opts), P(C.c_float), P(C.c_uint8), P(rt_stats)]),
         "rt_render_device": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_void_p, C.c_void_p, C.c_void_p]),
+        "rt_ctx_reserve": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_int]),
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
         "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
         "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
@@ -405,17 +406,22 @@ class Context:
     def render(self, opts, rgb=True, bgr=True, out=None, stats=True):
         """Synchronous render of opts' tile into host numpy arrays.
         Returns (rgb float32 [tile_h, tile_w, 3] or None, bgr uint8 [tile_h, pitch] or None, stats).
+        With RT_OUT_FRAME_ROWS in opts.flags, out= holds whole-frame arrays (height rows) and the tile's
+        rows are written into their frame rows.
         out: (rgb, bgr) arrays to reuse (either None to skip that output); stats=False passes
         no rt_stats (the drop-in call of INTEGRATION.md: no counter read-back), returns None."""
-        pitch = opts.bgr_pitch or 3 * opts.tile_w
+        frame = bool(opts.flags & RT_OUT_FRAME_ROWS)
+        pitch = opts.bgr_pitch or 3 * (opts.width if frame else opts.tile_w)
+        rows, cols = (opts.height, opts.width) if frame else (opts.tile_h, opts.tile_w)
         if out is not None:
             out_rgb, out_bgr = out
             rgb, bgr = out_rgb is not None, out_bgr is not None
-            assert not rgb or (out_rgb.dtype == np.float32 and out_rgb.size >= opts.tile_h * opts.tile_w * 3
+            assert not rgb or (out_rgb.dtype == np.float32 and out_rgb.size >= rows * cols * 3
                                and out_rgb.flags.c_contiguous)
-            assert not bgr or (out_bgr.dtype == np.uint8 and out_bgr.size >= opts.tile_h * pitch
+            assert not bgr or (out_bgr.dtype == np.uint8 and out_bgr.size >= rows * pitch
                                and out_bgr.flags.c_contiguous)
         else:
+            assert not frame, "RT_OUT_FRAME_ROWS renders into caller frames: pass out=(rgb, bgr)"
             out_rgb = np.zeros((opts.tile_h, opts.tile_w, 3), np.float32) if rgb else None
             out_bgr = np.full((opts.tile_h, pitch), 0xCD, np.uint8) if bgr else None
         st = rt_stats() if stats else None
@@ -430,6 +436,11 @@ class Context:
         """Asynchronous render into device buffers (raw pointers, e.g. torch tensor.data_ptr())."""
         _check(lib.rt_render_device(self._h, C.byref(opts), C.c_void_p(d_rgb_ptr or 0),
                                     C.c_void_p(d_bgr_ptr or 0), C.c_void_p(stream_ptr or 0)), self._h)
+
+    def reserve(self, opts, host=False):
+        """rt_ctx_reserve: allocate and warm up everything a render with opts needs (host: rt_render's
+        buffers too), so that render runs warm."""
+        _check(lib.rt_ctx_reserve(self._h, C.byref(opts), 1 if host else 0), self._h)
 
     def stats(self):
         st = rt_stats()

@@ -772,6 +772,187 @@ def test_sparse_host_copies_bit_identical(gpu_ctx, scene):
                         assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), (w, h, pitch, kv, outs)
 
 
+def _hip():
+    import ctypes as C
+    return C.CDLL("libamdhip64.so.7")      # the HIP runtime librtamd.so runs on (already loaded: by soname)
+
+
+class _Pinned:
+    """A page-locked host array (hipHostMalloc of the HIP runtime librtamd.so uses): rt_render DMAs
+    into it directly instead of through its staging slices."""
+
+    def __init__(self, shape, dtype, fill):
+        import ctypes as C
+        self.hip = _hip()
+        self.p = C.c_void_p()
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        assert self.hip.hipHostMalloc(C.byref(self.p), C.c_size_t(nbytes), 0) == 0
+        self.arr = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.p.value)).view(dtype).reshape(shape)
+        self.arr[...] = fill
+
+    def free(self):
+        self.arr = None
+        self.hip.hipHostFree(self.p)
+
+
+@pytest.mark.parametrize("scene", ["config3", "fresnel"])
+def test_sparse_host_copies_banded_tiles(gpu_ctx, scene):
+    """Sparse copies for row-band tiles (a rank's share of a multi-GPU frame:
+    band_stride > 1, band_phase > 0, a ragged band count), into pageable and
+    page-locked buffers holding garbage: every byte and colour as the plain
+    copy (sparse_out 0)."""
+    w, h = 197, 160
+    spec = {"config3": scenes.config3, "fresnel": scenes.config2_fresnel}[scene](w, h)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    for band, stride, phase, pitch in [(16, 2, 1, 0), (16, 3, 0, 604), (8, 8, 7, 0), (5, 4, 2, 0)]:
+        rows = sum(min(band, h - b * band) for b in range(phase, (h + band - 1) // band, stride)
+                   if (b + 1) * band <= h)           # whole bands only (check_opts: the tile stays in the frame)
+        o = lr.render_opts(w, h, max_depth=spec.max_depth, spp=1, algo=lr.RT_ALGO_WAVEFRONT, band=band,
+                           band_stride=stride, band_phase=phase, tile_h=rows, bgr_pitch=pitch)
+        with _with_tuning(gpu_ctx, sparse_out=0):
+            base = gpu_ctx.render(o)
+        for pinned in (False, True):
+            for outs in [(True, True), (False, True), (True, False)]:
+                mk = (lambda s, d, f: _Pinned(s, d, f)) if pinned else (lambda s, d, f: type("A", (), {
+                    "arr": np.full(s, f, d), "free": lambda self: None})())
+                rgb = mk(base[0].shape, np.float32, np.nan) if outs[0] else None
+                bgr = mk(base[1].shape, np.uint8, 0xAB) if outs[1] else None
+                try:
+                    with _with_tuning(gpu_ctx, sparse_out=1):
+                        got = gpu_ctx.render(o, out=(rgb.arr if rgb else None, bgr.arr if bgr else None))
+                    if outs[1]:
+                        assert np.array_equal(got[1], base[1]), (band, stride, phase, pitch, pinned, outs)
+                    if outs[0]:
+                        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), (band, stride, phase,
+                                                                                                  pinned, outs)
+                finally:
+                    for a in (rgb, bgr):
+                        if a:
+                            a.free()
+
+
+def test_sparse_host_copies_large_tile_pinned(gpu_ctx):
+    """A tile large enough that the frame copy and the 16 packed row ranges
+    really overlap the generations (1024 x 512, depth 8), into a page-locked
+    and a pageable buffer: bit for bit the plain copy."""
+    spec = scenes.config3(1024, 512)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    o = lr.render_opts(1024, 512, max_depth=8, spp=1)
+    with _with_tuning(gpu_ctx, sparse_out=0):
+        base = gpu_ctx.render(o)
+    rgb, bgr = _Pinned(base[0].shape, np.float32, np.nan), _Pinned(base[1].shape, np.uint8, 0x5A)
+    try:
+        got = gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
+        assert np.array_equal(got[1], base[1])
+        assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32))
+    finally:
+        rgb.free()
+        bgr.free()
+    got = gpu_ctx.render(o, out=(np.full_like(base[0], np.nan), np.full_like(base[1], 0x5A)))
+    assert np.array_equal(got[1], base[1])
+    assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("sparse", [1, 0])
+def test_frame_rows_gather_matches_whole_frame(gpu_ctx, sparse):
+    """RT_OUT_FRAME_ROWS (the multi-GPU host gather, main.rs:45-58 split over
+    devices): N "ranks" render their 16-row bands straight into one shared
+    frame (page-locked, like bench.py's shared frame, and pageable), each
+    writing only its rows; with a ragged last band rendered as its own tile,
+    a padded BMP pitch, and a partial-width tile (columns x0.. of the frame):
+    the frame equals the whole-frame render bit for bit, and the oracle's."""
+    W, H, band = 150, 100, 16
+    spec = scenes.config3(W, H)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    pitch = (3 * W + 3) & ~3
+    whole = gpu_ctx.render(lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, bgr_pitch=pitch))
+    ref = ref64.render(spec)
+    assert np.array_equal(whole[1][:, :3 * W], ref["bgr"])
+    full = H // band
+    for n, pinned in [(3, True), (2, False), (1, True)]:
+        mk = (lambda s, d, f: _Pinned(s, d, f)) if pinned else (lambda s, d, f: type("A", (), {
+            "arr": np.full(s, f, d), "free": lambda self: None})())
+        rgb, bgr = mk((H, W, 3), np.float32, np.nan), mk((H, pitch), np.uint8, 0xAB)
+        try:
+            with _with_tuning(gpu_ctx, sparse_out=sparse):
+                for r in range(n):
+                    nb = len(range(r, full, n))
+                    o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, band=band, band_stride=n, band_phase=r,
+                                       tile_h=nb * band, bgr_pitch=pitch,
+                                       flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                    gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
+                # the ragged last band (rows full*band .. H-1) as one more tile
+                o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, y0=full * band, tile_h=H - full * band,
+                                   bgr_pitch=pitch, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
+            assert np.array_equal(bgr.arr, whole[1]), (n, pinned)
+            assert np.array_equal(rgb.arr.view(np.uint32), whole[0].view(np.uint32)), (n, pinned)
+            # a partial-width tile (columns 40..139 of rows 20..59) lands in its columns; the rest is untouched
+            bgr.arr[...] = 0xAB
+            rgb.arr[...] = np.nan
+            with _with_tuning(gpu_ctx, sparse_out=sparse):
+                o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=40, tile_w=100, y0=20, tile_h=40,
+                                   bgr_pitch=pitch, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
+            assert np.array_equal(bgr.arr[20:60, 120:420], whole[1][20:60, 120:420])
+            assert (bgr.arr[20:60, :120] == 0xAB).all() and (bgr.arr[20:60, 420:] == 0xAB).all()
+            assert (bgr.arr[:20] == 0xAB).all() and (bgr.arr[60:] == 0xAB).all()
+            assert np.array_equal(rgb.arr[20:60, 40:140].view(np.uint32), whole[0][20:60, 40:140].view(np.uint32))
+            assert np.isnan(rgb.arr[20:60, :40]).all() and np.isnan(rgb.arr[20:60, 140:]).all()
+            # ... and the tile at the right edge writes the BMP row padding (zero)
+            with _with_tuning(gpu_ctx, sparse_out=sparse):
+                o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=50, tile_w=W - 50, y0=0, tile_h=8,
+                                   bgr_pitch=pitch, flags=lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                gpu_ctx.render(o, out=(None, bgr.arr))
+            assert np.array_equal(bgr.arr[:8, 150:], whole[1][:8, 150:])
+            assert (bgr.arr[:8, 3 * W:] == 0).all() and (bgr.arr[:8, :150] == 0xAB).all()
+        finally:
+            rgb.free()
+            bgr.free()
+
+
+def test_frame_rows_rejects_bad_layouts(gpu_ctx):
+    spec = scenes.config3(64, 32)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    fr = lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS
+    bgr = np.zeros((32, 64 * 3), np.uint8)
+    with pytest.raises(lr.RtError) as e:          # a frame pitch below 3 * width
+        gpu_ctx.render(lr.render_opts(64, 32, tile_w=32, bgr_pitch=100, flags=fr, max_depth=2), out=(None, bgr))
+    assert e.value.code == lr.RT_E_INVALID
+    with pytest.raises(lr.RtError) as e:          # device buffers have no frame rows
+        gpu_ctx.render_device(lr.render_opts(64, 32, flags=fr, max_depth=2), 0, 1 << 40)
+    assert e.value.code == lr.RT_E_INVALID
+
+
+def test_reserve_then_render_is_unchanged(gpu_ctx):
+    """rt_ctx_reserve allocates and warms up without rendering: the render after
+    it gives the same bytes and counts as without it, the statistics of the
+    render before it are untouched, and reserving for a render already
+    prepared is cheap (no allocation)."""
+    import time
+    spec = scenes.config3(256, 192)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    o = lr.render_opts(256, 192, max_depth=8, spp=1)
+    rgb0, bgr0, st0 = gpu_ctx.render(o)
+    gpu_ctx.reserve(o, host=True)
+    gpu_ctx.reserve(o, host=False)
+    assert gpu_ctx.stats().rays == st0.rays
+    t0 = time.perf_counter()
+    gpu_ctx.reserve(o, host=True)
+    assert time.perf_counter() - t0 < 0.5
+    rgb1, bgr1, st1 = gpu_ctx.render(o)
+    assert np.array_equal(bgr1, bgr0) and np.array_equal(rgb1.view(np.uint32), rgb0.view(np.uint32))
+    assert st1.rays == st0.rays
+    with lr.Context(0) as fresh:                    # a fresh context: reserve before its first render
+        with pytest.raises(lr.RtError) as e:
+            fresh.reserve(o)
+        assert e.value.code == lr.RT_E_NOSCENE
+        fresh.upload(lr.Scene.deserialize(spec.to_text()))
+        fresh.reserve(o, host=True)
+        rgb2, bgr2, st2 = fresh.render(o)
+    assert np.array_equal(bgr2, bgr0) and np.array_equal(rgb2.view(np.uint32), rgb0.view(np.uint32))
+
+
 def test_default_spp_is_the_scenes_antialias(gpu_ctx):
     """rt_render_opts.spp = 0 (the default options) renders with the uploaded
     scene's Options.antialias (scene.rs:191-198)."""

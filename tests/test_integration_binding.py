@@ -170,7 +170,7 @@ def test_rust_structs_match_the_header_field_for_field(c_layout):
         assert rsize == size, f"{rname}: Rust size {rsize} vs sizeof({cname}) = {size}"
 
 
-def test_abi_sizes_at_version_4(c_layout):
+def test_abi_sizes_at_version_5(c_layout):
     assert c_layout["rt_render_opts"][0] == 72
     assert c_layout["rt_stats"][0] == 80
 

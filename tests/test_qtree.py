@@ -112,3 +112,17 @@ def test_not_representable_trees_are_refused():
     s.sphere((1e300, 0.0, -5.0), 1.0, scenes.phong((0.5, 0.5, 0.5), (0.3, 0.3, 0.3), 20.0, (0, 0, 0)))
     nodes, boxes, first, count, info = lr.Scene.deserialize(s.to_text()).qtree_nodes()
     assert info[0] == 0 and len(nodes) == 0
+
+
+def test_size_query_fills_info_only():
+    """cap_nodes 0 with null buffers is a size query: RT_OK and info[]
+    as the full call reports it; a buffer too small is RT_E_INVALID."""
+    import ctypes as C
+    sc = lr.Scene.deserialize(scenes.config3(32, 32).to_text())
+    info = np.zeros(3, np.int64)
+    rc = lr.lib.rt_qtree_nodes(sc.handle, 0, None, None, None, None, 0, info.ctypes.data_as(C.POINTER(C.c_int64)))
+    assert rc == lr.RT_OK and info[0] > 1
+    assert tuple(int(x) for x in info) == sc.qtree_nodes()[4]
+    with pytest.raises(lr.RtError) as e:
+        sc.qtree_nodes(cap=1)
+    assert e.value.code == lr.RT_E_INVALID

@@ -54,7 +54,7 @@ extern "C" {
 
 /* 5: rt_out_flags gained RT_OUT_FRAME_ROWS (rt_render writes a banded tile
  * straight into its rows of a whole-frame host buffer); rt_ctx_reserve added;
- * rt_kernel_family index 6 is RT_KF_COMPOSE (earlier ABI-4 builds named it
+ * rt_sqrt_check added; rt_kernel_family index 6 is RT_KF_COMPOSE (earlier ABI-4 builds named it
  * RT_KF_SHADOW); the tuning keys fuse, lists,
  * lists0, fuse_from, prefix4_kb, cam_prefix_kb, tail_from, tail_max,
  * eager_fold, fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs and
@@ -299,6 +299,11 @@ int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
  * and as the device's own f64 division -> slow[i], for n operand pairs.  Tests
  * compare both with IEEE division bit for bit.  Synchronous. */
 int rt_div_a2_check(rt_ctx* ctx, const double* x, const double* a, uint32_t n, double* fast, double* slow);
+/* Diagnostic (device): the sphere test's square root (shapes.rs:67) as the device
+ * computes it (the f64 sqrt sequence without its scaling of operands below 2^-767,
+ * DESIGN.md §4) -> fast[i], and the device's own sqrt -> slow[i].  Tests compare
+ * both with IEEE sqrt bit for bit.  Synchronous. */
+int rt_sqrt_check(rt_ctx* ctx, const double* x, uint32_t n, double* fast, double* slow);
 /* Queue sizes of the last wavefront chunk: queue[k] = rays traced at depth k
  * (generation 0: 0, the camera rays are not queued), shaded[k] = hits that
  * issued shadow queries.  Diagnostic. */
@@ -349,7 +354,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * the rows, 0 equal), sparse_out (rt_render into host memory, a one-chunk
  * wavefront render: the frame is copied after the camera pass while the
  * generations run, then only the 16-pixel row segments holding pixels whose
- * chain was still running, packed on the device).
+ * chain was still running, packed on the device), chain_on_caller (1: a
+ * one-lane render's nearest-hit chain runs on the caller's stream itself, no
+ * fork and join between hardware queues; 0: on the context's high-priority
+ * chain stream).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

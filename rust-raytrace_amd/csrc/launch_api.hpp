@@ -80,6 +80,9 @@ struct WfStreams {
     // sparse host copies (b.mark set): after generation 0 (sp_cam), stream sp_s runs the segment
     // kernels into sp_bits / sp_cnt / sp_off (then sp_ready); after the fold stream a packs the
     // flagged segments into sp_bgr / sp_rgb (null: that output is off).  sp_s null: off.
+    // lazy_tally: no wf_tally launch; the caller runs launch_tally later, when statistics are
+    // asked for (the queue sizes it reads stay in the working set until the next render)
+    bool lazy_tally = false;
     hipStream_t sp_s = nullptr;
     hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
     uint32_t *sp_bits = nullptr, *sp_cnt = nullptr, *sp_off = nullptr;
@@ -89,6 +92,9 @@ struct WfStreams {
 hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int src, int src_occ,
                             bool count, const WfStreams& ws, hipEvent_t mark, int mark_gen);
 hipError_t upload_srgb_table(const double* avg255);
+// wf_tally of one chunk (rays, shadow rays and per-generation queue sizes into b.totals /
+// b.gen_totals) on stream s: what launch_wavefront runs at the end unless ws.lazy_tally.
+hipError_t launch_tally(const FrameParams& fp, const WfBufs& b, int n_lights, int generations, hipStream_t s);
 // Sparse host copies (tuning sparse_out): pixels per row segment; after the camera pass
 // (b.mark set) segbits / rowcnt / rowoff of the chunk's rows (wf_chain_segs + wf_row_scan);
 // after the fold the flagged segments packed in row order (wf_chain_pack).
@@ -104,6 +110,8 @@ hipError_t launch_warmup(uint32_t workgroups, hipStream_t s);
 hipError_t launch_path_warmup(hipStream_t s);
 // Diagnostic: div_a2(x, sphere_k(a)) and x / (2a) on the device (rt_div_a2_check).
 hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s);
+// Diagnostic: sqrt_win(x) and sqrt(x) on the device (rt_sqrt_check).
+hipError_t launch_sqrt_probe(const double* x, uint32_t n, double* fast, double* slow, hipStream_t s);
 
 // The general path (path_kernel.hip): every material / light / camera class,
 // keyed random draws, one work-item per pixel over the HBM recursion stack.

@@ -36,7 +36,8 @@ enum TuneKey : int {
     kTuneChunkPixels, kTuneBvhLeaf, kTuneLgrid, kTuneLgridRes, kTuneSrc, kTuneSrcOcc, kTunePrefixKb2, kTuneLanes,
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
-    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneSparseOut, kTuneCount
+    kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneSparseOut,
+    kTuneChainOnCaller, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -96,6 +97,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"sparse_out", 1, 0, 1},                     // rt_render into host memory, one chunk: copy the frame after the camera
                                                  // pass, then only the 16-pixel segments holding chain pixels (§3.11;
                                                  // C3 BGR 4.00 -> 3.46-3.63 ms, RGB + BGR 8.09-8.17 -> 7.67-7.72 ms)
+    {"chain_on_caller", 0, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
+                                                 // itself (no fork / join hop between hardware queues at the start and
+                                                 // end of the render; the chain then runs at the caller stream's priority)
 };
 
 }  // namespace
@@ -269,6 +273,14 @@ struct rt_ctx {
     std::vector<LaunchInterval> tint;
     hipEvent_t fork = nullptr;
     bool wf_used = false;
+    // a one-chunk wavefront render leaves its tally (ray counts, per-generation queue sizes) to
+    // the first rt_ctx_stats / rt_ctx_generation_counts after it (flush_tally): not on the chain
+    struct PendingTally {
+        bool on = false;
+        FrameParams fp{};
+        WfBufs b{};
+        int n_lights = 0, gens = 0;
+    } tally;
     uint32_t scene_spp = 1;           // the uploaded scene's Options.antialias (rt_render_opts.spp = 0)
     hipEvent_t render_done = nullptr; // end of the last render on its stream: the next one waits for it
     bool render_pending = false;
@@ -479,6 +491,8 @@ int ensure_wf(rt_ctx* c, rt_ctx::Lane& L, uint32_t cap, uint32_t G, uint32_t R, 
     b.o_ccol = off; off = align_up(off + s_ccol, 256);
     if (off > L.bytes) {
         if (L.mem) {
+            // every render still using it is done (its chain may have run on a caller's stream)
+            if (c->render_pending) (void)hipEventSynchronize(c->render_done);
             (void)hipStreamSynchronize(L.s);
             for (hipStream_t x : L.sb) (void)hipStreamSynchronize(x);
             (void)hipFree(L.mem);
@@ -1175,6 +1189,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
     if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)
         return fail(c, RT_E_UNSUPPORTED, "the wavefront path handles at most 32 lights");
     if (!dry) {
+        c->tally.on = false;
         HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
         c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
         c->last_stream = st;
@@ -1405,12 +1420,14 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             m->used = &c->t_used;
             m->out = &c->tint;
         }
+        // the chain on the caller's stream (tuning chain_on_caller, one lane), or on the lane's own
+        // (high-priority) stream after a fork from the caller's; the b streams need no fork: their
+        // first work waits for the chain's generation 0 (near_done), which comes after it
+        const bool on_caller = c->t(kTuneChainOnCaller) != 0 && n_lanes == 1;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
-        HIP_TRY(c, hipEventRecord(c->fork, st));
-        for (int l = 0; l < n_lanes; ++l) {
-            HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
-            if (split)
-                for (int i = 0; i < n_b; ++i) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].sb[i], c->fork, 0));
+        if (!on_caller) {
+            HIP_TRY(c, hipEventRecord(c->fork, st));
+            for (int l = 0; l < n_lanes; ++l) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
         }
         for (uint32_t ci = 0; ci < n_chunks; ++ci) {
             rt_ctx::Lane& L = c->lanes[ci % n_lanes];
@@ -1421,10 +1438,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             WfBufs b = L.b;
             b.slots = tiles_x * 64 * ((f.rows + 7) / 8);
             WfStreams ws{};
-            ws.a = L.s;
+            ws.a = on_caller ? st : L.s;
             ws.nb = split ? n_b : 1;
             for (int i = 0; i < ws.nb; ++i) {
-                ws.b[i] = split ? L.sb[i] : L.s;
+                ws.b[i] = split ? L.sb[i] : ws.a;
                 ws.b_done[i] = split ? L.b_done[i] : nullptr;
                 ws.mb[i] = timed ? (split ? &marks_b[i] : &marks) : nullptr;
             }
@@ -1451,6 +1468,14 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;
+            ws.lazy_tally = n_chunks == 1 && n_lanes == 1;
+            if (ws.lazy_tally) {
+                c->tally.on = true;
+                c->tally.fp = f;
+                c->tally.b = b;
+                c->tally.n_lights = c->dsc.n_lights;
+                c->tally.gens = static_cast<int>(o->max_depth) + 2;
+            }
             ws.cam = cam;
             ws.fold_ev = c->n_bands == 0 ? nullptr : &c->band_ev[ci];
             if (c->sparse_on) {
@@ -1468,7 +1493,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                               : 0;
             HIP_TRY(c, launch_wavefront(c->dsc, f, b, src, src_occ, count, ws, L.mark, mark_gen));
         }
-        for (int l = 0; l < n_lanes; ++l) {
+        for (int l = 0; l < n_lanes && !on_caller; ++l) {
             HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));
             HIP_TRY(c, hipStreamWaitEvent(st, c->lanes[l].done, 0));
         }
@@ -1548,9 +1573,41 @@ int rt_div_a2_check(rt_ctx* c, const double* x, const double* a, uint32_t n, dou
     });
 }
 
+int rt_sqrt_check(rt_ctx* c, const double* x, uint32_t n, double* fast, double* slow) {
+    if (!c || (n && (!x || !fast || !slow))) return RT_E_INVALID;
+    if (n == 0) return RT_OK;
+    return guarded(c, [&] {
+        HIP_TRY(c, hipSetDevice(c->device));
+        const size_t bytes = static_cast<size_t>(n) * sizeof(double);
+        double* d = nullptr;
+        HIP_TRY(c, hipMalloc(&d, 3 * bytes));
+        auto body = [&]() -> int {
+            HIP_TRY(c, hipMemcpyAsync(d, x, bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_sqrt_probe(d, n, d + n, d + 2 * static_cast<size_t>(n), c->stream));
+            HIP_TRY(c, hipMemcpyAsync(fast, d + n, bytes, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(slow, d + 2 * static_cast<size_t>(n), bytes, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            return RT_OK;
+        };
+        const int rc = body();
+        (void)hipFree(d);
+        return rc;
+    });
+}
+
+// The tally a one-chunk render left pending, after that render, on the context's stream.
+static int flush_tally(rt_ctx* c) {
+    if (!c->tally.on) return RT_OK;
+    c->tally.on = false;
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->render_done, 0));
+    HIP_TRY(c, launch_tally(c->tally.fp, c->tally.b, c->tally.n_lights, c->tally.gens, c->stream));
+    return RT_OK;
+}
+
 int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = flush_tally(c); rc != RT_OK) return rc;
     unsigned long long h[kCounterWords];
     if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
     HIP_TRY(c, hipMemcpyAsync(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
@@ -1579,6 +1636,7 @@ int rt_ctx_generation_counts(rt_ctx* c, uint32_t* queue, uint32_t* shaded, int n
     if (!c || n < 0 || (n && (!queue || !shaded))) return RT_E_INVALID;
     if (!c->wf_used) return fail(c, RT_E_NOSCENE, "no wavefront render yet");
     HIP_TRY(c, hipSetDevice(c->device));
+    if (const int rc = flush_tally(c); rc != RT_OK) return rc;
     if (c->last_stream) HIP_TRY(c, hipStreamSynchronize(c->last_stream));
     unsigned long long h[kCntWords];
     HIP_TRY(c, hipMemcpyAsync(h, c->d_counters + kGenTotals, sizeof h, hipMemcpyDeviceToHost, c->stream));

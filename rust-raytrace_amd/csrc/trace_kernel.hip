@@ -1515,9 +1515,12 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     hipError_t e;
     // the tally reads only the queue sizes: on stream a while the b streams finish the last shading
-    if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
-    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);
-    if (ws.ma && (e = ws.ma->mark(ws.a, kKfTally)) != hipSuccess) return e;
+    // (or later, when statistics are asked for: ws.lazy_tally)
+    if (!ws.lazy_tally) {
+        if (ws.ma && (e = ws.ma->begin(ws.a)) != hipSuccess) return e;
+        hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);
+        if (ws.ma && (e = ws.ma->mark(ws.a, kKfTally)) != hipSuccess) return e;
+    }
     for (int i = 0; i < ws.nb; ++i) {
         if (ws.b[i] == ws.a) continue;
         if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
@@ -1539,6 +1542,11 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     // every row of the chunk is final now (the fold runs in chain order, not by rows)
     if (ws.fold_ev && (e = hipEventRecord(*ws.fold_ev, ws.a)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_tally(const FrameParams& fp, const WfBufs& b, int n_lights, int generations, hipStream_t s) {
+    hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, n_lights, generations);
     return hipGetLastError();
 }
 
@@ -1603,6 +1611,21 @@ __global__ __launch_bounds__(256) void div_a2_probe(const double* x, const doubl
         fast[i] = div_a2(x[i], k);
         slow[i] = x[i] / (2.0 * a[i]);
     }
+}
+
+// Diagnostic (rt_sqrt_check): the sphere test's square root as sphere_roots computes it
+// (sqrt_win) and as the compiler's own f64 sqrt, side by side.
+__global__ __launch_bounds__(256) void sqrt_probe(const double* x, uint32_t n, double* fast, double* slow) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        fast[i] = sqrt_win(x[i]);
+        slow[i] = sqrt(x[i]);
+    }
+}
+
+hipError_t launch_sqrt_probe(const double* x, uint32_t n, double* fast, double* slow, hipStream_t s) {
+    const uint32_t blocks = std::max(1u, std::min(4096u, (n + 255u) / 256u));
+    hipLaunchKernelGGL(sqrt_probe, dim3(blocks), dim3(256), 0, s, x, n, fast, slow);
+    return hipGetLastError();
 }
 
 hipError_t launch_div_a2_probe(const double* x, const double* a, uint32_t n, double* fast, double* slow, hipStream_t s) {

@@ -128,6 +128,7 @@ def _load():
                                      C.c_size_t, P(C.c_int64)]),
         "rt_div_a2_check": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), C.c_uint32, P(C.c_double),
                                       P(C.c_double)]),
+        "rt_sqrt_check": (C.c_int, [C.c_void_p, P(C.c_double), C.c_uint32, P(C.c_double), P(C.c_double)]),
         "rt_ctx_set_tuning": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
         "rt_ctx_get_tuning": (C.c_int, [C.c_void_p, C.c_char_p, P(C.c_int64)]),
         "rt_tuning_key": (C.c_char_p, [C.c_int]),
@@ -464,6 +465,18 @@ class Context:
         P = C.POINTER(C.c_double)
         _check(lib.rt_div_a2_check(self._h, x.ctypes.data_as(P), a.ctypes.data_as(P), x.size, fast.ctypes.data_as(P),
                                    slow.ctypes.data_as(P)), self._h)
+        return fast, slow
+
+    def sqrt_check(self, x):
+        """Diagnostic: (the sphere test's sqrt as the device computes it, the device's own
+        f64 sqrt) for a float64 array x (rt_sqrt_check)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        assert x.ndim == 1
+        fast = np.empty_like(x)
+        slow = np.empty_like(x)
+        P = C.POINTER(C.c_double)
+        _check(lib.rt_sqrt_check(self._h, x.ctypes.data_as(P), x.size, fast.ctypes.data_as(P), slow.ctypes.data_as(P)),
+               self._h)
         return fast, slow
 
     def kernel_times(self):

@@ -67,3 +67,43 @@ def test_division_by_2a_is_ieee_bit_for_bit(gpu_ctx):
     ex = (x.view(np.uint64) >> np.uint64(52)) & np.uint64(0x7FF)
     inside = (ea2 >= 923) & (ea2 <= 1123) & (ex >= 123) & (ex <= 1622)
     assert inside.sum() > 5_000_000 and (~inside).sum() > 1_000_000
+
+
+def test_sphere_sqrt_is_ieee_bit_for_bit(gpu_ctx):
+    """The sphere test's square root (shapes.rs:67) as sphere_roots computes it:
+    sqrt_win, the compiler's f64 sqrt sequence without its scaling of operands
+    below 2^-767 (and its +-0 / +inf fixup), inside [2^-767, +inf), the full
+    sqrt outside (trace_common.hpp).  Against the device's own
+    sqrt and numpy's (IEEE) on > 10^7 operands: every exponent, both edges of
+    the window and just outside, denormals, +-0, infinities, NaNs, negatives."""
+    rng = np.random.default_rng(20261018)
+    n = 1 << 21
+
+    def f64(exp, size):
+        mant = rng.integers(0, 1 << 52, size=size, dtype=np.uint64)
+        e = np.broadcast_to(np.asarray(exp, dtype=np.uint64), (size,))
+        return ((e << np.uint64(52)) | mant).view(np.float64)
+
+    xs = [f64(rng.integers(1023 - 80, 1023 + 80, size=n), n),        # the renders' discriminants
+          f64(rng.integers(0, 2047, size=2 * n), 2 * n)]              # every exponent, denormals included
+    for e in range(252, 261):                                         # the window's lower edge 2^-767 (biased 256)
+        xs.append(f64(e, n // 4))
+    xs.append(f64(2046, n // 4))                                      # the largest finite binade
+    # perfect squares and their neighbours (round-to-nearest ties do not exist for sqrt, but exact roots do)
+    r = rng.uniform(1.0, 2.0 ** 26, n).astype(np.float64).round()
+    sq = r * r
+    xs += [sq, np.nextafter(sq, 0.0), np.nextafter(sq, np.inf)]
+    xs.append(-np.abs(f64(rng.integers(0, 2047, size=n // 4), n // 4)))
+    xs.append(np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, 2.0 ** -767, np.nextafter(2.0 ** -767, 0.0),
+                        np.nextafter(2.0 ** -767, 1.0), 1.7976931348623157e308, 2.2250738585072014e-308, 1.0, 4.0]))
+    x = np.concatenate(xs)
+    assert x.size >= 10_000_000
+    fast, slow = gpu_ctx.sqrt_check(x)
+    with np.errstate(all="ignore"):
+        ref = np.sqrt(x)
+    ok_slow = _bits_equal(slow, ref)
+    assert ok_slow.all(), f"device sqrt differs from IEEE on {(~ok_slow).sum()} operands, e.g. {x[~ok_slow][:3]}"
+    ok = _bits_equal(fast, slow)
+    assert ok.all(), f"sqrt_win differs from sqrt on {(~ok).sum()} operands, e.g. {x[~ok][:3]}"
+    inside = (x >= 2.0 ** -767) & np.isfinite(x)
+    assert inside.sum() > 5_000_000 and (~inside).sum() > 1_000_000

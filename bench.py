@@ -493,9 +493,9 @@ def main():
     # rt_ctx_reserve (outside the timed region, like the upload): the schedule's streams and hardware
     # queues, the working set and the queues' scratch, so that the first frame runs warm
     reserve_ms = []
-    for c in ctxs:
+    for c, s_ in zip(ctxs, streams):
         t0r = time.perf_counter()
-        c.reserve(opts)
+        c.reserve(opts, stream_ptr=s_.cuda_stream)
         reserve_ms.append((time.perf_counter() - t0r) * 1e3)
     # the first two frames after it, against each other: what a process that renders one frame (as
     # main.rs does) pays for its render once ctx_create, the upload and the reserve are done

@@ -290,8 +290,10 @@ int rt_render_device(rt_ctx* ctx, const rt_render_opts* opts, void* d_rgb, void*
  * allocates nothing: a process that renders one frame (main.rs:13-60) calls
  * it after rt_scene_upload, e.g. while it parses or opens its output.  Needs
  * an uploaded scene (the schedule depends on it); RT_E_NOMEM if the working
- * set does not fit even as the smallest chunks. */
-int rt_ctx_reserve(rt_ctx* ctx, const rt_render_opts* opts, int host);
+ * set does not fit even as the smallest chunks.  stream: the hipStream_t the
+ * rt_render_device calls will be issued on (its hardware queue is set up too;
+ * NULL = the context's own stream, which rt_render uses). */
+int rt_ctx_reserve(rt_ctx* ctx, const rt_render_opts* opts, int host, void* stream);
 int rt_ctx_stats(rt_ctx* ctx, rt_stats* stats);
 /* Diagnostic (device): the sphere test's division t = x / (2a) (shapes.rs:68,75)
  * computed as the device computes it (the per-ray reciprocal of 2a finished with
@@ -357,7 +359,9 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * chain was still running, packed on the device), chain_on_caller (1: a
  * one-lane render's nearest-hit chain runs on the caller's stream itself, no
  * fork and join between hardware queues; 0: on the context's high-priority
- * chain stream).
+ * chain stream), copy_engine (rt_render's device -> host copies: 0
+ * hipMemcpyAsync, e = 1..16 the device's SDMA engine e - 1 driven directly,
+ * -1 the engine the runtime prefers).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

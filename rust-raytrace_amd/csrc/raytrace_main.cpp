@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
             o.max_depth = a.max_depth; o.spp = spp; o.algo = a.algo; o.jitter = a.jitter; o.seed = a.seed;
             o.flags = RT_OUT_BGR_U8 | RT_OUT_FRAME_ROWS; o.bgr_pitch = pitch;
             o.band = band; o.band_stride = G; o.band_phase = g; o.tile_h = my_full * band;
-            if (o.tile_h && ((rc[g] = rt_ctx_reserve(ctx, &o, 1)) != RT_OK ||
+            if (o.tile_h && ((rc[g] = rt_ctx_reserve(ctx, &o, 1, nullptr)) != RT_OK ||
                              (rc[g] = rt_render(ctx, &o, nullptr, frame.data(), &st[g])) != RT_OK)) {
                 errs[g] = rt_last_error(ctx); rt_ctx_destroy(ctx); return;
             }

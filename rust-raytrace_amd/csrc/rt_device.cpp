@@ -2,6 +2,8 @@
 // See include/raytrace_amd.h for the contract and the reference interfaces
 // these replace.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <cmath>
 #include <cstdio>
@@ -37,7 +39,7 @@ enum TuneKey : int {
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
     kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneSparseOut,
-    kTuneChainOnCaller, kTuneCount
+    kTuneChainOnCaller, kTuneCopyEngine, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -97,6 +99,9 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"sparse_out", 1, 0, 1},                     // rt_render into host memory, one chunk: copy the frame after the camera
                                                  // pass, then only the 16-pixel segments holding chain pixels (§3.11;
                                                  // C3 BGR 4.00 -> 3.46-3.63 ms, RGB + BGR 8.09-8.17 -> 7.67-7.72 ms)
+    {"copy_engine", 0, -1, 16},                  // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
+                                                 // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
+                                                 // (hsa_amd_memory_async_copy_on_engine), -1 the preferred engine
     {"chain_on_caller", 0, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
                                                  // itself (no fork / join hop between hardware queues at the start and
                                                  // end of the render; the chain then runs at the caller stream's priority)
@@ -314,6 +319,13 @@ struct rt_ctx {
     hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
     static constexpr int kSpRanges = 16;   // row ranges of the packed copy, each scattered as it lands
     hipEvent_t sp_ev[kSpRanges] = {};
+    // copies on an SDMA engine (tuning copy_engine): the device's and a CPU agent, the engine, and
+    // one completion signal per staging slice / packed range / direct copy batch
+    int sdma_state = 0;                    // 0 not set up, 1 usable, -1 unavailable
+    hsa_agent_t hsa_gpu{}, hsa_cpu{};
+    uint32_t sdma_avail = 0, sdma_pref = 0;
+    static constexpr int kSdmaSignals = kRing + kSpRanges + 1;
+    hsa_signal_t sdma_sig[kSdmaSignals] = {};
     int64_t tune[kTuneCount];
     std::string err;
     rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
@@ -610,6 +622,11 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->sp_cam) (void)hipEventDestroy(c->sp_cam);
     if (c->sp_ready) (void)hipEventDestroy(c->sp_ready);
     if (c->d_sp) (void)hipFree(c->d_sp);
+    if (c->sdma_state == 1) {
+        for (hsa_signal_t sg : c->sdma_sig)
+            if (sg.handle) (void)hsa_signal_destroy(sg);
+        (void)hsa_shut_down();             // balances sdma_setup's hsa_init
+    }
     if (c->h_sp_meta) (void)hipHostFree(c->h_sp_meta);
     if (c->h_sp_pk) (void)hipHostFree(c->h_sp_pk);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -1663,6 +1680,98 @@ int rt_ctx_kernel_times(rt_ctx* c, double* ms, uint32_t* launches, int n) {
     return RT_OK;
 }
 
+// ---- SDMA copy engines (tuning copy_engine) --------------------------------------------
+// hipMemcpyAsync moves rt_render's frame to the host at ~29 GB/s on the boxes measured
+// (tools/sdma_probe.hip: a blit kernel or the runtime's choice of engine), one SDMA engine
+// driven directly at ~53 GB/s.  The engine's queue does not see HIP events, so the host waits
+// for the event a copy depends on (hipEventSynchronize) before it queues the copy; each batch
+// of copies completes a signal the host waits on.
+static hsa_status_t sdma_find_agents(hsa_agent_t a, void* data) {
+    auto* c = static_cast<rt_ctx*>(data);
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && c->hsa_cpu.handle == 0) c->hsa_cpu = a;
+    if (t == HSA_DEVICE_TYPE_GPU && c->hsa_gpu.handle == 0) {
+        // the HIP device's agent: same PCI domain, bus and device
+        uint32_t bdf = 0, dom = 0;
+        int bus = -1, dev = -1, hdom = -1;
+        (void)hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf);
+        (void)hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &dom);
+        if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device) == hipSuccess &&
+            hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->device) == hipSuccess &&
+            hipDeviceGetAttribute(&hdom, hipDeviceAttributePciDomainID, c->device) == hipSuccess &&
+            static_cast<int>((bdf >> 8) & 0xFF) == bus && static_cast<int>((bdf >> 3) & 0x1F) == dev &&
+            static_cast<int>(dom) == hdom)
+            c->hsa_gpu = a;
+        (void)hipGetLastError();
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+// Set up once per context; false if the device has no usable engine (the HIP path is used).
+static bool sdma_setup(rt_ctx* c) {
+    if (c->sdma_state) return c->sdma_state == 1;
+    c->sdma_state = -1;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return false;
+    bool ok = hsa_iterate_agents(sdma_find_agents, c) == HSA_STATUS_SUCCESS && c->hsa_gpu.handle && c->hsa_cpu.handle &&
+              hsa_amd_memory_copy_engine_status(c->hsa_cpu, c->hsa_gpu, &c->sdma_avail) == HSA_STATUS_SUCCESS &&
+              c->sdma_avail != 0;
+    if (ok && hsa_amd_memory_get_preferred_copy_engine(c->hsa_cpu, c->hsa_gpu, &c->sdma_pref) != HSA_STATUS_SUCCESS)
+        c->sdma_pref = 0;
+    for (int i = 0; ok && i < rt_ctx::kSdmaSignals; ++i) ok = hsa_signal_create(0, 0, nullptr, &c->sdma_sig[i]) == HSA_STATUS_SUCCESS;
+    if (!ok) {
+        for (hsa_signal_t& sg : c->sdma_sig)
+            if (sg.handle) { (void)hsa_signal_destroy(sg); sg.handle = 0; }
+        (void)hsa_shut_down();
+        return false;
+    }
+    c->sdma_state = 1;
+    return true;
+}
+
+// The engine rt_render's copies use now (0: hipMemcpyAsync).
+static uint32_t sdma_engine(rt_ctx* c) {
+    const int64_t e = c->t(kTuneCopyEngine);
+    if (e == 0 || !sdma_setup(c)) return 0;
+    uint32_t bit = 0;
+    if (e > 0) bit = 1u << (e - 1);
+    else {
+        const uint32_t m = (c->sdma_pref & c->sdma_avail) ? (c->sdma_pref & c->sdma_avail) : c->sdma_avail;
+        bit = m & (~m + 1u);
+    }
+    return (bit & c->sdma_avail) ? bit : 0;
+}
+
+// Wait until signal `si` is 0 (every copy counted on it done); a copy that has not completed
+// after 30 s is an error, not a hang.
+static int sdma_wait(rt_ctx* c, int si) {
+    static const uint64_t hint = [] {
+        uint64_t f = 0;
+        return hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f ? f / 1000 : 1000000;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hsa_signal_wait_scacquire(c->sdma_sig[si], HSA_SIGNAL_CONDITION_EQ, 0, hint, HSA_WAIT_STATE_ACTIVE) != 0)
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+            return fail(c, RT_E_HIP, "an SDMA copy did not complete");
+    return RT_OK;
+}
+
+// Device -> pinned host copy on the engine, counted on signal `si` (one more pending copy); the
+// caller waits with sdma_wait.
+static int sdma_copy(rt_ctx* c, uint32_t engine, int si, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return RT_OK;
+    hsa_signal_t sg = c->sdma_sig[si];
+    hsa_signal_add_screlease(sg, 1);
+    const hsa_status_t st = hsa_amd_memory_async_copy_on_engine(dst, c->hsa_cpu, src, c->hsa_gpu, bytes, 0, nullptr, sg,
+                                                                static_cast<hsa_amd_sdma_engine_id_t>(engine), true);
+    if (st != HSA_STATUS_SUCCESS) {
+        hsa_signal_subtract_screlease(sg, 1);
+        (void)sdma_wait(c, si);              // the copies queued before it still complete
+        return fail(c, RT_E_HIP, "hsa_amd_memory_async_copy_on_engine failed (" + std::to_string(st) + ")");
+    }
+    return RT_OK;
+}
+
 // Where rt_render puts a device row (RT_OUT_FRAME_ROWS or not): local row j of the tile, dev_pitch
 // bytes apart on the device, row_bytes of it copied, lands at host byte offset host_row(j) *
 // host_pitch + host_x.  A plain tile: host_row(j) = j, the host rows laid out as the device's; a
@@ -1691,10 +1800,11 @@ struct OutMap {
 // filling slices ahead while the host pool empties them in order into their
 // host rows.  wait = false (sparse copies): no wait on the bands, the copy
 // stream's order alone (its segment kernels follow the camera pass).
-static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, uint32_t rows, bool wait = true) {
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, uint32_t rows, hipEvent_t after = nullptr) {
     if (!rows || !m.row_bytes) return RT_OK;
     int rc = ensure_copy_stream(c);
     if (rc != RT_OK) return rc;
+    const uint32_t engine = sdma_engine(c);          // 0: hipMemcpyAsync on the copy stream
     const auto* s8 = static_cast<const uint8_t*>(src);
     auto* d8 = static_cast<uint8_t*>(dst);
     hipPointerAttribute_t attr{};
@@ -1722,20 +1832,50 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, 
             j += n;
         }
     }
+    // a piece is copied once its chunk band is final (band_ev; the whole render: render_done),
+    // or after `after`: the copy stream waits for the event, the host for an engine's copies
+    auto band_event = [&](int bi) { return after ? after : c->n_bands > 0 ? c->band_ev[bi] : c->render_done; };
     auto wait_band = [&](int bi) -> hipError_t {
-        if (!wait) return hipSuccess;
-        return hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[bi] : c->render_done, 0);
+        return engine ? hipEventSynchronize(band_event(bi)) : hipStreamWaitEvent(c->copy_stream, band_event(bi), 0);
     };
-    if (pinned) {
+    if (pinned && engine && contig) {                  // every piece straight into the caller's rows
+        constexpr int si = rt_ctx::kSdmaSignals - 1;
         int last = -1;
         for (const Piece& pc : pieces) {
             if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
-            if (contig)
-                HIP_TRY(c, hipMemcpyAsync(d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
-                                          hipMemcpyDeviceToHost, c->copy_stream));
-            else
+            if ((rc = sdma_copy(c, engine, si, d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch)) != RT_OK)
+                return rc;
+        }
+        return sdma_wait(c, si);
+    }
+    if (pinned) {
+        int last = -1;
+        for (size_t i = 0; i < pieces.size();) {
+            const Piece& pc = pieces[i];
+            if (pc.band != last) {                     // (the rows of a partial-width tile: 2D copies on the stream)
+                HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, band_event(pc.band), 0));
+                last = pc.band;
+            }
+            if (contig) {
+                // a regular run of pieces (a tile's row bands: equal sizes, equal steps on both sides) as
+                // one 2D copy, one piece per row of it
+                size_t k = i + 1;
+                const size_t ds = pieces.size() > i + 1 ? m.host_off(pieces[i + 1].j0) - m.host_off(pc.j0) : 0;
+                while (k < pieces.size() && pieces[k].band == pc.band && pieces[k].n == pc.n &&
+                       pieces[k].j0 == pc.j0 + (k - i) * pc.n && m.host_off(pieces[k].j0) == m.host_off(pc.j0) + (k - i) * ds)
+                    ++k;
+                if (k - i > 1)
+                    HIP_TRY(c, hipMemcpy2DAsync(d8 + m.host_off(pc.j0), ds, s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
+                                                pc.n * m.dev_pitch, k - i, hipMemcpyDeviceToHost, c->copy_stream));
+                else
+                    HIP_TRY(c, hipMemcpyAsync(d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
+                                              hipMemcpyDeviceToHost, c->copy_stream));
+                i = k;
+            } else {
                 HIP_TRY(c, hipMemcpy2DAsync(d8 + m.host_off(pc.j0), m.host_pitch, s8 + pc.j0 * m.dev_pitch, m.dev_pitch,
                                             m.row_bytes, pc.n, hipMemcpyDeviceToHost, c->copy_stream));
+                ++i;
+            }
         }
         HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
         return RT_OK;
@@ -1759,13 +1899,22 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, 
             const Piece& pc = pieces[issued];
             if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
             const int slot = static_cast<int>(issued % kRing);
-            HIP_TRY(c, hipMemcpyAsync(c->pin[slot], s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch, hipMemcpyDeviceToHost,
-                                      c->copy_stream));
-            HIP_TRY(c, hipEventRecord(c->pin_ev[slot], c->copy_stream));
+            if (engine) {
+                if ((rc = sdma_copy(c, engine, slot, c->pin[slot], s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch)) != RT_OK)
+                    return rc;
+            } else {
+                HIP_TRY(c, hipMemcpyAsync(c->pin[slot], s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch, hipMemcpyDeviceToHost,
+                                          c->copy_stream));
+                HIP_TRY(c, hipEventRecord(c->pin_ev[slot], c->copy_stream));
+            }
             ++issued;
         }
         const int slot = static_cast<int>(drained % kRing);
-        HIP_TRY(c, hipEventSynchronize(c->pin_ev[slot]));
+        if (engine) {
+            if ((rc = sdma_wait(c, slot)) != RT_OK) return rc;
+        } else {
+            HIP_TRY(c, hipEventSynchronize(c->pin_ev[slot]));
+        }
         const Piece& pc = pieces[drained];
         const auto* from = static_cast<const uint8_t*>(c->pin[slot]);
         if (!m.frame && contig) {
@@ -1811,8 +1960,9 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     auto* h_bits = h_off + (rows + 1);
     HIP_TRY(c, hipMemcpyAsync(h_off, c->d_sp_off, s_off, hipMemcpyDeviceToHost, c->copy_stream));
     HIP_TRY(c, hipMemcpyAsync(h_bits, c->d_sp_bits, s_bits, hipMemcpyDeviceToHost, c->copy_stream));
-    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, rows, false)) != RT_OK) return rc;
-    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, rows, false)) != RT_OK) return rc;
+    // the frame as the camera pass left it (sp_ready: after the segment kernels, which follow the camera pass)
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, rows, c->sp_ready)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, rows, c->sp_ready)) != RT_OK) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->copy_stream));      // (the offsets and bits were queued first)
     const double t_frame = us();
     const uint64_t total = h_off[rows];
@@ -1821,12 +1971,25 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     if ((rc = ensure_pinned(c, c->h_sp_pk, c->h_sp_pk_cap, std::max<size_t>(1, pk_b + pk_r))) != RT_OK) return rc;
     auto* hb = static_cast<uint8_t*>(c->h_sp_pk);
     auto* hr = reinterpret_cast<float*>(hb + pk_b);
-    HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, c->n_bands > 0 ? c->band_ev[0] : c->render_done, 0));
+    // the packed segments once the render is done: on the copy stream after its end event, or on the
+    // engine once the host has seen it, in row ranges, each with its own event / signal
+    const hipEvent_t done = c->n_bands > 0 ? c->band_ev[0] : c->render_done;
+    const uint32_t engine = sdma_engine(c);
+    if (engine) HIP_TRY(c, hipEventSynchronize(done));
+    else HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, done, 0));
     const int nr = static_cast<int>(std::min<uint32_t>(rt_ctx::kSpRanges, rows));
     auto r_at = [&](int j) { return static_cast<uint32_t>(static_cast<uint64_t>(rows) * j / nr); };
     for (int j = 0; j < nr; ++j) {
-        if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
         const uint64_t a = h_off[r_at(j)], e = h_off[r_at(j + 1)];
+        if (engine) {
+            if (e > a && out_bgr && (rc = sdma_copy(c, engine, kRing + j, hb + a * seg_b, c->d_sp_bgr + a * seg_b, (e - a) * seg_b)) != RT_OK)
+                return rc;
+            if (e > a && out_rgb &&
+                (rc = sdma_copy(c, engine, kRing + j, hr + a * 3 * kSegPx, c->d_sp_rgb + a * 3 * kSegPx, (e - a) * seg_r)) != RT_OK)
+                return rc;
+            continue;
+        }
+        if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
         if (e > a && out_bgr)
             HIP_TRY(c, hipMemcpyAsync(hb + a * seg_b, c->d_sp_bgr + a * seg_b, (e - a) * seg_b, hipMemcpyDeviceToHost, c->copy_stream));
         if (e > a && out_rgb)
@@ -1856,7 +2019,11 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     // each range scattered by the pool as soon as it has landed (the later ones still in flight)
     double t_first = 0.0;
     for (int j = 0; j < nr; ++j) {
-        HIP_TRY(c, hipEventSynchronize(c->sp_ev[j]));
+        if (engine) {
+            if ((rc = sdma_wait(c, kRing + j)) != RT_OK) return rc;
+        } else {
+            HIP_TRY(c, hipEventSynchronize(c->sp_ev[j]));
+        }
         if (j == 0) t_first = us();
         const uint32_t ra = r_at(j), rb = r_at(j + 1);
         const size_t parts = std::min<size_t>(HostCopyPool::kParts, rb - ra);
@@ -1959,7 +2126,7 @@ int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_b
 
 // rt_ctx_reserve: render_device's allocations and streams without its launches (dry), plus, for
 // rt_render (host), the device frame, the staging slices and the sparse copies' pinned buffers.
-static int reserve(rt_ctx* c, const rt_render_opts* o, int host) {
+static int reserve(rt_ctx* c, const rt_render_opts* o, int host, void* stream) {
     if (!c->has_scene) return fail(c, RT_E_NOSCENE, "no scene uploaded");
     uint32_t spp, band, stride, pitch;
     int rc = check_opts(c, o, spp, band, stride, pitch);
@@ -1968,7 +2135,7 @@ static int reserve(rt_ctx* c, const rt_render_opts* o, int host) {
     rt_render_opts oo = *o;
     if (!host) {
         if (o->flags & RT_OUT_FRAME_ROWS) return fail(c, RT_E_INVALID, "RT_OUT_FRAME_ROWS is for rt_render's host buffers");
-        return render_device(c, &oo, nullptr, nullptr, nullptr, true);
+        return render_device(c, &oo, nullptr, nullptr, stream, true);
     }
     OutMap mr, mb;
     uint32_t dev_pitch = pitch;
@@ -1999,12 +2166,18 @@ static int reserve(rt_ctx* c, const rt_render_opts* o, int host) {
         for (int j = 0; j < rt_ctx::kSpRanges; ++j)
             if (!c->sp_ev[j]) HIP_TRY(c, hipEventCreateWithFlags(&c->sp_ev[j], hipEventDisableTiming));
     }
+    // the copy engine's queue is set up at its first copy (tens of ms): one small copy now
+    if (const uint32_t engine = sdma_engine(c)) {
+        constexpr int si = rt_ctx::kSdmaSignals - 1;
+        if ((rc = sdma_copy(c, engine, si, c->pin[0], c->d_counters, 4096)) != RT_OK || (rc = sdma_wait(c, si)) != RT_OK)
+            return rc;
+    }
     return RT_OK;
 }
 
-int rt_ctx_reserve(rt_ctx* c, const rt_render_opts* o, int host) {
+int rt_ctx_reserve(rt_ctx* c, const rt_render_opts* o, int host, void* stream) {
     if (!c || !o) return RT_E_INVALID;
-    return guarded(c, [&] { return reserve(c, o, host); });
+    return guarded(c, [&] { return reserve(c, o, host, stream); });
 }
 
 int rt_ctx_set_tuning(rt_ctx* c, const char* key, int64_t value) {

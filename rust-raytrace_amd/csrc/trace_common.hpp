@@ -189,22 +189,6 @@ __device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, const
     return disc > 0.0 && sphere_roots(b, disc, k, t);
 }
 
-// For disc > 0: true only if the t sphere_roots would return is certainly > T (the
-// best t so far, >= 0), so the sphere cannot win the nearest hit (ties included), and
-// its square root and division can be skipped.  With u = 2^-53 (one rounding of each
-// of sqrt, -b - sq and the division), the computed t1 exceeds T whenever
-// -b - T a2 (1 + 3u) > sqrt(disc) (1 + u); the f64 test below asks for w > 0 and
-// w^2 > disc (1 + 2^-48), with w = -b - T a2 (1 + 2^-50) lowered by 2^-50 (|b| + T a2)
-// for its own roundings (margins of 8u and more, each rounding of the test itself
-// <= u; w > 2^-400 keeps every term of the test a normal number, where those
-// relative bounds hold).  Then t1 > 0, so t1 is the reported t (t2 is never
-// consulted).  T = inf, NaN operands and overflow to inf all answer false.
-__device__ __forceinline__ bool sphere_beyond(double b, double disc, const SphK& k, double T) {
-    const double ta = T * k.a2;
-    const double w = ((-b) - ta * (1.0 + 0x1p-50)) - (fabs(b) + ta) * 0x1p-50;
-    return w > 0x1p-400 && w * w > disc * (1.0 + 0x1p-48);
-}
-
 // shapes.rs:100-112: t = n.(p - o) / n.d ; None iff t <= 0 (a NaN t is a hit).
 __device__ __forceinline__ bool plane_t(const DevPlane& p, const Ray& r, double& t) {
     const double ex = p.px - r.ox, ey = p.py - r.oy, ez = p.pz - r.oz;
@@ -658,12 +642,6 @@ __device__ __forceinline__ Hit nearest_bvh(const DevScene& sc, const BvhView& v,
 // statement is the masked push of the far child, then tests its leaf, then
 // pops past the entries the current best rules out.  Same visiting order,
 // culling and result as nearest_bvh.
-#ifndef RT_LEAF2
-#define RT_LEAF2 0
-#endif
-#ifndef RT_TSKIP
-#define RT_TSKIP 0
-#endif
 template <bool kCount = false, int kNodes = 0, int kReg = 0, int kCompactBits = 0>
 __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView& v, const Ray& r, Work* w = nullptr) {
     Hit h = nearest_planes(sc, r);
@@ -758,40 +736,6 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
         if (cur != kNone) {
             const int first = (~cur) >> 3, cnt = ((~cur) & 7) + 1;
             if constexpr (kCount) w->spheres += cnt;
-#if RT_LEAF2
-            // the leaf's spheres two at a time: both discriminants first (two independent f64
-            // chains, both sphere loads in flight together), then the square root and division
-            // only for the spheres with disc > 0 that may still win (sphere_beyond), one per
-            // lane per round: a wave runs as many rounds as its busiest lane needs, not one per
-            // sphere slot in which any lane has a hit
-            for (int k0 = first; k0 < first + cnt; k0 += 2) {
-                RT_WSTEP(1);
-                const bool two = k0 + 1 < first + cnt;
-                const DevSphere s0 = v.sph[k0], s1 = v.sph[two ? k0 + 1 : k0];
-                double b0, b1;
-                const double d0 = sphere_disc(s0, r, sk, b0), d1 = sphere_disc(s1, r, sk, b1);
-                bool p0 = d0 > 0.0, p1 = two && d1 > 0.0;
-#if RT_TSKIP
-                if (h.obj != INT32_MAX) {          // a best t exists: skip the spheres that cannot reach it
-                    p0 = p0 && !sphere_beyond(b0, d0, sk, h.t);
-                    p1 = p1 && !sphere_beyond(b1, d1, sk, h.t);
-                }
-#endif
-                while (p0 || p1) {
-                    const bool use0 = p0;
-                    const int k = use0 ? k0 : k0 + 1;
-                    double t;
-                    if (sphere_roots(use0 ? b0 : b1, use0 ? d0 : d1, sk, t)) {
-                        const int32_t obj = v.obj[k];
-                        if (t < h.t || (t == h.t && obj < h.obj)) {
-                            h.t = t; h.obj = obj; h.prim = k;
-                            tlim = t_limit(rb, t);
-                        }
-                    }
-                    if (use0) p0 = false; else p1 = false;
-                }
-            }
-#else
             for (int k = first; k < first + cnt; ++k) {
                 RT_WSTEP(1);
                 double t;
@@ -803,7 +747,6 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
                     }
                 }
             }
-#endif
         }
         RT_WSTAMP(q2);
         cur = kNone;

@@ -116,7 +116,7 @@ def _load():
         "rt_render_opts_default": (None, [P(rt_render_opts), C.c_uint32, C.c_uint32]),
         "rt_render": (C.c_int, [C.c_void_p, P(rt_render_opts), P(C.c_float), P(C.c_uint8), P(rt_stats)]),
         "rt_render_device": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_void_p, C.c_void_p, C.c_void_p]),
-        "rt_ctx_reserve": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_int]),
+        "rt_ctx_reserve": (C.c_int, [C.c_void_p, P(rt_render_opts), C.c_int, C.c_void_p]),
         "rt_ctx_stats": (C.c_int, [C.c_void_p, P(rt_stats)]),
         "rt_ctx_generation_counts": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_int]),
         "rt_ctx_kernel_times": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint32), C.c_int]),
@@ -438,10 +438,10 @@ class Context:
         _check(lib.rt_render_device(self._h, C.byref(opts), C.c_void_p(d_rgb_ptr or 0),
                                     C.c_void_p(d_bgr_ptr or 0), C.c_void_p(stream_ptr or 0)), self._h)
 
-    def reserve(self, opts, host=False):
+    def reserve(self, opts, host=False, stream_ptr=None):
         """rt_ctx_reserve: allocate and warm up everything a render with opts needs (host: rt_render's
-        buffers too), so that render runs warm."""
-        _check(lib.rt_ctx_reserve(self._h, C.byref(opts), 1 if host else 0), self._h)
+        buffers too; stream_ptr: the stream render_device will be called with), so that render runs warm."""
+        _check(lib.rt_ctx_reserve(self._h, C.byref(opts), 1 if host else 0, C.c_void_p(stream_ptr or 0)), self._h)
 
     def stats(self):
         st = rt_stats()

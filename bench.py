@@ -326,7 +326,7 @@ def frame_gather(dist, world, rank, ctx, lr, W, H, pitch, common, steps, red_dev
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 ms = t.item()
             out[key] = ms
-        del rgb, bgr
+        del rgb, bgr, outs               # every view of the shared frame, before its mapping closes
     finally:
         if world > 1:
             dist.barrier()

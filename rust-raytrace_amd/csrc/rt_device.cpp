@@ -102,9 +102,10 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"copy_engine", 0, -1, 16},                  // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
                                                  // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
                                                  // (hsa_amd_memory_async_copy_on_engine), -1 the preferred engine
-    {"chain_on_caller", 0, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
+    {"chain_on_caller", 1, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
                                                  // itself (no fork / join hop between hardware queues at the start and
-                                                 // end of the render; the chain then runs at the caller stream's priority)
+                                                 // end of the render; the chain then runs at the caller stream's priority;
+                                                 // round 6, same box: C3 2.916 vs 2.928 ms, 8-way share 0.706 vs 0.713 ms)
 };
 
 }  // namespace

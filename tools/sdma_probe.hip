@@ -84,8 +84,6 @@ int main(int argc, char** argv) {
         }
         hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
     };
-    int first_engine = 0;
-    for (int b = 0; b < 16; ++b) if (emask & (1u << b)) { first_engine = 1 << b; break; }
 
     const int iters = 200000;
     const int blocks = 256 * 8;
@@ -122,11 +120,14 @@ int main(int argc, char** argv) {
         hsa_copy(h, 0);
         t = ms_since(t0);
         std::printf("hsa async copy -> hipHostMalloc:   %.3f ms  %.1f GB/s\n", t, bytes / t / 1e6);
-        if (first_engine) {
-            t0 = Clock::now();
-            hsa_copy(h, first_engine);
-            t = ms_since(t0);
-            std::printf("hsa copy on engine 0x%x -> pinned:  %.3f ms  %.1f GB/s\n", first_engine, t, bytes / t / 1e6);
+        for (int b = 0; b < 16; ++b) {                 // every available engine (its first use sets up its queue)
+            if (!(emask & (1u << b))) continue;
+            for (int k = 0; k < 2; ++k) {
+                t0 = Clock::now();
+                hsa_copy(h, 1 << b);
+                t = ms_since(t0);
+                if (k == 1) std::printf("hsa copy on engine 0x%x -> pinned:  %.3f ms  %.1f GB/s\n", 1 << b, t, bytes / t / 1e6);
+            }
         }
         t0 = Clock::now();
         hsa_copy(reg, 0);

@@ -361,7 +361,7 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * fork and join between hardware queues; 0: on the context's high-priority
  * chain stream), copy_engine (rt_render's device -> host copies: 0
  * hipMemcpyAsync, e = 1..16 the device's SDMA engine e - 1 driven directly,
- * -1 the engine the runtime prefers).
+ * -1 its engines 0-3 in turn).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -101,7 +101,9 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // C3 BGR 4.00 -> 3.46-3.63 ms, RGB + BGR 8.09-8.17 -> 7.67-7.72 ms)
     {"copy_engine", 0, -1, 16},                  // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
                                                  // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
-                                                 // (hsa_amd_memory_async_copy_on_engine), -1 the preferred engine
+                                                 // (hsa_amd_memory_async_copy_on_engine), -1 its first four engines in turn
+                                                 // (round 6, same box, 8-way C3 share into a page-locked frame: BGR 1.21 vs
+                                                 // 0.99 ms, RGB + BGR 1.84 vs 1.70 ms with -1; C4 share and whole frames equal)
     {"chain_on_caller", 1, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
                                                  // itself (no fork / join hop between hardware queues at the start and
                                                  // end of the render; the chain then runs at the caller stream's priority;
@@ -283,6 +285,7 @@ struct rt_ctx {
     // the first rt_ctx_stats / rt_ctx_generation_counts after it (flush_tally): not on the chain
     struct PendingTally {
         bool on = false;
+        bool zero = false;                 // the render left the counters to be cleared before the tally
         FrameParams fp{};
         WfBufs b{};
         int n_lights = 0, gens = 0;
@@ -317,14 +320,14 @@ struct rt_ctx {
     size_t h_sp_meta_cap = 0;
     void* h_sp_pk = nullptr;
     size_t h_sp_pk_cap = 0;
-    hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
+    hipEvent_t sp_cam = nullptr, sp_ready = nullptr, cp_done = nullptr;
     static constexpr int kSpRanges = 16;   // row ranges of the packed copy, each scattered as it lands
     hipEvent_t sp_ev[kSpRanges] = {};
     // copies on an SDMA engine (tuning copy_engine): the device's and a CPU agent, the engine, and
     // one completion signal per staging slice / packed range / direct copy batch
     int sdma_state = 0;                    // 0 not set up, 1 usable, -1 unavailable
     hsa_agent_t hsa_gpu{}, hsa_cpu{};
-    uint32_t sdma_avail = 0, sdma_pref = 0;
+    uint32_t sdma_avail = 0, sdma_pref = 0, sdma_turn = 0;
     static constexpr int kSdmaSignals = kRing + kSpRanges + 1;
     hsa_signal_t sdma_sig[kSdmaSignals] = {};
     int64_t tune[kTuneCount];
@@ -622,6 +625,7 @@ void rt_ctx_destroy(rt_ctx* c) {
     for (hipEvent_t e : c->sp_ev) if (e) (void)hipEventDestroy(e);
     if (c->sp_cam) (void)hipEventDestroy(c->sp_cam);
     if (c->sp_ready) (void)hipEventDestroy(c->sp_ready);
+    if (c->cp_done) (void)hipEventDestroy(c->cp_done);
     if (c->d_sp) (void)hipFree(c->d_sp);
     if (c->sdma_state == 1) {
         for (hsa_signal_t sg : c->sdma_sig)
@@ -1206,9 +1210,14 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         return fail(c, RT_E_INVALID, "sphere list does not fit in LDS; use RT_ALGO_BRUTE_GLOBAL");
     if ((mode == RT_ALGO_WAVEFRONT || mode == RT_ALGO_WAVEFRONT_BRUTE) && c->dsc.n_lights > 32)
         return fail(c, RT_E_UNSUPPORTED, "the wavefront path handles at most 32 lights");
+    // the statistics counters start at zero: cleared here, or, for a one-chunk wavefront render
+    // without RT_COUNT_WORK (its tally is lazy), by flush_tally just before that tally
+    auto zero_counters = [&]() -> int {
+        HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
+        return RT_OK;
+    };
     if (!dry) {
         c->tally.on = false;
-        HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), st));
         c->last_pixels = static_cast<uint64_t>(o->tile_w) * o->tile_h;
         c->last_stream = st;
         c->last_spp_traced = 1;
@@ -1218,6 +1227,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
     c->sparse_on = false;
     if (dry && (o->tile_w == 0 || o->tile_h == 0)) return warm_streams(c, {st});
     if (o->tile_w == 0 || o->tile_h == 0) {
+        if ((rc = zero_counters()) != RT_OK) return rc;
         c->last_timed = false;
         HIP_TRY(c, hipEventRecord(c->render_done, st));
         c->render_pending = true;
@@ -1429,6 +1439,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             std::fprintf(stderr, "rtamd: chunks %u x %u rows (first %u), lanes %d, G %u, R %u\n", n_chunks, chunk_rows, first_rows,
                          n_lanes, G, R);
         const bool count = (o->flags & RT_COUNT_WORK) != 0;
+        const bool lazy_tally = n_chunks == 1 && n_lanes == 1;
+        if ((!lazy_tally || count) && (rc = zero_counters()) != RT_OK) return rc;
         // per-launch timing needs one in-order stream
         const bool timed = (o->flags & RT_TIME_KERNELS) != 0 && n_lanes == 1;
         LaunchMarks marks, marks_b[kMaxBStreams];
@@ -1486,9 +1498,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;
-            ws.lazy_tally = n_chunks == 1 && n_lanes == 1;
+            ws.lazy_tally = lazy_tally;
             if (ws.lazy_tally) {
                 c->tally.on = true;
+                c->tally.zero = !count;         // (a counted render zeroed them above: its test counts are in them)
                 c->tally.fp = f;
                 c->tally.b = b;
                 c->tally.n_lights = c->dsc.n_lights;
@@ -1544,12 +1557,14 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         }
         ps.mem = static_cast<unsigned char*>(c->d_path);
         if (dry) return warm_streams(c, {st});
+        if ((rc = zero_counters()) != RT_OK) return rc;
         const bool staged = path_lds_bytes(c->dsc, true) <= 48 * 1024;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_path(c->dsc, fp, ps, staged, st));
         HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {
         if (dry) return warm_streams(c, {st});
+        if ((rc = zero_counters()) != RT_OK) return rc;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
         HIP_TRY(c, hipEventRecord(c->ev1, st));
@@ -1618,6 +1633,7 @@ static int flush_tally(rt_ctx* c) {
     if (!c->tally.on) return RT_OK;
     c->tally.on = false;
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->render_done, 0));
+    if (c->tally.zero) HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * sizeof(unsigned long long), c->stream));
     HIP_TRY(c, launch_tally(c->tally.fp, c->tally.b, c->tally.n_lights, c->tally.gens, c->stream));
     return RT_OK;
 }
@@ -1730,17 +1746,17 @@ static bool sdma_setup(rt_ctx* c) {
     return true;
 }
 
-// The engine rt_render's copies use now (0: hipMemcpyAsync).
+// The engines rt_render's copies use now, as a mask taken in turn (0: hipMemcpyAsync).  -1: the
+// device's engines 0-3 (tools/sdma_probe: ~53 GB/s each on MI355X, the PCIe link's rate; engines
+// 4-15 move 7-12.5 GB/s); several in turn hide each copy's fixed cost behind the others' transfers
+// (a rank's 64 row bands of 192 KB: 38 GB/s on four engines, 14 GB/s on one).
 static uint32_t sdma_engine(rt_ctx* c) {
     const int64_t e = c->t(kTuneCopyEngine);
     if (e == 0 || !sdma_setup(c)) return 0;
-    uint32_t bit = 0;
-    if (e > 0) bit = 1u << (e - 1);
-    else {
-        const uint32_t m = (c->sdma_pref & c->sdma_avail) ? (c->sdma_pref & c->sdma_avail) : c->sdma_avail;
-        bit = m & (~m + 1u);
-    }
-    return (bit & c->sdma_avail) ? bit : 0;
+    if (e > 0) return (1u << (e - 1)) & c->sdma_avail;
+    if (c->sdma_avail & 0xFu) return c->sdma_avail & 0xFu;
+    const uint32_t m = (c->sdma_pref & c->sdma_avail) ? (c->sdma_pref & c->sdma_avail) : c->sdma_avail;
+    return m & (~m + 1u);
 }
 
 // Wait until signal `si` is 0 (every copy counted on it done); a copy that has not completed
@@ -1757,10 +1773,16 @@ static int sdma_wait(rt_ctx* c, int si) {
     return RT_OK;
 }
 
-// Device -> pinned host copy on the engine, counted on signal `si` (one more pending copy); the
-// caller waits with sdma_wait.
-static int sdma_copy(rt_ctx* c, uint32_t engine, int si, void* dst, const void* src, size_t bytes) {
+// Device -> pinned host copy on the next engine of `engines` (in turn), counted on signal `si` (one
+// more pending copy); the caller waits with sdma_wait.  Copies on different engines complete in
+// any order: a wait covers exactly the copies counted on its signal.
+static int sdma_copy(rt_ctx* c, uint32_t engines, int si, void* dst, const void* src, size_t bytes) {
     if (!bytes) return RT_OK;
+    uint32_t engine = 0;
+    for (int k = 0; k < 32 && !engine; ++k) {
+        const uint32_t bit = 1u << (c->sdma_turn++ & 31u);
+        if (engines & bit) engine = bit;
+    }
     hsa_signal_t sg = c->sdma_sig[si];
     hsa_signal_add_screlease(sg, 1);
     const hsa_status_t st = hsa_amd_memory_async_copy_on_engine(dst, c->hsa_cpu, src, c->hsa_gpu, bytes, 0, nullptr, sg,
@@ -1771,6 +1793,16 @@ static int sdma_copy(rt_ctx* c, uint32_t engine, int si, void* dst, const void* 
         return fail(c, RT_E_HIP, "hsa_amd_memory_async_copy_on_engine failed (" + std::to_string(st) + ")");
     }
     return RT_OK;
+}
+
+// Wait for an event by polling it: a blocking wait's wake-up costs tens of microseconds, which a
+// frame of a few hundred microseconds notices at every step of its copies.
+static hipError_t spin_wait(hipEvent_t ev) {
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        std::this_thread::yield();
+    }
 }
 
 // Where rt_render puts a device row (RT_OUT_FRAME_ROWS or not): local row j of the tile, dev_pitch
@@ -1801,10 +1833,12 @@ struct OutMap {
 // filling slices ahead while the host pool empties them in order into their
 // host rows.  wait = false (sparse copies): no wait on the bands, the copy
 // stream's order alone (its segment kernels follow the camera pass).
-static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, uint32_t rows, hipEvent_t after = nullptr) {
+static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, uint32_t rows, hipEvent_t after = nullptr,
+                        bool sync = true) {
     if (!rows || !m.row_bytes) return RT_OK;
     int rc = ensure_copy_stream(c);
     if (rc != RT_OK) return rc;
+    if (!c->cp_done) HIP_TRY(c, hipEventCreateWithFlags(&c->cp_done, hipEventDisableTiming));
     const uint32_t engine = sdma_engine(c);          // 0: hipMemcpyAsync on the copy stream
     const auto* s8 = static_cast<const uint8_t*>(src);
     auto* d8 = static_cast<uint8_t*>(dst);
@@ -1839,46 +1873,30 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, 
     auto wait_band = [&](int bi) -> hipError_t {
         return engine ? hipEventSynchronize(band_event(bi)) : hipStreamWaitEvent(c->copy_stream, band_event(bi), 0);
     };
-    if (pinned && engine && contig) {                  // every piece straight into the caller's rows
+    // page-locked destination: every piece straight into the caller's rows, one copy per piece (the
+    // rows of a partial-width tile: one per row), on the engines or the copy stream.  (Not
+    // hipMemcpy2DAsync: a 2D copy of rows whose length is not a multiple of 4 was seen to land
+    // after the stream's later event, tools/copy_stress.py.)
+    if (pinned) {
         constexpr int si = rt_ctx::kSdmaSignals - 1;
         int last = -1;
         for (const Piece& pc : pieces) {
             if (pc.band != last) { HIP_TRY(c, wait_band(pc.band)); last = pc.band; }
-            if ((rc = sdma_copy(c, engine, si, d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch)) != RT_OK)
-                return rc;
-        }
-        return sdma_wait(c, si);
-    }
-    if (pinned) {
-        int last = -1;
-        for (size_t i = 0; i < pieces.size();) {
-            const Piece& pc = pieces[i];
-            if (pc.band != last) {                     // (the rows of a partial-width tile: 2D copies on the stream)
-                HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, band_event(pc.band), 0));
-                last = pc.band;
-            }
-            if (contig) {
-                // a regular run of pieces (a tile's row bands: equal sizes, equal steps on both sides) as
-                // one 2D copy, one piece per row of it
-                size_t k = i + 1;
-                const size_t ds = pieces.size() > i + 1 ? m.host_off(pieces[i + 1].j0) - m.host_off(pc.j0) : 0;
-                while (k < pieces.size() && pieces[k].band == pc.band && pieces[k].n == pc.n &&
-                       pieces[k].j0 == pc.j0 + (k - i) * pc.n && m.host_off(pieces[k].j0) == m.host_off(pc.j0) + (k - i) * ds)
-                    ++k;
-                if (k - i > 1)
-                    HIP_TRY(c, hipMemcpy2DAsync(d8 + m.host_off(pc.j0), ds, s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
-                                                pc.n * m.dev_pitch, k - i, hipMemcpyDeviceToHost, c->copy_stream));
-                else
-                    HIP_TRY(c, hipMemcpyAsync(d8 + m.host_off(pc.j0), s8 + pc.j0 * m.dev_pitch, pc.n * m.dev_pitch,
-                                              hipMemcpyDeviceToHost, c->copy_stream));
-                i = k;
-            } else {
-                HIP_TRY(c, hipMemcpy2DAsync(d8 + m.host_off(pc.j0), m.host_pitch, s8 + pc.j0 * m.dev_pitch, m.dev_pitch,
-                                            m.row_bytes, pc.n, hipMemcpyDeviceToHost, c->copy_stream));
-                ++i;
+            for (uint32_t j = pc.j0; j < pc.j0 + pc.n; j += contig ? pc.n : 1) {
+                void* to = d8 + m.host_off(j);
+                const void* from = s8 + j * m.dev_pitch;
+                const size_t len = contig ? pc.n * m.dev_pitch : m.row_bytes;
+                if (engine) {
+                    if ((rc = sdma_copy(c, engine, si, to, from, len)) != RT_OK) return rc;
+                } else {
+                    HIP_TRY(c, hipMemcpyAsync(to, from, len, hipMemcpyDeviceToHost, c->copy_stream));
+                }
             }
         }
-        HIP_TRY(c, hipStreamSynchronize(c->copy_stream));
+        if (!sync) return RT_OK;
+        if (engine) return sdma_wait(c, si);
+        HIP_TRY(c, hipEventRecord(c->cp_done, c->copy_stream));
+        HIP_TRY(c, spin_wait(c->cp_done));
         return RT_OK;
     }
     if (slice > c->pin_cap) {                      // rows wider than a slice: larger slices
@@ -1914,7 +1932,7 @@ static int copy_to_host(rt_ctx* c, void* dst, const void* src, const OutMap& m, 
         if (engine) {
             if ((rc = sdma_wait(c, slot)) != RT_OK) return rc;
         } else {
-            HIP_TRY(c, hipEventSynchronize(c->pin_ev[slot]));
+            HIP_TRY(c, spin_wait(c->pin_ev[slot]));
         }
         const Piece& pc = pieces[drained];
         const auto* from = static_cast<const uint8_t*>(c->pin[slot]);
@@ -1961,10 +1979,16 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     auto* h_bits = h_off + (rows + 1);
     HIP_TRY(c, hipMemcpyAsync(h_off, c->d_sp_off, s_off, hipMemcpyDeviceToHost, c->copy_stream));
     HIP_TRY(c, hipMemcpyAsync(h_bits, c->d_sp_bits, s_bits, hipMemcpyDeviceToHost, c->copy_stream));
-    // the frame as the camera pass left it (sp_ready: after the segment kernels, which follow the camera pass)
-    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, rows, c->sp_ready)) != RT_OK) return rc;
-    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, rows, c->sp_ready)) != RT_OK) return rc;
-    HIP_TRY(c, hipStreamSynchronize(c->copy_stream));      // (the offsets and bits were queued first)
+    if (!c->cp_done) HIP_TRY(c, hipEventCreateWithFlags(&c->cp_done, hipEventDisableTiming));
+    HIP_TRY(c, hipEventRecord(c->cp_done, c->copy_stream));          // the offsets and bits have landed
+    // the frame as the camera pass left it (sp_ready: after the segment kernels, which follow the camera pass):
+    // into a page-locked frame the copies are only queued here (the packed ranges queue behind them and
+    // the host waits for those), into pageable memory the staging slices are drained as they land
+    const uint32_t engine = sdma_engine(c);
+    if (out_bgr && (rc = copy_to_host(c, out_bgr, c->d_bgr, mb, rows, c->sp_ready, false)) != RT_OK) return rc;
+    if (out_rgb && (rc = copy_to_host(c, out_rgb, c->d_rgb, mr, rows, c->sp_ready, false)) != RT_OK) return rc;
+    const double t_queued = us();
+    HIP_TRY(c, spin_wait(c->cp_done));
     const double t_frame = us();
     const uint64_t total = h_off[rows];
     const size_t seg_b = 3 * kSegPx, seg_r = 3 * kSegPx * sizeof(float);
@@ -1975,10 +1999,12 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     // the packed segments once the render is done: on the copy stream after its end event, or on the
     // engine once the host has seen it, in row ranges, each with its own event / signal
     const hipEvent_t done = c->n_bands > 0 ? c->band_ev[0] : c->render_done;
-    const uint32_t engine = sdma_engine(c);
-    if (engine) HIP_TRY(c, hipEventSynchronize(done));
+    if (engine) HIP_TRY(c, spin_wait(done));
     else HIP_TRY(c, hipStreamWaitEvent(c->copy_stream, done, 0));
-    const int nr = static_cast<int>(std::min<uint32_t>(rt_ctx::kSpRanges, rows));
+    const double t_done = us();
+    // ranges of at least ~2 MB (each copy has a fixed cost of its own), at most kSpRanges
+    const int nr = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>({static_cast<uint64_t>(rt_ctx::kSpRanges), rows,
+                                                                             (pk_b + pk_r + (2u << 20) - 1) / (2u << 20)})));
     auto r_at = [&](int j) { return static_cast<uint32_t>(static_cast<uint64_t>(rows) * j / nr); };
     for (int j = 0; j < nr; ++j) {
         const uint64_t a = h_off[r_at(j)], e = h_off[r_at(j + 1)];
@@ -2019,11 +2045,13 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     };
     // each range scattered by the pool as soon as it has landed (the later ones still in flight)
     double t_first = 0.0;
+    // (engine: the frame's copies were queued on the same engine before the ranges; its signal first)
+    if (engine && (rc = sdma_wait(c, rt_ctx::kSdmaSignals - 1)) != RT_OK) return rc;
     for (int j = 0; j < nr; ++j) {
         if (engine) {
             if ((rc = sdma_wait(c, kRing + j)) != RT_OK) return rc;
         } else {
-            HIP_TRY(c, hipEventSynchronize(c->sp_ev[j]));
+            HIP_TRY(c, spin_wait(c->sp_ev[j]));
         }
         if (j == 0) t_first = us();
         const uint32_t ra = r_at(j), rb = r_at(j + 1);
@@ -2033,9 +2061,10 @@ static int copy_sparse(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
         });
     }
     if (c->t(kTuneVerbose))
-        std::fprintf(stderr, "rtamd: sparse copy: %llu of %llu segments; frame copied at %.0f us, first packed range at %.0f, "
-                     "done at %.0f\n", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nseg) * rows,
-                     t_frame, t_first, us());
+        std::fprintf(stderr, "rtamd: sparse copy: %llu of %llu segments; frame copies queued at %.0f us, offsets in at %.0f, "
+                     "render done seen at %.0f (engine only), first packed range in at %.0f, done at %.0f\n",
+                     static_cast<unsigned long long>(total), static_cast<unsigned long long>(nseg) * rows, t_queued, t_frame,
+                     engine ? t_done : 0.0, t_first, us());
     return RT_OK;
 }
 

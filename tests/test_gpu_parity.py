@@ -862,7 +862,7 @@ def test_sparse_host_copies_large_tile_pinned(gpu_ctx, engine):
         assert np.array_equal(got[0].view(np.uint32), base[0].view(np.uint32)), sparse
 
 
-@pytest.mark.parametrize("sparse,engine", [(1, 0), (0, 0), (1, -1), (0, 1)])
+@pytest.mark.parametrize("sparse,engine", [(1, 0), (0, 0), (1, -1), (0, -1), (1, 1)])
 def test_frame_rows_gather_matches_whole_frame(gpu_ctx, sparse, engine):
     """RT_OUT_FRAME_ROWS (the multi-GPU host gather, main.rs:45-58 split over
     devices): N "ranks" render their 16-row bands straight into one shared
@@ -871,7 +871,9 @@ def test_frame_rows_gather_matches_whole_frame(gpu_ctx, sparse, engine):
     a padded BMP pitch, and a partial-width tile (columns x0.. of the frame):
     the frame equals the whole-frame render bit for bit, and the oracle's.
     engine: the copies through hipMemcpyAsync (0) or an SDMA engine driven
-    directly (tuning copy_engine)."""
+    directly (tuning copy_engine: -1 engines 0-3 in turn, 1 engine 0 alone).
+    Each layout is rendered three times (ordering races between the copies and
+    the host scatter show up on first use, tools/copy_stress.py)."""
     W, H, band = 150, 100, 16
     spec = scenes.config3(W, H)
     gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
@@ -898,25 +900,27 @@ def test_frame_rows_gather_matches_whole_frame(gpu_ctx, sparse, engine):
                 gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
             assert np.array_equal(bgr.arr, whole[1]), (n, pinned)
             assert np.array_equal(rgb.arr.view(np.uint32), whole[0].view(np.uint32)), (n, pinned)
-            # a partial-width tile (columns 40..139 of rows 20..59) lands in its columns; the rest is untouched
-            bgr.arr[...] = 0xAB
-            rgb.arr[...] = np.nan
-            with _with_tuning(gpu_ctx, sparse_out=sparse, copy_engine=engine):
-                o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=40, tile_w=100, y0=20, tile_h=40,
-                                   bgr_pitch=pitch, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
-                gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
-            assert np.array_equal(bgr.arr[20:60, 120:420], whole[1][20:60, 120:420])
-            assert (bgr.arr[20:60, :120] == 0xAB).all() and (bgr.arr[20:60, 420:] == 0xAB).all()
-            assert (bgr.arr[:20] == 0xAB).all() and (bgr.arr[60:] == 0xAB).all()
-            assert np.array_equal(rgb.arr[20:60, 40:140].view(np.uint32), whole[0][20:60, 40:140].view(np.uint32))
-            assert np.isnan(rgb.arr[20:60, :40]).all() and np.isnan(rgb.arr[20:60, 140:]).all()
-            # ... and the tile at the right edge writes the BMP row padding (zero)
-            with _with_tuning(gpu_ctx, sparse_out=sparse, copy_engine=engine):
-                o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=50, tile_w=W - 50, y0=0, tile_h=8,
-                                   bgr_pitch=pitch, flags=lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
-                gpu_ctx.render(o, out=(None, bgr.arr))
-            assert np.array_equal(bgr.arr[:8, 150:], whole[1][:8, 150:])
-            assert (bgr.arr[:8, 3 * W:] == 0).all() and (bgr.arr[:8, :150] == 0xAB).all()
+            for rep in range(3):
+                # a partial-width tile (columns 40..139 of rows 20..59) lands in its columns; the rest is untouched
+                bgr.arr[...] = 0xAB
+                rgb.arr[...] = np.nan
+                with _with_tuning(gpu_ctx, sparse_out=sparse, copy_engine=engine):
+                    o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=40, tile_w=100, y0=20, tile_h=40,
+                                       bgr_pitch=pitch, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                    gpu_ctx.render(o, out=(rgb.arr, bgr.arr))
+                assert np.array_equal(bgr.arr[20:60, 120:420], whole[1][20:60, 120:420]), (n, pinned, rep)
+                assert (bgr.arr[20:60, :120] == 0xAB).all() and (bgr.arr[20:60, 420:] == 0xAB).all()
+                assert (bgr.arr[:20] == 0xAB).all() and (bgr.arr[60:] == 0xAB).all()
+                assert np.array_equal(rgb.arr[20:60, 40:140].view(np.uint32), whole[0][20:60, 40:140].view(np.uint32))
+                assert np.isnan(rgb.arr[20:60, :40]).all() and np.isnan(rgb.arr[20:60, 140:]).all()
+                # ... and the tile at the right edge writes the BMP row padding (zero)
+                bgr.arr[...] = 0xAB
+                with _with_tuning(gpu_ctx, sparse_out=sparse, copy_engine=engine):
+                    o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, x0=50, tile_w=W - 50, y0=0, tile_h=8,
+                                       bgr_pitch=pitch, flags=lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                    gpu_ctx.render(o, out=(None, bgr.arr))
+                assert np.array_equal(bgr.arr[:8, 150:], whole[1][:8, 150:]), (n, pinned, rep)
+                assert (bgr.arr[:8, 3 * W:] == 0).all() and (bgr.arr[:8, :150] == 0xAB).all()
         finally:
             rgb.free()
             bgr.free()

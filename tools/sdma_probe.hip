@@ -148,6 +148,37 @@ int main(int argc, char** argv) {
         std::printf("busy kernel alone %.3f ms; beside hipMemcpyAsync %.3f ms (copy %.3f ms); beside hsa copy %.3f ms "
                     "(copy %.3f ms)\n", alone, with_hip, c1, with_hsa, c2);
     }
+    // a rank's row bands into a shared frame: nb pieces of `pb` bytes, `stride` pieces apart on the host
+    // (8 ranks: every 8th band), through hipMemcpyAsync per piece, one hipMemcpy2DAsync, and engines
+    // driven directly (one, or four round-robin)
+    for (size_t pb : {size_t(196608), size_t(786432), size_t(1572864)}) {
+        const size_t nb = std::min<size_t>(64, bytes / pb / 8), stride = 8 * pb;
+        if (nb < 2) continue;
+        auto t0 = Clock::now();
+        for (size_t b = 0; b < nb; ++b)
+            CK(hipMemcpyAsync(static_cast<char*>(h) + b * stride, static_cast<char*>(d) + b * pb, pb, hipMemcpyDeviceToHost, sc));
+        CK(hipStreamSynchronize(sc));
+        const double t1 = ms_since(t0);
+        t0 = Clock::now();
+        CK(hipMemcpy2DAsync(h, stride, d, pb, pb, nb, hipMemcpyDeviceToHost, sc));
+        CK(hipStreamSynchronize(sc));
+        const double t2 = ms_since(t0);
+        double te[2] = {0, 0};
+        for (int ne : {1, 4}) {
+            t0 = Clock::now();
+            hsa_signal_store_relaxed(sig, static_cast<hsa_signal_value_t>(nb));
+            for (size_t b = 0; b < nb; ++b)
+                HK(hsa_amd_memory_async_copy_on_engine(static_cast<char*>(h) + b * stride, g_cpu, static_cast<char*>(d) + b * pb,
+                                                       g_gpu, pb, 0, nullptr, sig,
+                                                       static_cast<hsa_amd_sdma_engine_id_t>(1u << (b % ne)), true));
+            hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_ACTIVE);
+            te[ne == 4] = ms_since(t0);
+        }
+        const double mbt = nb * pb / 1e6;
+        std::printf("bands %zu x %zu KB: per-piece hipMemcpyAsync %.3f ms (%.1f GB/s), one 2D copy %.3f ms (%.1f GB/s), "
+                    "engine 0 %.3f ms (%.1f GB/s), engines 0-3 %.3f ms (%.1f GB/s)\n", nb, pb >> 10, t1, mbt / t1, t2,
+                    mbt / t2, te[0], mbt / te[0], te[1], mbt / te[1]);
+    }
     // correctness of the hsa copy into registered memory
     CK(hipMemset(d, 7, bytes));
     CK(hipDeviceSynchronize());

@@ -165,8 +165,31 @@ __device__ __forceinline__ double sphere_disc(const DevSphere& s, const Ray& r, 
     return b * b - k.a4 * cc;
 }
 
+#ifndef RT_ROOTS_BF
+#define RT_ROOTS_BF 1        // (round 6: C3 2.912-2.917 vs 2.924-2.930 ms with the branchy form, same box)
+#endif
 __device__ __forceinline__ bool sphere_roots(double b, double disc, const SphK& k, double& t) {
     const double sq = sqrt_win(disc);
+#if RT_ROOTS_BF
+    // both roots' quotients straight-line (div_a2's three operations, whose result for x <= 0 or NaN is
+    // never > 0), the real division only for a positive numerator outside the window (rare)
+    const double x1 = -b - sq, x2 = -b + sq;
+    auto fast = [&](double x) {
+        const double q0 = x * k.ra2;
+        const double e = fma(-k.a2, q0, x);
+        return fma(e, k.ra2, q0);
+    };
+    auto in_win = [&](double x) { return ((static_cast<uint32_t>(__double2hiint(x)) >> 20) & 0x7FFu) - 123u < k.win; };
+    double t1 = fast(x1), t2 = fast(x2);
+    const bool slow1 = x1 > 0.0 && !in_win(x1), slow2 = x2 > 0.0 && !in_win(x2);
+    if (slow1 || slow2) {
+        if (slow1) t1 = x1 / k.a2;
+        if (slow2) t2 = x2 / k.a2;
+    }
+    const bool h1 = t1 > 0.0;
+    t = h1 ? t1 : t2;
+    return h1 || t2 > 0.0;
+#else
     // a2 >= 0 (or NaN): x <= 0 or NaN gives x / a2 <= 0, -0 or NaN, never > 0, so the
     // division is skipped there (a root behind the origin)
     const double x1 = -b - sq;
@@ -180,6 +203,7 @@ __device__ __forceinline__ bool sphere_roots(double b, double disc, const SphK& 
         if (t2 > 0.0) { t = t2; return true; }
     }
     return false;
+#endif
 }
 
 // The exact quadratic; true + the t the reference returns, or false for None.

@@ -1521,8 +1521,10 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
         hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, ws.a, fp, b, sc.n_lights, gens);
         if (ws.ma && (e = ws.ma->mark(ws.a, kKfTally)) != hipSuccess) return e;
     }
+    // the b streams' work joins stream a (with the fused tail only b[0]'s early fold is left: the
+    // tail's launch already waited for every b stream, and none has had work since)
     for (int i = 0; i < ws.nb; ++i) {
-        if (ws.b[i] == ws.a) continue;
+        if (ws.b[i] == ws.a || (ws.tail_fuse > 0 && i > 0)) continue;
         if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
     }

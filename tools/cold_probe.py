@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--host", action="store_true", help="rt_render into pageable host buffers instead of device ones")
     ap.add_argument("--config", default="c3", choices=["c3", "c4"])
     ap.add_argument("--tiny", action="store_true", help="render an 8-row tile first (every kernel launched once)")
+    ap.add_argument("--api", action="store_true", help="host cost per render: enqueue time against wall time")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -64,6 +65,31 @@ def main():
             torch.cuda.synchronize(dev)
         out[f"render{i}"] = time.perf_counter() - t
     print(" ".join(f"{k} {v * 1e3:.3f} ms" for k, v in out.items()), flush=True)
+    if a.api:
+        # host cost per frame: enqueueing K renders back to back (no wait) against their GPU time,
+        # and the HIP calls a render makes that may reach the kernel driver
+        import ctypes as C
+        hip = C.CDLL("libamdhip64.so.7")
+        fr, tot = C.c_size_t(), C.c_size_t()
+        t = time.perf_counter()
+        for _ in range(1000):
+            hip.hipMemGetInfo(C.byref(fr), C.byref(tot))
+        print(f"hipMemGetInfo {(time.perf_counter() - t) * 1e3:.3f} us per call", flush=True)
+        for shard in (1, 8):
+            ob = lr.render_opts(side, side, max_depth=8, spp=1, band=16, band_stride=shard, band_phase=0,
+                                tile_h=side // shard)
+            for _ in range(3):
+                ctx.render_device(ob, rgb.data_ptr(), bgr.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize(dev)
+            K = 50
+            t = time.perf_counter()
+            for _ in range(K):
+                ctx.render_device(ob, rgb.data_ptr(), bgr.data_ptr(), s.cuda_stream)
+            te = time.perf_counter() - t
+            torch.cuda.synchronize(dev)
+            tt = time.perf_counter() - t
+            print(f"share 1/{shard}: enqueue {te / K * 1e3:.3f} ms per render, wall {tt / K * 1e3:.3f} ms per render",
+                  flush=True)
     ctx.close()
 
 

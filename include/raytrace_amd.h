@@ -33,7 +33,9 @@
  *     different contexts may be driven concurrently (one host thread per GPU).
  *   - A context's renders are ordered: each waits (on the device, not the
  *     host) for the context's previous render, whatever streams they were
- *     issued on, because they share the context's working set.
+ *     issued on, because they share the context's working set.  A stream
+ *     passed to rt_render_device must outlive the renders issued on it (a
+ *     render on the same stream as the previous one relies on stream order).
  *     rt_scene_upload waits for every render still reading the old scene.
  *   - Nothing is read from the environment: a render's schedule depends only
  *     on the scene, the options and the context's tuning (rt_ctx_set_tuning).

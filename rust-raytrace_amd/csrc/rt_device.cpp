@@ -239,7 +239,7 @@ struct rt_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr;             // start of the last render (its end: render_done, also a timing event)
     void* d_blob = nullptr;
     size_t blob_bytes = 0;
     DevScene dsc{};
@@ -293,6 +293,7 @@ struct rt_ctx {
     uint32_t scene_spp = 1;           // the uploaded scene's Options.antialias (rt_render_opts.spp = 0)
     hipEvent_t render_done = nullptr; // end of the last render on its stream: the next one waits for it
     bool render_pending = false;
+    hipStream_t done_stream = nullptr;     // the stream render_done was recorded on
     uint32_t last_spp_traced = 1;     // chain schedules trace one of spp identical centre-jitter samples
     uint32_t last_chunks = 0;         // wavefront chunks of the last render (0: other schedules)
     // rt_render: pinned staging slices for the device -> host copy of the outputs, a copy
@@ -588,9 +589,9 @@ int rt_ctx_create(int device, rt_ctx** out) {
     auto cleanup = [&](int rc) { rt_ctx_destroy(c); return rc; };
     if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, RT_E_HIP, "hipSetDevice failed"));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->render_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&c->render_done) != hipSuccess ||
         hipMalloc(&c->d_counters, kCounterWords * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_srgb, 255 * sizeof(double)) != hipSuccess ||
         hipMemcpy(c->d_srgb, srgb_average_table(), 255 * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
@@ -637,7 +638,6 @@ void rt_ctx_destroy(rt_ctx* c) {
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1159,7 +1159,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : c->stream;
     // The context's working sets (counters, wavefront buffers, path stacks) are
     // shared by its renders: a render on another stream waits for the previous one.
-    if (c->render_pending) HIP_TRY(c, hipStreamWaitEvent(st, c->render_done, 0));
+    // (on the stream the previous render ended on, stream order alone suffices)
+    if (c->render_pending && st != c->done_stream) HIP_TRY(c, hipStreamWaitEvent(st, c->render_done, 0));
     FrameParams fp{};
     fp.hw = static_cast<double>(o->width) / 2.0;              // main.rs:39-41
     fp.hh = static_cast<double>(o->height) / 2.0;
@@ -1230,6 +1231,7 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         if ((rc = zero_counters()) != RT_OK) return rc;
         c->last_timed = false;
         HIP_TRY(c, hipEventRecord(c->render_done, st));
+        c->done_stream = st;
         c->render_pending = true;
         return RT_OK;
     }
@@ -1528,7 +1530,6 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             HIP_TRY(c, hipEventRecord(c->lanes[l].done, c->lanes[l].s));
             HIP_TRY(c, hipStreamWaitEvent(st, c->lanes[l].done, 0));
         }
-        HIP_TRY(c, hipEventRecord(c->ev1, st));
         c->wf_used = true;
     } else if (mode == RT_ALGO_PATH) {
         // persistent grid: enough work-items to fill every CU; each owns one
@@ -1561,18 +1562,17 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         const bool staged = path_lds_bytes(c->dsc, true) <= 48 * 1024;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_path(c->dsc, fp, ps, staged, st));
-        HIP_TRY(c, hipEventRecord(c->ev1, st));
     } else {
         if (dry) return warm_streams(c, {st});
         if ((rc = zero_counters()) != RT_OK) return rc;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
-        HIP_TRY(c, hipEventRecord(c->ev1, st));
     }
     // the chain schedules (wavefront, megakernel) trace one camera ray tree per
     // pixel and count it spp times: the spp centre-jitter samples are identical
     if (mode != RT_ALGO_PATH) c->last_spp_traced = spp;
     HIP_TRY(c, hipEventRecord(c->render_done, st));
+    c->done_stream = st;
     c->render_pending = true;
     c->last_timed = true;
     return RT_OK;
@@ -1659,8 +1659,8 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     s->chunks = c->last_chunks;
     if (c->last_timed) {
         float ms = 0.f;
-        HIP_TRY(c, hipEventSynchronize(c->ev1));
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        HIP_TRY(c, hipEventSynchronize(c->render_done));
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->render_done));
         s->kernel_ms = ms;
     }
     return RT_OK;

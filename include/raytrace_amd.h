@@ -61,7 +61,8 @@ extern "C" {
  * lists0, fuse_from, prefix4_kb, cam_prefix_kb, tail_from, tail_max,
  * eager_fold, fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs and
  * shade_wgs (variants measured slower and removed) are gone:
- * rt_ctx_set_tuning answers RT_E_INVALID for them.  rt_stats unchanged (80 B).
+ * rt_ctx_set_tuning answers RT_E_INVALID for them; tuning keys chain_on_caller,
+ * copy_engine and dev_join added.  rt_stats unchanged (80 B).
  * 4: rt_abi_version() added; RT_KF_TAIL (RT_KF_COUNT 8).  A caller checks
  * rt_abi_version() == RT_ABI_VERSION of the header it was built against before
  * passing any struct; any change of a struct, enum value or tuning key bumps it. */
@@ -363,7 +364,10 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * fork and join between hardware queues; 0: on the context's high-priority
  * chain stream), copy_engine (rt_render's device -> host copies: 0
  * hipMemcpyAsync, e = 1..16 the device's SDMA engine e - 1 driven directly,
- * -1 its engines 0-3 in turn).
+ * -1 its engines 0-3 in turn), dev_join (1: the b streams join the chain's
+ * stream on the device, a one-wave kernel polling flags that the b streams set
+ * after their work; 0: through events; a join that waits 2 s gives up and
+ * makes the next rt_ctx_stats fail).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.
  * Unknown key or value out of range -> RT_E_INVALID.  Results never depend on
  * them (tests/test_gpu_parity.py renders under several and compares bits). */

@@ -39,7 +39,7 @@ enum TuneKey : int {
     kTuneStaggerGen, kTuneRegions, kTuneSplit, kTuneBStreams, kTuneCam, kTuneDeal, kTuneSpreadBelow, kTunePathGroup,
     kTuneCuMask, kTunePrio, kTuneVerbose, kTuneGridOcc, kTuneCompact, kTuneHalf, kTuneWfBudgetMb, kTuneCamGridRes,
     kTuneAQueue, kTuneTailFuse, kTuneTailWidth, kTuneQTree, kTuneCompose, kTuneHostChunks, kTuneHostFirst, kTuneSparseOut,
-    kTuneChainOnCaller, kTuneCopyEngine, kTuneCount
+    kTuneChainOnCaller, kTuneCopyEngine, kTuneDevJoin, kTuneCount
 };
 struct TuneDef {
     const char* name;
@@ -108,6 +108,9 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // itself (no fork / join hop between hardware queues at the start and
                                                  // end of the render; the chain then runs at the caller stream's priority;
                                                  // round 6, same box: C3 2.916 vs 2.928 ms, 8-way share 0.706 vs 0.713 ms)
+    {"dev_join", 1, 0, 1},                       // 1: the b streams join the chain's stream on the device (a one-wave
+                                                 // kernel polling a flag the b stream's last kernel is followed by),
+                                                 // 0: through events (a barrier packet on the chain's queue)
 };
 
 }  // namespace
@@ -273,6 +276,8 @@ struct rt_ctx {
         void* mem = nullptr;
         size_t bytes = 0;
         WfBufs b{};
+        uint64_t* dj = nullptr;            // device-side join flags (kDjWords words, zeroed once)
+        uint64_t dj_n = 0;                 // the last join number handed out on them
     };
     std::vector<Lane> lanes;
     // RT_TIME_KERNELS: launch intervals accumulated since the last harvest
@@ -433,6 +438,7 @@ void drop_lanes(rt_ctx* c) {
         for (hipEvent_t e : L.near_done) if (e) (void)hipEventDestroy(e);
         if (L.s) (void)hipStreamDestroy(L.s);
         for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
+        if (L.dj) (void)hipFree(L.dj);
     }
     c->lanes.clear();
 }
@@ -477,6 +483,8 @@ int ensure_lanes(rt_ctx* c, int n) {
         HIP_TRY(c, hipEventCreateWithFlags(&M.done, hipEventDisableTiming));
         M.near_done.assign(kMaxGenerations, nullptr);
         for (hipEvent_t& e : M.near_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&M.dj), kDjWords * sizeof(uint64_t)));
+        HIP_TRY(c, hipMemset(M.dj, 0, kDjWords * sizeof(uint64_t)));
     }
     return RT_OK;
 }
@@ -1500,6 +1508,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
                 ws.tail_wgs = static_cast<int>(std::min<uint32_t>(G, static_cast<uint32_t>(c->n_cu)));
             }
             ws.ma = timed ? &marks : nullptr;
+            if (split && c->t(kTuneDevJoin)) {
+                ws.dj_flags = L.dj;
+                ws.dj_next = &L.dj_n;
+            }
             ws.lazy_tally = lazy_tally;
             if (ws.lazy_tally) {
                 c->tally.on = true;
@@ -1657,6 +1669,12 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     s->pixels = c->last_pixels;
     s->traced_rays = c->last_spp_traced > 1 ? s->rays / c->last_spp_traced : s->rays;
     s->chunks = c->last_chunks;
+    for (const auto& L : c->lanes) {               // a device-side join that gave up (wf_join's 2 s limit)
+        uint64_t err = 0;
+        if (!L.dj) continue;
+        HIP_TRY(c, hipMemcpy(&err, L.dj + kDjError, sizeof err, hipMemcpyDeviceToHost));
+        if (err) return fail(c, RT_E_HIP, "a device-side stream join timed out (tuning dev_join)");
+    }
     if (c->last_timed) {
         float ms = 0.f;
         HIP_TRY(c, hipEventSynchronize(c->render_done));

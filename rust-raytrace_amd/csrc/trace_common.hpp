@@ -165,12 +165,23 @@ __device__ __forceinline__ double sphere_disc(const DevSphere& s, const Ray& r, 
     return b * b - k.a4 * cc;
 }
 
+// kBF: the branch-free form (both quotients straight-line) or the branchy one (a division only
+// for a positive numerator, the second root only when the first is behind).  Round 6, same box:
+// C3 2.912-2.917 vs 2.924-2.930 ms branch-free everywhere, but C5 305.3 vs 294.6 ms and C4 49.46 vs
+// 49.27 ms; the binary16 walk of trees beyond LDS (RT_BF_HALF) takes the branchy form.
 #ifndef RT_ROOTS_BF
-#define RT_ROOTS_BF 1        // (round 6: C3 2.912-2.917 vs 2.924-2.930 ms with the branchy form, same box)
+#define RT_ROOTS_BF 1
 #endif
+#ifndef RT_BF_HALF
+#define RT_BF_HALF 0
+#endif
+#ifndef RT_BF_LDS
+#define RT_BF_LDS 1
+#endif
+template <bool kBF = (RT_ROOTS_BF != 0)>
 __device__ __forceinline__ bool sphere_roots(double b, double disc, const SphK& k, double& t) {
     const double sq = sqrt_win(disc);
-#if RT_ROOTS_BF
+    if constexpr (kBF) {
     // both roots' quotients straight-line (div_a2's three operations, whose result for x <= 0 or NaN is
     // never > 0), the real division only for a positive numerator outside the window (rare)
     const double x1 = -b - sq, x2 = -b + sq;
@@ -189,7 +200,7 @@ __device__ __forceinline__ bool sphere_roots(double b, double disc, const SphK& 
     const bool h1 = t1 > 0.0;
     t = h1 ? t1 : t2;
     return h1 || t2 > 0.0;
-#else
+    } else {
     // a2 >= 0 (or NaN): x <= 0 or NaN gives x / a2 <= 0, -0 or NaN, never > 0, so the
     // division is skipped there (a root behind the origin)
     const double x1 = -b - sq;
@@ -203,14 +214,15 @@ __device__ __forceinline__ bool sphere_roots(double b, double disc, const SphK& 
         if (t2 > 0.0) { t = t2; return true; }
     }
     return false;
-#endif
+    }
 }
 
 // The exact quadratic; true + the t the reference returns, or false for None.
+template <bool kBF = (RT_ROOTS_BF != 0)>
 __device__ __forceinline__ bool sphere_t(const DevSphere& s, const Ray& r, const SphK& k, double& t) {
     double b;
     const double disc = sphere_disc(s, r, k, b);
-    return disc > 0.0 && sphere_roots(b, disc, k, t);
+    return disc > 0.0 && sphere_roots<kBF>(b, disc, k, t);
 }
 
 // shapes.rs:100-112: t = n.(p - o) / n.d ; None iff t <= 0 (a NaN t is a hit).
@@ -763,7 +775,7 @@ __device__ __forceinline__ Hit nearest_bvh_bl(const DevScene& sc, const BvhView&
             for (int k = first; k < first + cnt; ++k) {
                 RT_WSTEP(1);
                 double t;
-                if (sphere_t(v.sph[k], r, sk, t)) {
+                if (sphere_t<kNodes == 3 ? (RT_BF_HALF != 0) : kNodes == 2 ? (RT_BF_LDS != 0) : (RT_ROOTS_BF != 0)>(v.sph[k], r, sk, t)) {
                     const int32_t obj = v.obj[k];
                     if (t < h.t || (t == h.t && obj < h.obj)) {
                         h.t = t; h.obj = obj; h.prim = k;

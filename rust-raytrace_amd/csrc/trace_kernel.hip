@@ -1393,6 +1393,29 @@ hipError_t launch_trace_frame(const DevScene& sc, const FrameParams& fp, int mod
 
 // The shadow queries and the shading of generation k on b stream sb (after its
 // nearest-hit launch).
+// Stream a waits for the work issued so far on the b streams of mask (those that are
+// not stream a itself): through events, or on the device (ws.dj_flags: launch_signal on
+// each, one launch_join on a).
+hipError_t join_b(const WfStreams& ws, uint32_t mask) {
+    hipError_t e;
+    uint32_t m = 0;
+    for (int i = 0; i < ws.nb; ++i)
+        if (((mask >> i) & 1u) && ws.b[i] != ws.a) m |= 1u << i;
+    if (!m) return hipSuccess;
+    if (ws.dj_flags) {
+        const uint64_t n = ++*ws.dj_next;
+        for (int i = 0; i < ws.nb; ++i)
+            if (((m >> i) & 1u) && (e = launch_signal(ws.dj_flags + i, n, ws.b[i])) != hipSuccess) return e;
+        return launch_join(ws.dj_flags, m, n, ws.a);
+    }
+    for (int i = 0; i < ws.nb; ++i) {
+        if (!((m >> i) & 1u)) continue;
+        if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 template <int kSrcO, bool kCount>
 hipError_t launch_shading(const DevScene& sc, const FrameParams& fp, const WfBufs& b, int k, const WfStreams& ws,
                           hipStream_t sb, LaunchMarks* mb) {
@@ -1421,11 +1444,7 @@ hipError_t launch_generation(const DevScene& sc, const FrameParams& fp, const Wf
     if (ws.tail_fuse > 0 && k >= ws.tail_fuse) {      // the fused tail: every generation >= T in one launch
         if (k > ws.tail_fuse) return hipSuccess;
         // the tail folds its chains: the levels of generations <= T-2 (the B streams) must be written
-        for (int i = 0; i < ws.nb; ++i) {
-            if (ws.b[i] == ws.a) continue;
-            if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
-        }
+        if ((e = join_b(ws, (1u << ws.nb) - 1u)) != hipSuccess) return e;
         // the chains that ended by generation T-1, folded on a B stream while the tail runs
         if (ws.b[0] != ws.a) {
             if ((e = hipEventRecord(ws.near_done[k], ws.a)) != hipSuccess) return e;
@@ -1523,11 +1542,7 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
     }
     // the b streams' work joins stream a (with the fused tail only b[0]'s early fold is left: the
     // tail's launch already waited for every b stream, and none has had work since)
-    for (int i = 0; i < ws.nb; ++i) {
-        if (ws.b[i] == ws.a || (ws.tail_fuse > 0 && i > 0)) continue;
-        if ((e = hipEventRecord(ws.b_done[i], ws.b[i])) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ws.a, ws.b_done[i], 0)) != hipSuccess) return e;
-    }
+    if ((e = join_b(ws, ws.tail_fuse > 0 ? 1u : (1u << ws.nb) - 1u)) != hipSuccess) return e;
     // the chains not folded yet (all of them without the fused tail, which folded every chain:
     // its own as it ended them, the others on a B stream)
     if (ws.tail_fuse == 0 && (e = launch_fold(sc, fp, b, ws.a, ws.ma, 0u, kNlevRunning - 1u)) != hipSuccess) return e;
@@ -1549,6 +1564,45 @@ hipError_t launch_wavefront(const DevScene& sc, const FrameParams& fp, const WfB
 
 hipError_t launch_tally(const FrameParams& fp, const WfBufs& b, int n_lights, int generations, hipStream_t s) {
     hipLaunchKernelGGL(wf_tally, dim3(1), dim3(kWfThreads), 0, s, fp, b, n_lights, generations);
+    return hipGetLastError();
+}
+
+// Device-side join of b streams into stream a (WfStreams::dj_flags): a b stream
+// ends its share with wf_signal (one work-item stores the join's number into
+// the stream's flag word once the kernels before it on that stream are done:
+// in-order stream), and stream a runs wf_join, one wave whose lane i polls
+// flag i until it reaches the number.  Instead of an event record on the b
+// stream and a barrier packet on stream a: the cross-queue event wait measured
+// ~50 us between the b stream's last kernel and stream a's next one, a kernel
+// boundary on one queue ~8 us.  Flags only grow (one number per join, from
+// the host), so they need no reset.  A join that has waited kJoinTimeout
+// (100 MHz ticks) gives up and sets the error word (flag 7, reported by
+// rt_ctx_stats): the stream goes on rather than hang the device.
+constexpr uint64_t kJoinTimeout = 200000000ull;      // 2 s
+__global__ __launch_bounds__(64) void wf_signal(uint64_t* flag, uint64_t n) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(64) void wf_join(uint64_t* flags, uint32_t mask, uint64_t n) {
+    const uint32_t i = threadIdx.x;
+    if (i < kDjFlags && ((mask >> i) & 1u)) {
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(&flags[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < n) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > kJoinTimeout) {
+                __hip_atomic_store(&flags[kDjError], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+}
+
+hipError_t launch_signal(uint64_t* flag, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(wf_signal, dim3(1), dim3(64), 0, s, flag, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_join(uint64_t* flags, uint32_t mask, uint64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(wf_join, dim3(1), dim3(64), 0, s, flags, mask, n);
     return hipGetLastError();
 }
 

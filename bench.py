@@ -511,20 +511,32 @@ def main():
     local_rays, local_traced = st.rays, st.traced_rays
     ctx.kernel_times()                     # discard anything recorded before the timed region
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # one context: a pair of HIP events brackets the K renders on their stream (the per-render
+    # device time is the span / K); an event pair per render would put two more marker packets
+    # between consecutive renders, ~10 us each on the device (the frame boundary's idle gap
+    # measured 40 vs ~20 us with them, rocprofv3 kernel trace of an 8-way share)
+    span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)] \
+        if F > 1 else []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if F == 1:
+        span[0].record(stream)
     for i in range(args.steps):
-        evs[i][0].record(streams[i % F])
+        if F > 1:
+            evs[i][0].record(streams[i % F])
         step(i=i)
-        evs[i][1].record(streams[i % F])
+        if F > 1:
+            evs[i][1].record(streams[i % F])
+    if F == 1:
+        span[1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in evs]
+    kernel_ms = [a.elapsed_time(b) for a, b in evs] if F > 1 else [span[0].elapsed_time(span[1]) / args.steps]
     avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
     if F > 1:
         # with frames in flight an event span covers other frames' work too: the roofline's

@@ -62,7 +62,8 @@ extern "C" {
  * eager_fold, fold_split, bmerge, wave_max, tail_fold, tail_shade, fold_wgs and
  * shade_wgs (variants measured slower and removed) are gone:
  * rt_ctx_set_tuning answers RT_E_INVALID for them; tuning keys chain_on_caller,
- * copy_engine and dev_join added.  rt_stats unchanged (80 B).
+ * copy_engine and dev_join added.  rt_stats unchanged (80 B); its kernel_ms is 0
+ * after an rt_render_device without RT_TIME_KERNELS / RT_COUNT_WORK.
  * 4: rt_abi_version() added; RT_KF_TAIL (RT_KF_COUNT 8).  A caller checks
  * rt_abi_version() == RT_ABI_VERSION of the header it was built against before
  * passing any struct; any change of a struct, enum value or tuning key bumps it. */
@@ -262,7 +263,10 @@ typedef struct {
     uint64_t rays;            /* every Scene::intersect query issued (camera + reflection + shadow) */
     uint64_t shadow_rays;
     uint64_t pixels;
-    double kernel_ms;         /* hipEvent time from the first to the last launch of the render */
+    double kernel_ms;         /* hipEvent time from the first to the last launch of the render
+                                 (rt_render, and rt_render_device with RT_TIME_KERNELS or
+                                 RT_COUNT_WORK; 0 for other rt_render_device renders, which
+                                 record no start event: one marker fewer between frames) */
     uint64_t box_tests;       /* RT_COUNT_WORK only: BVH slab tests (2 per inner node visited) */
     uint64_t sphere_tests;    /* RT_COUNT_WORK only: exact ray-sphere quadratics evaluated */
     uint64_t shadow_box_tests, shadow_sphere_tests;   /* the shadow-query share of the two above */

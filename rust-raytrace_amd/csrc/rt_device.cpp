@@ -262,6 +262,11 @@ struct rt_ctx {
     size_t bgr_cap = 0;
     uint64_t last_pixels = 0;
     bool last_timed = false;
+    bool ev0_set = true;                   // ev0 was recorded at the start of the last render
+    // rt_render_device without RT_TIME_KERNELS / RT_COUNT_WORK: no ev0 (rt_stats.kernel_ms 0): the
+    // marker between consecutive renders on the caller's stream cost ~4-6 us of device time per
+    // frame (8-way C3 share 0.655-0.656 vs 0.659-0.662 ms, C3 2.800 vs 2.812 ms, same box)
+    bool skip_ev0 = false;
     hipStream_t last_stream = nullptr;
     // Wavefront lanes: each owns a stream and a working set (grown on demand,
     // kept across renders).  Row chunks of a render are dealt round-robin over
@@ -1464,7 +1469,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         // (high-priority) stream after a fork from the caller's; the b streams need no fork: their
         // first work waits for the chain's generation 0 (near_done), which comes after it
         const bool on_caller = c->t(kTuneChainOnCaller) != 0 && n_lanes == 1;
-        HIP_TRY(c, hipEventRecord(c->ev0, st));
+        c->ev0_set = !c->skip_ev0;
+        if (c->ev0_set) HIP_TRY(c, hipEventRecord(c->ev0, st));
         if (!on_caller) {
             HIP_TRY(c, hipEventRecord(c->fork, st));
             for (int l = 0; l < n_lanes; ++l) HIP_TRY(c, hipStreamWaitEvent(c->lanes[l].s, c->fork, 0));
@@ -1572,11 +1578,13 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
         if (dry) return warm_streams(c, {st});
         if ((rc = zero_counters()) != RT_OK) return rc;
         const bool staged = path_lds_bytes(c->dsc, true) <= 48 * 1024;
+        c->ev0_set = true;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_path(c->dsc, fp, ps, staged, st));
     } else {
         if (dry) return warm_streams(c, {st});
         if ((rc = zero_counters()) != RT_OK) return rc;
+        c->ev0_set = true;
         HIP_TRY(c, hipEventRecord(c->ev0, st));
         HIP_TRY(c, launch_trace_frame(c->dsc, fp, mode, st));
     }
@@ -1592,7 +1600,10 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
 
 int rt_render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* d_bgr, void* stream) {
     if (!c) return RT_E_INVALID;
-    return guarded(c, [&] { return render_device(c, o, d_rgb, d_bgr, stream); });
+    c->skip_ev0 = o && !(o->flags & (RT_TIME_KERNELS | RT_COUNT_WORK));
+    const int rc = guarded(c, [&] { return render_device(c, o, d_rgb, d_bgr, stream); });
+    c->skip_ev0 = false;
+    return rc;
 }
 
 int rt_div_a2_check(rt_ctx* c, const double* x, const double* a, uint32_t n, double* fast, double* slow) {
@@ -1675,7 +1686,7 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
         HIP_TRY(c, hipMemcpy(&err, L.dj + kDjError, sizeof err, hipMemcpyDeviceToHost));
         if (err) return fail(c, RT_E_HIP, "a device-side stream join timed out (tuning dev_join)");
     }
-    if (c->last_timed) {
+    if (c->last_timed && c->ev0_set) {
         float ms = 0.f;
         HIP_TRY(c, hipEventSynchronize(c->render_done));
         HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->render_done));

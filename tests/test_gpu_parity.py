@@ -697,7 +697,8 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(src=25, src_occ=11), dict(prio=0), dict(grid_occ=0), dict(spread_below=1 << 20),
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
                dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
-               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1)]:
+               dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1),
+               dict(dev_join=0), dict(dev_join=0, tail_fuse=0), dict(dev_join=1, tail_fuse=0, bstreams=3)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv
@@ -999,13 +1000,25 @@ streams = [torch.cuda.Stream(dev) for _ in range(2)]
 with lr.Context(0) as ctx:
     ctx.upload(lr.Scene.deserialize(spec.to_text()))
     o = lr.render_opts(128, 128, max_depth=spec.max_depth, spp=1)
-    for _ in range(3):
-        for (a, b), s in zip(outs, streams):
-            ctx.render_device(o, a.data_ptr(), b.data_ptr(), s.cuda_stream)
+    ref = ref64.render(spec)
+    for join in (1, 0):                       # b streams joined on the device / through events
+        ctx.set_tuning("dev_join", join)
+        for t in outs:
+            t[1].fill_(0)
+        for _ in range(3):
+            for (a, b), s in zip(outs, streams):
+                ctx.render_device(o, a.data_ptr(), b.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        for a, b in outs:
+            assert np.array_equal(b.cpu().numpy(), ref["bgr"]), join
+    # a plain rt_render_device records no start event: kernel_ms 0; with RT_TIME_KERNELS it is timed
+    assert ctx.stats().kernel_ms == 0.0
+    ot = lr.render_opts(128, 128, max_depth=spec.max_depth, spp=1,
+                        flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_TIME_KERNELS)
+    ctx.render_device(ot, outs[0][0].data_ptr(), outs[0][1].data_ptr(), streams[0].cuda_stream)
     torch.cuda.synchronize(dev)
-ref = ref64.render(spec)
-for a, b in outs:
-    assert np.array_equal(b.cpu().numpy(), ref["bgr"])
+    assert ctx.stats().kernel_ms > 0.0
+    ctx.kernel_times()
 print("ordered ok")
 """
 

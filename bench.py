@@ -513,8 +513,8 @@ def main():
 
     # one context: a pair of HIP events brackets the K renders on their stream (the per-render
     # device time is the span / K); an event pair per render would put two more marker packets
-    # between consecutive renders, ~10 us each on the device (the frame boundary's idle gap
-    # measured 40 vs ~20 us with them, rocprofv3 kernel trace of an 8-way share)
+    # between consecutive renders on the device (rocprofv3 kernel trace of an 8-way C3 share: the
+    # idle gap at the frame boundary 40 us with them, 32 us without)
     span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)] \
         if F > 1 else []

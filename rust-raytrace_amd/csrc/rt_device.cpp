@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <strings.h>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -343,7 +344,14 @@ struct rt_ctx {
     hsa_signal_t sdma_sig[kSdmaSignals] = {};
     int64_t tune[kTuneCount];
     std::string err;
-    rt_ctx() { for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt; }
+    rt_ctx() {
+        for (int i = 0; i < kTuneCount; ++i) tune[i] = kTune[i].dflt;
+        // a device-side join spins while the b streams finish: it needs their kernels to run beside
+        // it, which kernel serialisation (rocprofv3 --pmc, AMD_SERIALIZE_KERNEL) does not allow (the
+        // join would wait out its 2 s limit): joins through events there
+        auto on = [](const char* v) { return v && *v && std::strcmp(v, "0") != 0 && strcasecmp(v, "false") != 0; };
+        if (on(std::getenv("ROCPROF_COUNTER_COLLECTION")) || on(std::getenv("AMD_SERIALIZE_KERNEL"))) tune[kTuneDevJoin] = 0;
+    }
     int64_t t(TuneKey k) const { return tune[k]; }
 };
 

@@ -1033,3 +1033,33 @@ def test_renders_on_two_streams_are_ordered():
     out = subprocess.run([sys.executable, "-c", _TWO_STREAMS, root, os.path.join(root, "rust-raytrace_amd")],
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0 and "ordered ok" in out.stdout, out.stderr[-3000:]
+
+
+_SERIALISED = r"""
+import sys
+sys.path[:0] = sys.argv[1:3]
+import numpy as np
+import libraytrace as lr
+from libraytrace import scenes
+from oracle import ref64
+spec = scenes.config3(96, 64)
+with lr.Context(0) as ctx:
+    assert ctx.get_tuning("dev_join") == 0
+    ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    rgb, bgr, st = ctx.render(lr.render_opts(96, 64, max_depth=spec.max_depth, spp=1))
+assert np.array_equal(bgr, ref64.render(spec)["bgr"])
+print("serialised ok")
+"""
+
+
+def test_device_join_off_under_kernel_serialisation():
+    """Under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION) the b
+    streams cannot run beside a spinning join kernel: a context created there
+    defaults dev_join to 0 (events), and renders stay exact."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ROCPROF_COUNTER_COLLECTION="1")
+    out = subprocess.run([sys.executable, "-c", _SERIALISED, root, os.path.join(root, "rust-raytrace_amd")],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0 and "serialised ok" in out.stdout, out.stderr[-3000:]

@@ -100,17 +100,34 @@ struct SphK {
     uint32_t win;
 };
 
-__device__ __forceinline__ SphK sphere_k(double a) {
-    SphK k;
-    k.a2 = 2.0 * a;
-    k.a4 = 4.0 * a;
-    double r = __builtin_amdgcn_rcp(k.a2);
-    double e = fma(-k.a2, r, 1.0);
+// Any denominator d (RT_DIVK: the normalisations' three divisions by one length): the same
+// reciprocal and window, and div_by below the same three operations as div_a2 -- which is
+// div_by with d = 2a, so rt_div_a2_check pins both.
+struct DivK {
+    double d, rd;
+    uint32_t win;
+};
+
+__device__ __forceinline__ DivK div_k(double d) {
+    DivK k;
+    k.d = d;
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
     r = fma(r, e, r);
-    e = fma(-k.a2, r, 1.0);
-    k.ra2 = fma(r, e, r);
-    const uint32_t ea = (static_cast<uint32_t>(__double2hiint(k.a2)) >> 20) & 0x7FFu;
-    k.win = ea - 923u < 201u ? 1500u : 0u;
+    e = fma(-d, r, 1.0);
+    k.rd = fma(r, e, r);
+    const uint32_t ed = (static_cast<uint32_t>(__double2hiint(d)) >> 20) & 0x7FFu;
+    k.win = ed - 923u < 201u ? 1500u : 0u;
+    return k;
+}
+
+__device__ __forceinline__ SphK sphere_k(double a) {
+    const DivK d = div_k(2.0 * a);
+    SphK k;
+    k.a2 = d.d;
+    k.a4 = 4.0 * a;
+    k.ra2 = d.rd;
+    k.win = d.win;
     return k;
 }
 
@@ -121,15 +138,17 @@ __device__ __forceinline__ SphK sphere_k(double a) {
 // operand (exponent gap < 768, no denormal quotient or reciprocal, x not tiny)
 // and div_fixup returns q with sign(x), so the three operations below give the
 // division's bits; any other x (0, denormal, huge, inf, NaN) takes the division.
-__device__ __forceinline__ double div_a2(double x, const SphK& k) {
+__device__ __forceinline__ double div_by(double x, const DivK& k) {
     const uint32_t ex = (static_cast<uint32_t>(__double2hiint(x)) >> 20) & 0x7FFu;
     if (ex - 123u < k.win) {
-        const double q0 = x * k.ra2;
-        const double e = fma(-k.a2, q0, x);
-        return fma(e, k.ra2, q0);
+        const double q0 = x * k.rd;
+        const double e = fma(-k.d, q0, x);
+        return fma(e, k.rd, q0);
     }
-    return x / k.a2;
+    return x / k.d;
 }
+
+__device__ __forceinline__ double div_a2(double x, const SphK& k) { return div_by(x, DivK{k.a2, k.ra2, k.win}); }
 
 // sqrt(x) as gfx950's correctly rounded f64 square root computes it (the compiler's
 // sequence: v_rsq_f64 refined by Goldschmidt / Newton steps), without the parts that
@@ -140,6 +159,12 @@ __device__ __forceinline__ double div_a2(double x, const SphK& k) {
 // any other x (tiny, denormal, 0, inf, NaN, negative) takes sqrt().
 #ifndef RT_WSQRT
 #define RT_WSQRT 1
+#endif
+// RT_DIVK: the normalisations (hit normal, light direction, half vector, camera ray) as
+// div_k / div_by and sqrt_win (round 6, same box: C3 2.790 vs 2.806 ms, 8-way share 0.655-0.658
+// vs 0.658-0.662 ms, C4 49.05 vs 49.24 ms, C5 291.0 vs 294.9 ms; exact: the GPU suite is green)
+#ifndef RT_DIVK
+#define RT_DIVK 1
 #endif
 __device__ __forceinline__ double sqrt_win(double x) {
     if (RT_WSQRT && x >= 0x1p-767 && x < __builtin_huge_val()) {
@@ -1191,8 +1216,13 @@ __device__ __forceinline__ void hit_normal(const DevScene& sc, const DevSphere* 
     if (prim >= 0) {
         const DevSphere s = S[prim];
         const double ux = ptx - s.cx, uy = pty - s.cy, uz = ptz - s.cz;
+#if RT_DIVK
+        const DivK l = div_k(sqrt_win(ux * ux + uy * uy + uz * uz));
+        nx = div_by(ux, l); ny = div_by(uy, l); nz = div_by(uz, l);
+#else
         const double l = sqrt(ux * ux + uy * uy + uz * uz);
         nx = ux / l; ny = uy / l; nz = uz / l;
+#endif
     } else {
         const DevPlane& p = sc.planes[~prim];
         nx = p.nx; ny = p.ny; nz = p.nz;
@@ -1205,8 +1235,13 @@ __device__ __forceinline__ bool light_dir(const DevLight& L, double ptx, double 
     if (L.kind == 0) {                       // PointLight
         const double vx = L.v[0] - ptx, vy = L.v[1] - pty, vz = L.v[2] - ptz;
         r2 = vx * vx + vy * vy + vz * vz;    // location.sqdist(pt)
+#if RT_DIVK
+        const DivK l = div_k(sqrt_win(r2));  // == norm of the same vector
+        lx = div_by(vx, l); ly = div_by(vy, l); lz = div_by(vz, l);
+#else
         const double l = sqrt(r2);           // == norm of the same vector
         lx = vx / l; ly = vy / l; lz = vz / l;
+#endif
         return true;
     }
     lx = -L.v[0]; ly = -L.v[1]; lz = -L.v[2];  // DirectionalLight: -direction, not normalised
@@ -1257,8 +1292,13 @@ __device__ __forceinline__ void add_light(Col& res, const DevMaterial& m, const 
     }
     if (specular) {
         const double hx = lx - dx, hy = ly - dy, hz = lz - dz;
+#if RT_DIVK
+        const DivK hl = div_k(sqrt_win(hx * hx + hy * hy + hz * hz));
+        const double c = clamp_zero(nx * div_by(hx, hl) + ny * div_by(hy, hl) + nz * div_by(hz, hl));
+#else
         const double hl = sqrt(hx * hx + hy * hy + hz * hz);
         const double c = clamp_zero(nx * (hx / hl) + ny * (hy / hl) + nz * (hz / hl));
+#endif
         const double p = pow(c, m.exponent);
         res.r = res.r + ((m.ks[0] * L.color[0]) * f) * p;
         res.g = res.g + ((m.ks[1] * L.color[1]) * f) * p;
@@ -1284,8 +1324,13 @@ __device__ __forceinline__ Ray camera_ray(const DevScene& sc, const FrameParams&
     const double dx = M[0] * px + M[1] * py + M[2] * 1.0;
     const double dy = M[3] * px + M[4] * py + M[5] * 1.0;
     const double dz = M[6] * px + M[7] * py + M[8] * 1.0;
+#if RT_DIVK
+    const DivK l = div_k(sqrt_win(dx * dx + dy * dy + dz * dz));
+    return Ray{sc.cam_pos[0], sc.cam_pos[1], sc.cam_pos[2], div_by(dx, l), div_by(dy, l), div_by(dz, l)};
+#else
     const double l = sqrt(dx * dx + dy * dy + dz * dz);
     return Ray{sc.cam_pos[0], sc.cam_pos[1], sc.cam_pos[2], dx / l, dy / l, dz / l};
+#endif
 }
 
 // Mirror direction and the offset origin of raytrace.rs:60-62.

@@ -100,19 +100,43 @@ constexpr TuneDef kTune[kTuneCount] = {
     {"sparse_out", 1, 0, 1},                     // rt_render into host memory, one chunk: copy the frame after the camera
                                                  // pass, then only the 16-pixel segments holding chain pixels (§3.11;
                                                  // C3 BGR 4.00 -> 3.46-3.63 ms, RGB + BGR 8.09-8.17 -> 7.67-7.72 ms)
-    {"copy_engine", 0, -1, 16},                  // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
-                                                 // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
-                                                 // (hsa_amd_memory_async_copy_on_engine), -1 its first four engines in turn
-                                                 // (round 6, same box, 8-way C3 share into a page-locked frame: BGR 1.21 vs
-                                                 // 0.99 ms, RGB + BGR 1.84 vs 1.70 ms with -1; C4 share and whole frames equal)
     {"chain_on_caller", 1, 0, 1},                // 1: a one-lane render's nearest-hit chain runs on the caller's stream
                                                  // itself (no fork / join hop between hardware queues at the start and
                                                  // end of the render; the chain then runs at the caller stream's priority;
-                                                 // round 6, same box: C3 2.916 vs 2.928 ms, 8-way share 0.706 vs 0.713 ms)
+                                                 // round 6, same box: 8-way C3 share 0.632-0.633 vs 0.650-0.657 ms, 4-way
+                                                 // 0.899 vs 0.926 ms, C3 2.767-2.779 vs 2.788-2.790 ms, C4 equal)
+    {"copy_engine", -1, -1, 16},                 // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
+                                                 // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
+                                                 // (hsa_amd_memory_async_copy_on_engine), -1 its first four engines in turn
+                                                 // (default -1; round 6, same box, C3 8-way share into a page-locked frame:
+                                                 // RGB + BGR 1.34 vs 1.79 ms (0), C4 share BGR 7.39 vs 8.29 ms)
     {"dev_join", 1, 0, 1},                       // 1: the b streams join the chain's stream on the device (a one-wave
                                                  // kernel polling a flag the b stream's last kernel is followed by),
                                                  // 0: through events (a barrier packet on the chain's queue)
 };
+
+// The table must follow the enum (a key set by name is read through its enum index): checked
+// at compile time for every key.
+constexpr bool same_name(const char* a, const char* b) { return *a == *b && (*a == 0 || same_name(a + 1, b + 1)); }
+static_assert(same_name(kTune[kTuneChunkPixels].name, "chunk_pixels") && same_name(kTune[kTuneBvhLeaf].name, "bvh_leaf") &&
+              same_name(kTune[kTuneLgrid].name, "light_grids") && same_name(kTune[kTuneLgridRes].name, "light_grid_res") &&
+              same_name(kTune[kTuneSrc].name, "src") && same_name(kTune[kTuneSrcOcc].name, "src_occ") &&
+              same_name(kTune[kTunePrefixKb2].name, "prefix_kb") && same_name(kTune[kTuneLanes].name, "lanes") &&
+              same_name(kTune[kTuneStaggerGen].name, "stagger_gen") && same_name(kTune[kTuneRegions].name, "regions") &&
+              same_name(kTune[kTuneSplit].name, "split") && same_name(kTune[kTuneBStreams].name, "bstreams") &&
+              same_name(kTune[kTuneCam].name, "cam") && same_name(kTune[kTuneDeal].name, "deal") &&
+              same_name(kTune[kTuneSpreadBelow].name, "spread_below") && same_name(kTune[kTunePathGroup].name, "path_group") &&
+              same_name(kTune[kTuneCuMask].name, "cu_mask") && same_name(kTune[kTunePrio].name, "prio") &&
+              same_name(kTune[kTuneVerbose].name, "verbose") && same_name(kTune[kTuneGridOcc].name, "grid_occ") &&
+              same_name(kTune[kTuneCompact].name, "compact_stack") && same_name(kTune[kTuneHalf].name, "half_nodes") &&
+              same_name(kTune[kTuneWfBudgetMb].name, "wf_budget_mb") && same_name(kTune[kTuneCamGridRes].name, "cam_grid_res") &&
+              same_name(kTune[kTuneAQueue].name, "a_queue") && same_name(kTune[kTuneTailFuse].name, "tail_fuse") &&
+              same_name(kTune[kTuneTailWidth].name, "tail_width") && same_name(kTune[kTuneQTree].name, "qtree") &&
+              same_name(kTune[kTuneCompose].name, "compose") && same_name(kTune[kTuneHostChunks].name, "host_chunks") &&
+              same_name(kTune[kTuneHostFirst].name, "host_first") && same_name(kTune[kTuneSparseOut].name, "sparse_out") &&
+              same_name(kTune[kTuneChainOnCaller].name, "chain_on_caller") &&
+              same_name(kTune[kTuneCopyEngine].name, "copy_engine") && same_name(kTune[kTuneDevJoin].name, "dev_join"),
+              "kTune[] out of step with TuneKey");
 
 }  // namespace
 

@@ -698,7 +698,8 @@ def test_tuning_knobs_do_not_change_results(gpu_ctx):
                dict(tail_fuse=1), dict(tail_fuse=3, regions=96), dict(tail_fuse=5, bstreams=1), dict(tail_fuse=2, deal=0),
                dict(tail_fuse=4, tail_width=64), dict(tail_fuse=6, tail_width=7), dict(tail_fuse=3, split=0),
                dict(compose=0), dict(compose=0, tail_fuse=3), dict(compose=0, cam=0), dict(compose=1),
-               dict(dev_join=0), dict(dev_join=0, tail_fuse=0), dict(dev_join=1, tail_fuse=0, bstreams=3)]:
+               dict(dev_join=0), dict(dev_join=0, tail_fuse=0), dict(dev_join=1, tail_fuse=0, bstreams=3),
+               dict(chain_on_caller=0), dict(chain_on_caller=0, dev_join=0), dict(copy_engine=0), dict(copy_engine=1)]:
         with _with_tuning(gpu_ctx, **kv):
             got = gpu_render(gpu_ctx, spec, lr.RT_ALGO_WAVEFRONT)
         assert np.array_equal(got[1], base[1]), kv

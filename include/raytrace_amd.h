@@ -368,8 +368,9 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * fork and join between hardware queues; 0: on the context's high-priority
  * chain stream), copy_engine (rt_render's device -> host copies: 0
  * hipMemcpyAsync, e = 1..16 the device's SDMA engine e - 1 driven directly,
- * -1 (default) its engines 0-3 in turn; a device without usable engines
- * takes hipMemcpyAsync), dev_join (1: the b streams join the chain's
+ * -1 its engines 0-3 in turn, -2 (default) -1 for a row-banded tile
+ * (band_stride > 1) and 0 otherwise; a device without usable engines takes
+ * hipMemcpyAsync), dev_join (1: the b streams join the chain's
  * stream on the device, a one-wave kernel polling flags that the b streams set
  * after their work; 0: through events; a join that waits 2 s gives up and
  * makes the next rt_ctx_stats fail; the default is 0 in a process whose

@@ -105,11 +105,13 @@ constexpr TuneDef kTune[kTuneCount] = {
                                                  // end of the render; the chain then runs at the caller stream's priority;
                                                  // round 6, same box: 8-way C3 share 0.632-0.633 vs 0.650-0.657 ms, 4-way
                                                  // 0.899 vs 0.926 ms, C3 2.767-2.779 vs 2.788-2.790 ms, C4 equal)
-    {"copy_engine", -1, -1, 16},                 // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
+    {"copy_engine", -2, -2, 16},                 // rt_render's device -> host copies of the frame: 0 hipMemcpyAsync on the
                                                  // copy stream, e (1..16) the device's SDMA engine e - 1 driven directly
-                                                 // (hsa_amd_memory_async_copy_on_engine), -1 its first four engines in turn
-                                                 // (default -1; round 6, same box, C3 8-way share into a page-locked frame:
-                                                 // RGB + BGR 1.34 vs 1.79 ms (0), C4 share BGR 7.39 vs 8.29 ms)
+                                                 // (hsa_amd_memory_async_copy_on_engine), -1 its first four engines in turn,
+                                                 // -2 (default) -1 for a row-banded tile (a rank's share: band_stride > 1),
+                                                 // 0 otherwise (round 6, same box: C3 8-way share into a page-locked frame
+                                                 // BGR 1.02 vs 1.35 ms, RGB + BGR 1.43 vs 1.74 ms with -1; C4 share BGR 7.36
+                                                 // vs 8.28 ms; the whole C3 frame BGR 3.65 vs 3.80 ms with 0)
     {"dev_join", 1, 0, 1},                       // 1: the b streams join the chain's stream on the device (a one-wave
                                                  // kernel polling a flag the b stream's last kernel is followed by),
                                                  // 0: through events (a barrier packet on the chain's queue)
@@ -362,6 +364,7 @@ struct rt_ctx {
     // copies on an SDMA engine (tuning copy_engine): the device's and a CPU agent, the engine, and
     // one completion signal per staging slice / packed range / direct copy batch
     int sdma_state = 0;                    // 0 not set up, 1 usable, -1 unavailable
+    bool copy_banded = false;              // the rt_render under way writes a row-banded tile (copy_engine -2)
     hsa_agent_t hsa_gpu{}, hsa_cpu{};
     uint32_t sdma_avail = 0, sdma_pref = 0, sdma_turn = 0;
     static constexpr int kSdmaSignals = kRing + kSpRanges + 1;
@@ -1812,7 +1815,8 @@ static bool sdma_setup(rt_ctx* c) {
 // 4-15 move 7-12.5 GB/s); several in turn hide each copy's fixed cost behind the others' transfers
 // (a rank's 64 row bands of 192 KB: 38 GB/s on four engines, 14 GB/s on one).
 static uint32_t sdma_engine(rt_ctx* c) {
-    const int64_t e = c->t(kTuneCopyEngine);
+    int64_t e = c->t(kTuneCopyEngine);
+    if (e == -2) e = c->copy_banded ? -1 : 0;
     if (e == 0 || !sdma_setup(c)) return 0;
     if (e > 0) return (1u << (e - 1)) & c->sdma_avail;
     if (c->sdma_avail & 0xFu) return c->sdma_avail & 0xFu;
@@ -2185,6 +2189,7 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     OutMap mr, mb;
     uint32_t dev_pitch = pitch;
     if ((rc = host_layout(c, o, pitch, mr, mb, &dev_pitch)) != RT_OK) return rc;
+    c->copy_banded = stride > 1;
     rt_render_opts oo = *o;
     oo.flags = (o->flags & ~(RT_OUT_RGB_F32 | RT_OUT_BGR_U8 | RT_OUT_FRAME_ROWS)) | (out_rgb ? RT_OUT_RGB_F32 : 0) |
                (out_bgr ? RT_OUT_BGR_U8 : 0);
@@ -2231,6 +2236,7 @@ static int reserve(rt_ctx* c, const rt_render_opts* o, int host, void* stream) {
     OutMap mr, mb;
     uint32_t dev_pitch = pitch;
     if ((rc = host_layout(c, o, pitch, mr, mb, &dev_pitch)) != RT_OK) return rc;
+    c->copy_banded = stride > 1;
     oo.flags &= ~RT_OUT_FRAME_ROWS;
     oo.bgr_pitch = dev_pitch;
     const bool rgb = (o->flags & RT_OUT_RGB_F32) != 0, bgr = (o->flags & RT_OUT_BGR_U8) != 0;

@@ -884,7 +884,7 @@ def test_frame_rows_gather_matches_whole_frame(gpu_ctx, sparse, engine):
     ref = ref64.render(spec)
     assert np.array_equal(whole[1][:, :3 * W], ref["bgr"])
     full = H // band
-    for n, pinned in [(3, True), (2, False), (1, True)]:
+    for n, pinned in [(3, True), (2, False), (1, True), (2, True)]:
         mk = (lambda s, d, f: _Pinned(s, d, f)) if pinned else (lambda s, d, f: type("A", (), {
             "arr": np.full(s, f, d), "free": lambda self: None})())
         rgb, bgr = mk((H, W, 3), np.float32, np.nan), mk((H, pitch), np.uint8, 0xAB)
@@ -1064,3 +1064,39 @@ def test_device_join_off_under_kernel_serialisation():
     out = subprocess.run([sys.executable, "-c", _SERIALISED, root, os.path.join(root, "rust-raytrace_amd")],
                          capture_output=True, text=True, timeout=240, env=env)
     assert out.returncode == 0 and "serialised ok" in out.stdout, out.stderr[-3000:]
+
+
+@pytest.mark.parametrize("engine", [-2, -1, 0])
+def test_frame_rows_into_registered_frame(gpu_ctx, engine):
+    """bench.py's multi-GPU frame: ordinary host memory page-locked with
+    hipHostRegister, every "rank" of 4 writing its full-width 16-row bands (a
+    ragged last band included) through the SDMA engines (copy_engine -2, the
+    default for banded tiles, and -1) or hipMemcpyAsync (0): the whole-frame
+    render bit for bit, with and without the sparse copies."""
+    import ctypes as C
+    W, H, band, n = 128, 136, 16, 4
+    spec = scenes.config3(W, H)
+    gpu_ctx.upload(lr.Scene.deserialize(spec.to_text()))
+    whole = gpu_ctx.render(lr.render_opts(W, H, max_depth=spec.max_depth, spp=1))
+    hip = _hip()
+    rgb = np.full((H, W, 3), np.nan, np.float32)
+    bgr = np.full((H, 3 * W), 0xAB, np.uint8)
+    for a in (rgb, bgr):
+        assert hip.hipHostRegister(C.c_void_p(a.ctypes.data), C.c_size_t(a.nbytes), 0) == 0
+    try:
+        for sparse in (1, 0):
+            rgb[...] = np.nan
+            bgr[...] = 0xAB
+            with _with_tuning(gpu_ctx, sparse_out=sparse, copy_engine=engine):
+                nbands = (H + band - 1) // band
+                for r in range(n):
+                    idx = list(range(r, nbands, n))
+                    rows = sum(min(band, H - q * band) for q in idx)
+                    o = lr.render_opts(W, H, max_depth=spec.max_depth, spp=1, band=band, band_stride=n, band_phase=r,
+                                       tile_h=rows, flags=lr.RT_OUT_RGB_F32 | lr.RT_OUT_BGR_U8 | lr.RT_OUT_FRAME_ROWS)
+                    gpu_ctx.render(o, out=(rgb, bgr))
+            assert np.array_equal(bgr, whole[1]), sparse
+            assert np.array_equal(rgb.view(np.uint32), whole[0].view(np.uint32)), sparse
+    finally:
+        for a in (rgb, bgr):
+            hip.hipHostUnregister(C.c_void_p(a.ctypes.data))

@@ -373,7 +373,7 @@ int rt_ctx_kernel_times(rt_ctx* ctx, double* ms, uint32_t* launches, int n);
  * hipMemcpyAsync), dev_join (1: the b streams join the chain's
  * stream on the device, a one-wave kernel polling flags that the b streams set
  * after their work; 0: through events; a join that waits 2 s gives up and
- * makes the next rt_ctx_stats fail; the default is 0 in a process whose
+ * makes the next rt_render or rt_ctx_stats fail; the default is 0 in a process whose
  * kernels are serialised, ROCPROF_COUNTER_COLLECTION or AMD_SERIALIZE_KERNEL
  * set, where the b streams could not run beside the join).
  * cu_mask, prio and a_queue rebuild the context's streams (after pending work) when changed.

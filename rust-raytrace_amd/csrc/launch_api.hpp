@@ -88,6 +88,7 @@ struct WfStreams {
     // advanced per join).  Null: events.
     uint64_t* dj_flags = nullptr;
     uint64_t* dj_next = nullptr;
+    uint64_t* dj_err = nullptr;         // device address of the lane's page-locked error word
     hipStream_t sp_s = nullptr;
     hipEvent_t sp_cam = nullptr, sp_ready = nullptr;
     uint32_t *sp_bits = nullptr, *sp_cnt = nullptr, *sp_off = nullptr;
@@ -100,12 +101,12 @@ hipError_t upload_srgb_table(const double* avg255);
 // wf_tally of one chunk (rays, shadow rays and per-generation queue sizes into b.totals /
 // b.gen_totals) on stream s: what launch_wavefront runs at the end unless ws.lazy_tally.
 hipError_t launch_tally(const FrameParams& fp, const WfBufs& b, int n_lights, int generations, hipStream_t s);
-// Device-side stream join: flag words 0 .. kDjFlags-1 (one per b stream) and the error word
-// kDjError (set when a join gave up after 2 s).  launch_signal stores n into *flag after the
-// stream's earlier work; launch_join waits until flag i >= n for every bit i of mask.
-constexpr int kDjFlags = 4, kDjError = 7, kDjWords = 8;
+// Device-side stream join: flag words 0 .. kDjFlags-1 (one per b stream).  launch_signal stores
+// n into *flag after the stream's earlier work; launch_join waits until flag i >= n for every
+// bit i of mask, or sets *err (a page-locked host word) after 2 s and goes on.
+constexpr int kDjFlags = 4, kDjWords = 8;
 hipError_t launch_signal(uint64_t* flag, uint64_t n, hipStream_t s);
-hipError_t launch_join(uint64_t* flags, uint32_t mask, uint64_t n, hipStream_t s);
+hipError_t launch_join(uint64_t* flags, uint32_t mask, uint64_t n, uint64_t* err, hipStream_t s);
 // Sparse host copies (tuning sparse_out): pixels per row segment; after the camera pass
 // (b.mark set) segbits / rowcnt / rowoff of the chunk's rows (wf_chain_segs + wf_row_scan);
 // after the fold the flagged segments packed in row order (wf_chain_pack).

@@ -310,6 +310,8 @@ struct rt_ctx {
         WfBufs b{};
         uint64_t* dj = nullptr;            // device-side join flags (kDjWords words, zeroed once)
         uint64_t dj_n = 0;                 // the last join number handed out on them
+        uint64_t* dj_err = nullptr;        // page-locked: a join gave up (host address; dj_err_dev the device's)
+        uint64_t* dj_err_dev = nullptr;
     };
     std::vector<Lane> lanes;
     // RT_TIME_KERNELS: launch intervals accumulated since the last harvest
@@ -365,6 +367,7 @@ struct rt_ctx {
     // one completion signal per staging slice / packed range / direct copy batch
     int sdma_state = 0;                    // 0 not set up, 1 usable, -1 unavailable
     bool copy_banded = false;              // the rt_render under way writes a row-banded tile (copy_engine -2)
+    bool dj_used = false;                  // a render joined its streams on the device (check_join_error)
     hsa_agent_t hsa_gpu{}, hsa_cpu{};
     uint32_t sdma_avail = 0, sdma_pref = 0, sdma_turn = 0;
     static constexpr int kSdmaSignals = kRing + kSpRanges + 1;
@@ -479,6 +482,7 @@ void drop_lanes(rt_ctx* c) {
         if (L.s) (void)hipStreamDestroy(L.s);
         for (hipStream_t x : L.sb) if (x) (void)hipStreamDestroy(x);
         if (L.dj) (void)hipFree(L.dj);
+        if (L.dj_err) (void)hipHostFree(L.dj_err);
     }
     c->lanes.clear();
 }
@@ -525,6 +529,9 @@ int ensure_lanes(rt_ctx* c, int n) {
         for (hipEvent_t& e : M.near_done) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&M.dj), kDjWords * sizeof(uint64_t)));
         HIP_TRY(c, hipMemset(M.dj, 0, kDjWords * sizeof(uint64_t)));
+        HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&M.dj_err), sizeof(uint64_t), hipHostMallocMapped));
+        *M.dj_err = 0;
+        HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&M.dj_err_dev), M.dj_err, 0));
     }
     return RT_OK;
 }
@@ -1552,6 +1559,8 @@ static int render_device(rt_ctx* c, const rt_render_opts* o, void* d_rgb, void* 
             if (split && c->t(kTuneDevJoin)) {
                 ws.dj_flags = L.dj;
                 ws.dj_next = &L.dj_n;
+                ws.dj_err = L.dj_err_dev;
+                c->dj_used = true;
             }
             ws.lazy_tally = lazy_tally;
             if (ws.lazy_tally) {
@@ -1696,6 +1705,19 @@ static int flush_tally(rt_ctx* c) {
     return RT_OK;
 }
 
+// A device-side join that gave up (wf_join's 2 s limit) since the last check: reported once (the
+// error word is cleared), by the rt_render whose synchronisation follows it or by rt_ctx_stats.
+// Only contexts whose renders joined on the device have anything to read (c->dj_used).
+static int check_join_error(rt_ctx* c) {
+    if (!c->dj_used) return RT_OK;
+    for (auto& L : c->lanes) {
+        if (!L.dj_err || !__atomic_load_n(L.dj_err, __ATOMIC_ACQUIRE)) continue;
+        __atomic_store_n(L.dj_err, 0ull, __ATOMIC_RELEASE);
+        return fail(c, RT_E_HIP, "a device-side stream join timed out (tuning dev_join): the render's results are not valid");
+    }
+    return RT_OK;
+}
+
 int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     if (!c || !s) return RT_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -1715,12 +1737,7 @@ int rt_ctx_stats(rt_ctx* c, rt_stats* s) {
     s->pixels = c->last_pixels;
     s->traced_rays = c->last_spp_traced > 1 ? s->rays / c->last_spp_traced : s->rays;
     s->chunks = c->last_chunks;
-    for (const auto& L : c->lanes) {               // a device-side join that gave up (wf_join's 2 s limit)
-        uint64_t err = 0;
-        if (!L.dj) continue;
-        HIP_TRY(c, hipMemcpy(&err, L.dj + kDjError, sizeof err, hipMemcpyDeviceToHost));
-        if (err) return fail(c, RT_E_HIP, "a device-side stream join timed out (tuning dev_join)");
-    }
+    if (const int rc = check_join_error(c); rc != RT_OK) return rc;
     if (c->last_timed && c->ev0_set) {
         float ms = 0.f;
         HIP_TRY(c, hipEventSynchronize(c->render_done));
@@ -2212,7 +2229,7 @@ static int render_host(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8
     }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (stats) return rt_ctx_stats(c, stats);
-    return RT_OK;
+    return check_join_error(c);
 }
 
 int rt_render(rt_ctx* c, const rt_render_opts* o, float* out_rgb, uint8_t* out_bgr, rt_stats* stats) {

@@ -1406,7 +1406,7 @@ hipError_t join_b(const WfStreams& ws, uint32_t mask) {
         const uint64_t n = ++*ws.dj_next;
         for (int i = 0; i < ws.nb; ++i)
             if (((m >> i) & 1u) && (e = launch_signal(ws.dj_flags + i, n, ws.b[i])) != hipSuccess) return e;
-        return launch_join(ws.dj_flags, m, n, ws.a);
+        return launch_join(ws.dj_flags, m, n, ws.dj_err, ws.a);
     }
     for (int i = 0; i < ws.nb; ++i) {
         if (!((m >> i) & 1u)) continue;
@@ -1576,20 +1576,21 @@ hipError_t launch_tally(const FrameParams& fp, const WfBufs& b, int n_lights, in
 // ~50 us between the b stream's last kernel and stream a's next one, a kernel
 // boundary on one queue ~8 us.  Flags only grow (one number per join, from
 // the host), so they need no reset.  A join that has waited kJoinTimeout
-// (100 MHz ticks) gives up and sets the error word (flag 7, reported by
-// rt_ctx_stats): the stream goes on rather than hang the device.
+// (100 MHz ticks) gives up and sets the error word (a page-locked host word,
+// reported by the next rt_render or rt_ctx_stats): the stream goes on rather
+// than hang the device.
 constexpr uint64_t kJoinTimeout = 200000000ull;      // 2 s
 __global__ __launch_bounds__(64) void wf_signal(uint64_t* flag, uint64_t n) {
     if (threadIdx.x == 0) __hip_atomic_store(flag, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
-__global__ __launch_bounds__(64) void wf_join(uint64_t* flags, uint32_t mask, uint64_t n) {
+__global__ __launch_bounds__(64) void wf_join(uint64_t* flags, uint32_t mask, uint64_t n, uint64_t* err) {
     const uint32_t i = threadIdx.x;
     if (i < kDjFlags && ((mask >> i) & 1u)) {
         const uint64_t t0 = wall_clock64();
         while (__hip_atomic_load(&flags[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < n) {
             __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > kJoinTimeout) {
-                __hip_atomic_store(&flags[kDjError], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wall_clock64() - t0 > kJoinTimeout) {       // err: a page-locked host word the host reads directly
+                __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
         }
@@ -1601,8 +1602,8 @@ hipError_t launch_signal(uint64_t* flag, uint64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_join(uint64_t* flags, uint32_t mask, uint64_t n, hipStream_t s) {
-    hipLaunchKernelGGL(wf_join, dim3(1), dim3(64), 0, s, flags, mask, n);
+hipError_t launch_join(uint64_t* flags, uint32_t mask, uint64_t n, uint64_t* err, hipStream_t s) {
+    hipLaunchKernelGGL(wf_join, dim3(1), dim3(64), 0, s, flags, mask, n, err);
     return hipGetLastError();
 }
 
